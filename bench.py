@@ -1,0 +1,220 @@
+#!/usr/bin/env python
+"""bench.py -- keyframe-pair GN iterations/s of the MI355X backend (BASELINE.json metric).
+
+One *step* = one ``gauss_newton_calib`` op call on the cfg3 factor graph (BASELINE.json
+configs[2]: 256 keyframe-pair edges incl. 129 loop closures, 128 keyframes, 512x384,
+calib.yaml parameters) with ``max_iter = 10`` and ``delta_thresh = 0`` so exactly 10 GN
+iterations run.  Throughput = 256 pairs x 10 iterations x steps / time.
+Inputs are synthetic (m3s.synth, fixed seed) and resident in HBM before timing.
+
+N > 1 (torchrun, one process per GPU): the SAME graph is edge-sharded across ranks and the
+per-iteration compact Hessian is summed with an RCCL all-reduce inside the op -> strong
+scaling; value = total pair-iterations / max-over-ranks wall time.
+
+Extra fields: ``roofline`` for the dominant kernel (the accumulate kernel, HBM-bound,
+45 algorithmic bytes per directed point-edge, timed with HIP events on its stream during
+the timed steps) and ``cpu_baseline`` (the CPU oracle -- a restatement of the reference
+backend, which has no CPU implementation -- on a bounded sample, rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mast3r-slam_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "keyframe-pair GN iters/sec @512×384, 256 edges; ATE-RMSE vs ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_POINT_EDGE = 45  # Xj 12 + Xi 12 + Cj 4 + Ci 4 + Q 4 + idx 8 + valid 1
+LOCAL = dict(sigma_ray=0.003, sigma_dist=10.0, sigma_pixel=1.0, sigma_depth=10.0, sigma_point=0.05,
+             C_conf=0.0, Q_conf=1.5, pixel_border=-10, depth_eps=1e-6)  # base.yaml:35-50
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg3", choices=["cfg1", "cfg2", "cfg3", "cfg4"])
+    ap.add_argument("--iters", type=int, default=None, help="GN iterations per op call")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "accum_traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    import mast3r_slam_backends as mb
+    from m3s import synth
+    from m3s.dist import RcclComm, gauss_newton_sharded, shard_range
+    from m3s.geometry import constrain_points_to_ray
+
+    spec = synth.CONFIGS[args.config]
+    mode = spec["mode"]
+    iters = args.iters if args.iters is not None else spec["iters"]
+    E_und = spec["E"]
+    E_dir = 2 * E_und
+    lo, hi = shard_range(E_dir, world, rank)
+    g = synth.make_graph(args.config, device=dev, edge_range=(lo, hi))
+    if mode == "calib":  # solve_GN_calib does this before the op (global_opt.py:172)
+        g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    comm = RcclComm(rank, world, device=dev) if world > 1 else None
+    Twc0 = g.Twc.clone()
+    Twc = g.Twc.clone()
+    L = dict(LOCAL, K=g.K, height=g.H, width=g.W)
+
+    def step():
+        Twc.copy_(Twc0)
+        if world == 1:
+            if mode == "calib":
+                mb.gauss_newton_calib(Twc, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
+                                      L["pixel_border"], L["depth_eps"], L["sigma_pixel"],
+                                      L["sigma_depth"], L["C_conf"], L["Q_conf"], iters, 0.0)
+            else:
+                mb.gauss_newton_rays(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, L["sigma_ray"],
+                                     L["sigma_dist"], L["C_conf"], L["Q_conf"], iters, 0.0)
+        else:
+            gauss_newton_sharded(mode, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, lo, comm,
+                                 iters, 0.0, **L)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    mb.lib.m3s_prof_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    prof = (ctypes.c_double * 4)()
+    nprof = ctypes.c_int(0)
+    mb.lib.m3s_prof_end(prof, ctypes.byref(nprof))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pair_iters = E_und * iters * args.steps
+    value = pair_iters / elapsed
+    n_it = max(nprof.value, 1)
+    acc_ms = prof[0] / n_it
+    bytes_launch = BYTES_PER_POINT_EDGE * g.HW * (hi - lo)
+    achieved = bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
+    traffic = None
+    if os.path.exists(args.traffic_file):
+        try:
+            tf = json.load(open(args.traffic_file))
+            if tf.get("config") == args.config and tf.get("n_gpus", 1) == world:
+                traffic = tf.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "keyframe-pair GN iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (m3s.synth seed 3: shared ray-cast world surface, projective matches)",
+        "config": {
+            "workload": f"{args.config}: gauss_newton_{mode} op call, {E_und} keyframe-pair edges "
+                        f"({E_dir} directed), {spec['N']} keyframes, {g.H}x{g.W}, {iters} GN iters/step, "
+                        f"delta_thresh=0",
+            "edges": E_und,
+            "directed_edges": E_dir,
+            "keyframes": spec["N"],
+            "H": g.H,
+            "W": g.W,
+            "gn_iters_per_step": iters,
+            "parallelism": f"edge-sharded x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+        },
+        "phase_ms_per_iter": {
+            "accumulate": acc_ms,
+            "reduce_compact_allreduce": prof[1] / n_it,
+            "solve": prof[2] / n_it,
+            "retract": prof[3] / n_it,
+        },
+        "roofline": {
+            "kernel": f"gn_accum_kernel<{mode}>",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_launch,
+            "avg_launch_ms": acc_ms,
+        },
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(g, mode, E_und)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(g, mode, E_und):
+    """The CPU oracle (restatement of the reference backend) on a bounded sample: ONE GN
+    iteration of the same graph (all directed edges, full 512x384), OpenMP threads =
+    OMP_NUM_THREADS."""
+    from oracle import oracle as O
+
+    c = lambda t: t.cpu().numpy()
+    if mode == "calib":
+        P = O.make_params("calib", LOCAL["sigma_pixel"], LOCAL["sigma_depth"], LOCAL["C_conf"],
+                          LOCAL["Q_conf"], K=c(g.K), height=g.H, width=g.W,
+                          pixel_border=LOCAL["pixel_border"], z_eps=LOCAL["depth_eps"], max_iter=1,
+                          delta_thresh=0.0)
+    else:
+        P = O.make_params("rays", LOCAL["sigma_ray"], LOCAL["sigma_dist"], LOCAL["C_conf"],
+                          LOCAL["Q_conf"], max_iter=1, delta_thresh=0.0)
+    arrs = [c(g.Twc), c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx), c(g.valid), c(g.Q)]
+    t0 = time.perf_counter()
+    O.gauss_newton(P, *arrs)
+    dt = time.perf_counter() - t0
+    return {
+        "value": E_und * 1 / dt,
+        "unit": "keyframe-pair GN iters/s",
+        "cores": O.num_threads(),
+        "kind": "port",
+        "sample": f"1 GN iteration of the same graph ({E_und} pairs, {2 * E_und} directed edges, "
+                  f"{g.H}x{g.W}) by the C oracle, {dt:.2f} s wall",
+    }
+
+
+if __name__ == "__main__":
+    main()

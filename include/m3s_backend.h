@@ -1,0 +1,171 @@
+/*
+ * m3s_backend.h -- C ABI of the MI355X-native MASt3R-SLAM backend
+ * (dense iterative-projection matching + Sim3 Gauss-Newton).
+ *
+ * This is the drop-in boundary that the Python module `mast3r_slam_backends`
+ * (mast3r-slam_amd/mast3r_slam_backends) binds with ctypes.  Each entry point
+ * replaces one pybind11 op of the reference module
+ * (/root/reference/mast3r_slam/backend/src/gn.cpp:116-123; prototypes gn.h:22-117).
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer to contiguous memory (torch.Tensor.data_ptr()).
+ *     bool tensors are passed as uint8_t (0/1), fp16 as uint16_t bit patterns.
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); all work
+ *     is enqueued on it.  Matching ops are fully asynchronous.  The GN ops perform
+ *     one host synchronisation per call (to plan the sparse system from ii/jj),
+ *     then enqueue all iterations without further host round trips.
+ *   - Return value: M3S_OK (0) or an error code; m3s_last_error() gives a
+ *     thread-local message.  The Python layer raises RuntimeError with it, as the
+ *     reference's TORCH_CHECK does.
+ */
+#ifndef M3S_BACKEND_H
+#define M3S_BACKEND_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    M3S_OK = 0,
+    M3S_ERR_INVALID = 1, /* bad shape / argument */
+    M3S_ERR_HIP = 2,     /* HIP runtime error */
+    M3S_ERR_WORKSPACE = 3,
+    M3S_ERR_COMM = 4
+};
+
+const char* m3s_last_error(void);
+/* Library build identifier ("m3s <version> gfx950"). */
+const char* m3s_version(void);
+
+/*
+ * iter_proj -- replaces iter_proj (gn.cpp:84-99 -> matching_kernels.cu:279-316).
+ *   rays      [B,H,W,9] f32  (ray, d/du, d/dv), H,W >= 3
+ *   pts       [B,N,3]   f32  normalised target rays
+ *   p_init    [B,N,2]   f32  initial (u,v) in image 1
+ *   p_new     [B,N,2]   f32  out
+ *   converged [B,N]     u8   out
+ */
+int m3s_iter_proj(const float* rays, const float* pts, const float* p_init,
+                  float* p_new, uint8_t* converged,
+                  int64_t B, int64_t H, int64_t W, int64_t N,
+                  int max_iter, float lambda_init, float cost_thresh, void* stream);
+
+/*
+ * refine_matches -- replaces refine_matches (gn.cpp:101-114 -> matching_kernels.cu:84-116).
+ *   D11 [B,H,W,F], D21 [B,N,F]  (fp16 bit patterns or f32)
+ *   p1  [B,N,2] i64 (u,v) -> p1_new [B,N,2] i64
+ */
+int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
+                           const int64_t* p1, int64_t* p1_new,
+                           int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
+                           int radius, int dilation_max, void* stream);
+int m3s_refine_matches_f32(const float* D11, const float* D21,
+                           const int64_t* p1, int64_t* p1_new,
+                           int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
+                           int radius, int dilation_max, void* stream);
+
+/* ---------------- Gauss-Newton ---------------- */
+
+enum { M3S_GN_POINTS = 0, M3S_GN_RAYS = 1, M3S_GN_CALIB = 2 };
+
+/*
+ * Common arguments of gauss_newton_{points,rays,calib} (gn.h:22-117).
+ *   Twc   [N,8]  f32  poses [t(3), q(4, xyzw), s], UPDATED IN PLACE (pose 0 pinned)
+ *   Xs    [N,HW,3] f32, Cs [N,HW] f32 (rows ordered by sorted unique keyframe id)
+ *   ii,jj [E_total] i64 GLOBAL keyframe ids of the directed edges
+ *   idx   [E_local,HW] i64, valid [E_local,HW] u8, Q [E_local,HW] f32 for the
+ *         directed edges edge_offset .. edge_offset+E_local-1 (single GPU:
+ *         edge_offset = 0, E_local = E_total)
+ *   dx    [N-1,7] f32 out: the last iteration's update (the op's return value)
+ *   ws    device workspace of >= m3s_gn_workspace_bytes(...) bytes
+ *   comm  NULL, or an m3s communicator: the per-iteration compact Hessian is
+ *         summed over ranks (RCCL all-reduce) before the replicated solve.
+ */
+typedef struct m3s_gn_args {
+    int mode;
+    float* Twc;
+    const float* Xs;
+    const float* Cs;
+    const int64_t* ii;
+    const int64_t* jj;
+    const int64_t* idx;
+    const uint8_t* valid;
+    const float* Q;
+    int64_t N, HW, E_total, E_local, edge_offset;
+    /* residual parameters */
+    float sigma0;           /* sigma_point | sigma_ray | sigma_pixel */
+    float sigma1;           /* -           | sigma_dist | sigma_depth */
+    float C_thresh, Q_thresh;
+    const float* K;         /* calib: device [3,3] f32; fx,fy,cx,cy = K[0][0],K[1][1],K[0][2],K[1][2] */
+    int height, width, pixel_border;
+    float z_eps;
+    int max_iter;
+    float delta_thresh;
+    float* dx;
+    void* ws;
+    size_t ws_bytes;
+    void* comm;
+    void* stream;
+} m3s_gn_args;
+
+size_t m3s_gn_workspace_bytes(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_local);
+
+/* Generic entry: replaces gauss_newton_{points,rays,calib}_cuda
+ * (gn_kernels.cu:725-811, 1140-1228, 1546-1637). */
+int m3s_gauss_newton(const m3s_gn_args* args);
+
+/* Thin positional wrappers with the reference's argument order (gn.h). */
+int m3s_gauss_newton_points(float* Twc, const float* Xs, const float* Cs,
+                            const int64_t* ii, const int64_t* jj, const int64_t* idx,
+                            const uint8_t* valid, const float* Q,
+                            int64_t N, int64_t HW, int64_t E,
+                            float sigma_point, float C_thresh, float Q_thresh,
+                            int max_iter, float delta_thresh,
+                            float* dx, void* ws, size_t ws_bytes, void* stream);
+int m3s_gauss_newton_rays(float* Twc, const float* Xs, const float* Cs,
+                          const int64_t* ii, const int64_t* jj, const int64_t* idx,
+                          const uint8_t* valid, const float* Q,
+                          int64_t N, int64_t HW, int64_t E,
+                          float sigma_ray, float sigma_dist, float C_thresh, float Q_thresh,
+                          int max_iter, float delta_thresh,
+                          float* dx, void* ws, size_t ws_bytes, void* stream);
+int m3s_gauss_newton_calib(float* Twc, const float* Xs, const float* Cs, const float* K,
+                           const int64_t* ii, const int64_t* jj, const int64_t* idx,
+                           const uint8_t* valid, const float* Q,
+                           int64_t N, int64_t HW, int64_t E,
+                           int height, int width, int pixel_border, float z_eps,
+                           float sigma_pixel, float sigma_depth, float C_thresh, float Q_thresh,
+                           int max_iter, float delta_thresh,
+                           float* dx, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * Debug / test entry: run ONE accumulate + assemble pass with the current Twc and
+ * write the dense normal equations H [n,n] and b [n] (n = 7(N-1), f64, host
+ * pointers), i.e. the system SparseBlock builds (gn_kernels.cu:71-113).
+ */
+int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, double* b_host);
+
+/*
+ * Phase timing (bench.py): between m3s_prof_begin() and m3s_prof_end() every GN
+ * iteration records HIP events on its stream.  out[0] = accumulate kernel ms,
+ * out[1] = edge reduce + compact (+ all-reduce) ms, out[2] = solve ms, out[3] = retract
+ * ms, summed over the *n_iter recorded iterations.  Not thread-safe; test/bench only.
+ */
+int m3s_prof_begin(void);
+int m3s_prof_end(double* out /* [4] */, int* n_iter);
+
+/* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
+
+#define M3S_COMM_ID_BYTES 128
+/* rank 0 creates the id, the caller broadcasts it (e.g. torch.distributed) */
+int m3s_comm_get_unique_id(void* id_out /* M3S_COMM_ID_BYTES */);
+int m3s_comm_init(const void* id, int nranks, int rank, void** comm_out);
+int m3s_comm_destroy(void* comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,506 @@
+// gn_driver.hip -- host driver of the Gauss-Newton ops (C ABI in include/m3s_backend.h).
+//
+// Replaces gauss_newton_{points,rays,calib}_cuda (reference gn_kernels.cu:725-811,
+// 1140-1228, 1546-1637) and SparseBlock (:57-159).  Per call:
+//   1. ONE host sync: copy ii/jj (and K) to the host, build the keyframe remap
+//      (unique + searchsorted, :161-170), the block-sparse layout of the pose graph and
+//      the deterministic CSR contribution lists; upload them into the workspace.
+//   2. Enqueue max_iter iterations on the caller's stream with no host round trip:
+//      accumulate -> edge reduce -> compact system [-> RCCL all-reduce] -> dense f64
+//      blocked Cholesky -> retraction.  The ||dx|| < delta_thresh early exit is a device
+//      flag that turns the remaining iterations into no-ops (same result as the
+//      reference's host `break`).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/m3s_backend.h"
+#include "gn_kernels.h"
+#include "m3s_common.h"
+#include "m3s_comm.h"
+
+namespace m3s {
+
+namespace {
+thread_local std::string g_err;
+
+// Optional phase timing with HIP events on the GN stream (bench.py roofline).
+struct Prof {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    std::vector<hipEvent_t> marks;  // per iteration: t0 accum t1 system t2 solve t3 retract t4
+    hipEvent_t get() {
+        if (pool.empty()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            return e;
+        }
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    void mark(hipStream_t st) {
+        if (!on) return;
+        hipEvent_t e = get();
+        if (e && hipEventRecord(e, st) == hipSuccess) marks.push_back(e);
+    }
+};
+Prof g_prof;
+}  // namespace
+
+void set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+const char* get_error() { return g_err.c_str(); }
+
+namespace {
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Number of point chunks per directed edge: enough workgroups to fill 256 CUs several
+// times over, at least 1024 points (one 4-point step of every lane) per workgroup.
+int choose_nchunks(int64_t HW, int64_t E_local) {
+    const int64_t target_wgs = 8192;
+    int64_t nc = (target_wgs + std::max<int64_t>(E_local, 1) - 1) / std::max<int64_t>(E_local, 1);
+    const int64_t max_nc = std::max<int64_t>(1, (HW + 1023) / 1024);
+    nc = std::min(std::max<int64_t>(nc, 1), max_nc);
+    int64_t chunk = align_up((size_t)((HW + nc - 1) / nc), 4);
+    nc = (HW + chunk - 1) / chunk;
+    return (int)std::max<int64_t>(nc, 1);
+}
+
+int chunk_points(int64_t HW, int nchunks) {
+    return (int)align_up((size_t)((HW + nchunks - 1) / nchunks), 4);
+}
+
+struct Layout {
+    size_t partials, edgeblk, compact, dense, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent,
+        grad_ptr, grad_ent, slotmap, total;
+    int nchunks, npad, nblk_max;
+};
+
+Layout make_layout(int64_t N, int64_t HW, int64_t E_total, int64_t E_local) {
+    Layout L{};
+    const int64_t npose = std::max<int64_t>(N - 1, 0);
+    const int64_t n = 7 * npose;
+    L.nchunks = choose_nchunks(HW, E_local);
+    L.npad = (int)std::max<int64_t>(kCholTile, align_up((size_t)n, kCholTile));
+    L.nblk_max = (int)(npose + E_total);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + std::max<size_t>(bytes, 1), 256);
+        return o;
+    };
+    L.partials = take(sizeof(float) * (size_t)E_local * L.nchunks * kNaccPad);
+    L.edgeblk = take(sizeof(double) * (size_t)E_local * kEdgeBlk);
+    L.compact = take(sizeof(double) * ((size_t)L.nblk_max * 28 + (size_t)npose * 7));
+    L.dense = take(sizeof(double) * (size_t)(L.npad + kCholTile) * L.npad);
+    L.x = take(sizeof(double) * (size_t)L.npad);
+    L.flags = take(sizeof(int) * kNumFlags);
+    L.ii_loc = take(sizeof(int) * (size_t)E_local);
+    L.jj_loc = take(sizeof(int) * (size_t)E_local);
+    L.blk_ptr = take(sizeof(int) * ((size_t)L.nblk_max + 1));
+    L.blk_ent = take(sizeof(int) * (size_t)E_local * 4);
+    L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
+    L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
+    L.slotmap = take(sizeof(int) * (size_t)npose * npose);
+    L.total = off;
+    return L;
+}
+
+// Host-side plan of the pose graph (identical on every rank: built from ALL edges).
+struct Plan {
+    int nblk = 0;
+    std::vector<int> ii_loc, jj_loc;              // local edges: Twc/Xs rows
+    std::vector<int> blk_ptr, blk_ent;            // CSR: slot -> (edge<<1 | neg)
+    std::vector<int> grad_ptr, grad_ent;          // CSR: pose -> (edge<<1 | neg)
+    std::vector<int> slotmap;                     // (npose x npose) -> slot or -1
+    float K[4] = {0, 0, 0, 0};
+};
+
+int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
+    const int64_t E = a.E_total;
+    std::vector<int64_t> hii(E), hjj(E);
+    float Kh[9] = {0};
+    if (E > 0) {
+        M3S_HIP_CHECK(hipMemcpyAsync(hii.data(), a.ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
+        M3S_HIP_CHECK(hipMemcpyAsync(hjj.data(), a.jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
+    }
+    if (a.mode == M3S_GN_CALIB)
+        M3S_HIP_CHECK(hipMemcpyAsync(Kh, a.K, sizeof(float) * 9, hipMemcpyDeviceToHost, st));
+    M3S_HIP_CHECK(hipStreamSynchronize(st));
+    plan.K[0] = Kh[0];  // fx = K[0][0]
+    plan.K[1] = Kh[4];  // fy = K[1][1]
+    plan.K[2] = Kh[2];  // cx = K[0][2]
+    plan.K[3] = Kh[5];  // cy = K[1][2]
+
+    // unique(cat(ii, jj)) sorted; searchsorted (gn_kernels.cu:161-170)
+    std::vector<int64_t> u;
+    u.reserve(2 * E);
+    u.insert(u.end(), hii.begin(), hii.end());
+    u.insert(u.end(), hjj.begin(), hjj.end());
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    auto row_of = [&](int64_t id) {
+        return (int64_t)(std::lower_bound(u.begin(), u.end(), id) - u.begin());
+    };
+    M3S_REQUIRE((int64_t)u.size() <= a.N,
+                "gauss_newton: %lld unique keyframe ids in ii/jj but only %lld poses in Twc/Xs",
+                (long long)u.size(), (long long)a.N);
+
+    const int npose = (int)(a.N - 1);
+    std::vector<int> iopt(E), jopt(E);
+    for (int64_t e = 0; e < E; e++) {
+        iopt[e] = (int)row_of(hii[e]) - 1;  // pin = num_fix = 1
+        jopt[e] = (int)row_of(hjj[e]) - 1;
+    }
+
+    // block slots: diagonal blocks first (slot p <-> pose p+1), then unordered pairs in
+    // order of first appearance over ALL edges.
+    std::map<std::pair<int, int>, int> slot_of;
+    plan.nblk = npose;
+    for (int64_t e = 0; e < E; e++) {
+        const int i = iopt[e], j = jopt[e];
+        if (i >= 0 && j >= 0 && i != j) {
+            const auto key = std::make_pair(std::min(i, j), std::max(i, j));
+            if (!slot_of.count(key)) slot_of[key] = plan.nblk++;
+        }
+    }
+    auto slot = [&](int r, int c) -> int {
+        if (r == c) return r;
+        return slot_of.at(std::make_pair(std::min(r, c), std::max(r, c)));
+    };
+
+    // contributions of the LOCAL edges (update_lhs order: (ii,ii,+) (ii,jj,-) (jj,ii,-) (jj,jj,+))
+    std::vector<std::vector<int>> blk_lists(plan.nblk), grad_lists(std::max(npose, 0));
+    plan.ii_loc.resize(a.E_local);
+    plan.jj_loc.resize(a.E_local);
+    for (int64_t el = 0; el < a.E_local; el++) {
+        const int64_t e = a.edge_offset + el;
+        const int i = iopt[e], j = jopt[e];
+        plan.ii_loc[el] = i + 1;
+        plan.jj_loc[el] = j + 1;
+        const int rr[4] = {i, i, j, j}, cc[4] = {i, j, i, j}, neg[4] = {0, 1, 1, 0};
+        for (int b = 0; b < 4; b++) {
+            if (rr[b] >= 0 && cc[b] >= 0 && rr[b] <= cc[b])
+                blk_lists[slot(rr[b], cc[b])].push_back((int)(el << 1) | neg[b]);
+        }
+        if (i >= 0) grad_lists[i].push_back((int)(el << 1) | 1);  // vi = -vj
+        if (j >= 0) grad_lists[j].push_back((int)(el << 1));
+    }
+    plan.blk_ptr.assign(1, 0);
+    for (auto& l : blk_lists) {
+        plan.blk_ent.insert(plan.blk_ent.end(), l.begin(), l.end());
+        plan.blk_ptr.push_back((int)plan.blk_ent.size());
+    }
+    plan.grad_ptr.assign(1, 0);
+    for (auto& l : grad_lists) {
+        plan.grad_ent.insert(plan.grad_ent.end(), l.begin(), l.end());
+        plan.grad_ptr.push_back((int)plan.grad_ent.size());
+    }
+    plan.slotmap.assign((size_t)std::max(npose, 0) * std::max(npose, 0), -1);
+    for (int p = 0; p < npose; p++) plan.slotmap[(size_t)p * npose + p] = p;
+    for (auto& kv : slot_of) {
+        const int r = kv.first.first, c = kv.first.second;
+        plan.slotmap[(size_t)r * npose + c] = kv.second;
+        plan.slotmap[(size_t)c * npose + r] = kv.second;
+    }
+    return M3S_OK;
+}
+
+int validate(const m3s_gn_args& a) {
+    M3S_REQUIRE(a.mode == M3S_GN_POINTS || a.mode == M3S_GN_RAYS || a.mode == M3S_GN_CALIB,
+                "gauss_newton: bad mode %d", a.mode);
+    M3S_REQUIRE(a.N >= 1 && a.HW >= 1, "gauss_newton: need N >= 1 poses and HW >= 1 points");
+    M3S_REQUIRE(a.E_total >= 0 && a.E_local >= 0 && a.edge_offset >= 0 &&
+                    a.edge_offset + a.E_local <= a.E_total,
+                "gauss_newton: bad edge range");
+    M3S_REQUIRE(a.HW < ((int64_t)1 << 31) && a.E_local < (1 << 30),
+                "gauss_newton: sizes exceed int32 indexing");
+    M3S_REQUIRE(a.mode != M3S_GN_CALIB || (a.K != nullptr && a.width > 0 && a.height > 0),
+                "gauss_newton_calib: K / image size required");
+    M3S_REQUIRE(a.Twc && a.Xs && a.Cs && a.dx, "gauss_newton: null pointer");
+    if (a.E_total > 0) M3S_REQUIRE(a.ii && a.jj, "gauss_newton: null ii/jj");
+    if (a.E_local > 0) M3S_REQUIRE(a.idx && a.valid && a.Q, "gauss_newton: null edge data");
+    const size_t need = make_layout(a.N, a.HW, a.E_total, a.E_local).total;
+    M3S_REQUIRE(a.ws != nullptr && a.ws_bytes >= need,
+                "gauss_newton: workspace too small (%zu < %zu bytes)", a.ws_bytes, need);
+    return M3S_OK;
+}
+
+struct Ctx {
+    Layout L;
+    Plan plan;
+    AccParams P;
+    bool vec;
+    char* ws;
+    hipStream_t st;
+    template <typename T>
+    T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
+};
+
+int setup(const m3s_gn_args& a, Ctx& c) {
+    int rc = validate(a);
+    if (rc) return rc;
+    c.st = (hipStream_t)a.stream;
+    c.ws = (char*)a.ws;
+    c.L = make_layout(a.N, a.HW, a.E_total, a.E_local);
+    rc = build_plan(a, c.st, c.plan);
+    if (rc) return rc;
+    const Layout& L = c.L;
+    const Plan& p = c.plan;
+    auto up = [&](size_t off, const std::vector<int>& v) -> hipError_t {
+        if (v.empty()) return hipSuccess;
+        return hipMemcpyAsync(c.ws + off, v.data(), sizeof(int) * v.size(), hipMemcpyHostToDevice, c.st);
+    };
+    M3S_HIP_CHECK(up(L.ii_loc, p.ii_loc));
+    M3S_HIP_CHECK(up(L.jj_loc, p.jj_loc));
+    M3S_HIP_CHECK(up(L.blk_ptr, p.blk_ptr));
+    M3S_HIP_CHECK(up(L.blk_ent, p.blk_ent));
+    M3S_HIP_CHECK(up(L.grad_ptr, p.grad_ptr));
+    M3S_HIP_CHECK(up(L.grad_ent, p.grad_ent));
+    M3S_HIP_CHECK(up(L.slotmap, p.slotmap));
+    M3S_HIP_CHECK(hipMemsetAsync(c.ws + L.flags, 0, sizeof(int) * kNumFlags, c.st));
+    // the host vectors die with this call: wait for the (pageable) uploads
+    M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+
+    AccParams& P = c.P;
+    P.s0_inv = 1.0f / a.sigma0;
+    P.s1_inv = (a.mode == M3S_GN_POINTS) ? 0.0f : 1.0f / a.sigma1;
+    P.C_thresh = a.C_thresh;
+    P.Q_thresh = a.Q_thresh;
+    P.fx = p.K[0];
+    P.fy = p.K[1];
+    P.cx = p.K[2];
+    P.cy = p.K[3];
+    P.pb_lo = (float)a.pixel_border;
+    P.pb_hi_u = (float)(a.width - 1 - a.pixel_border);
+    P.pb_hi_v = (float)(a.height - 1 - a.pixel_border);
+    P.z_eps = a.z_eps;
+    P.width = a.width > 0 ? a.width : 1;
+    P.height = a.height;
+    P.inv_width = 1.0f / (float)P.width;
+    P.HW = (int)a.HW;
+    P.chunk = chunk_points(a.HW, L.nchunks);
+    auto al16 = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
+    c.vec = (a.HW % 4 == 0) && al16(a.Xs) && al16(a.Cs) && al16(a.idx) && al16(a.valid) &&
+            al16(a.Q);
+    return M3S_OK;
+}
+
+// accumulate + edge reduce + compact (+ all-reduce): the system of one iteration
+int enqueue_system(const m3s_gn_args& a, Ctx& c) {
+    const Layout& L = c.L;
+    int* flags = c.at<int>(L.flags);
+    if (a.E_local > 0) {
+        g_prof.mark(c.st);
+        M3S_HIP_CHECK(launch_accum(a.mode, c.vec, dim3(L.nchunks, (unsigned)a.E_local), c.st,
+                                   a.Twc, a.Xs, a.Cs, c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
+                                   a.idx, a.valid, a.Q, c.P, c.at<float>(L.partials), flags));
+        g_prof.mark(c.st);
+        M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
+                                         a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
+    }
+    const int npose = (int)(a.N - 1);
+    M3S_HIP_CHECK(launch_compact(c.st, c.at<double>(L.edgeblk), c.at<int>(L.blk_ptr),
+                                 c.at<int>(L.blk_ent), c.at<int>(L.grad_ptr),
+                                 c.at<int>(L.grad_ent), c.plan.nblk, npose,
+                                 c.at<double>(L.compact), flags));
+    if (a.comm) {
+        const size_t count = (size_t)c.plan.nblk * 28 + (size_t)npose * 7;
+        int rc = comm_allreduce_sum_f64(a.comm, c.at<double>(L.compact), count, c.st);
+        if (rc) return rc;
+    }
+    return M3S_OK;
+}
+
+int run(const m3s_gn_args& a) {
+    Ctx c;
+    int rc = setup(a, c);
+    if (rc) return rc;
+    const int npose = (int)(a.N - 1);
+    if (npose <= 0) return M3S_OK;  // nothing to optimise (all poses pinned)
+    const Layout& L = c.L;
+    int* flags = c.at<int>(L.flags);
+    for (int itr = 0; itr < a.max_iter; itr++) {
+        g_prof.mark(c.st);
+        rc = enqueue_system(a, c);
+        if (rc) return rc;
+        g_prof.mark(c.st);
+        M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.at<int>(L.slotmap),
+                                   c.plan.nblk, npose, 7 * npose, L.npad, c.at<double>(L.dense),
+                                   c.at<double>(L.x), flags));
+        g_prof.mark(c.st);
+        M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
+                                     a.delta_thresh, flags));
+        g_prof.mark(c.st);
+    }
+    return M3S_OK;
+}
+
+}  // namespace
+}  // namespace m3s
+
+using namespace m3s;
+
+extern "C" const char* m3s_last_error(void) { return m3s::get_error(); }
+
+extern "C" const char* m3s_version(void) { return "m3s 0.1.0 gfx950"; }
+
+extern "C" size_t m3s_gn_workspace_bytes(int mode, int64_t N, int64_t HW, int64_t E_total,
+                                         int64_t E_local) {
+    (void)mode;
+    if (N < 1 || HW < 1 || E_total < 0 || E_local < 0) return 0;
+    return make_layout(N, HW, E_total, E_local).total;
+}
+
+extern "C" int m3s_gauss_newton(const m3s_gn_args* args) {
+    if (!args) {
+        set_error("gauss_newton: null args");
+        return M3S_ERR_INVALID;
+    }
+    return run(*args);
+}
+
+extern "C" int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, double* b_host) {
+    if (!args) {
+        set_error("gn_build_system: null args");
+        return M3S_ERR_INVALID;
+    }
+    const m3s_gn_args& a = *args;
+    Ctx c;
+    int rc = setup(a, c);
+    if (rc) return rc;
+    const int npose = (int)(a.N - 1);
+    const int n = 7 * npose;
+    if (npose <= 0) return M3S_OK;
+    rc = enqueue_system(a, c);
+    if (rc) return rc;
+    const Layout& L = c.L;
+    M3S_HIP_CHECK(launch_fill_only(c.st, c.at<double>(L.compact), c.at<int>(L.slotmap), c.plan.nblk,
+                                   npose, n, L.npad, c.at<double>(L.dense), c.at<int>(L.flags)));
+    M3S_HIP_CHECK(hipMemcpy2DAsync(H_host, sizeof(double) * n, c.at<double>(L.dense),
+                                   sizeof(double) * L.npad, sizeof(double) * n, n,
+                                   hipMemcpyDeviceToHost, c.st));
+    M3S_HIP_CHECK(hipMemcpyAsync(b_host, c.at<double>(L.dense) + (size_t)L.npad * L.npad,
+                                 sizeof(double) * n, hipMemcpyDeviceToHost, c.st));
+    M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+    return M3S_OK;
+}
+
+namespace {
+m3s_gn_args base_args(int mode, float* Twc, const float* Xs, const float* Cs, const int64_t* ii,
+                      const int64_t* jj, const int64_t* idx, const uint8_t* valid, const float* Q,
+                      int64_t N, int64_t HW, int64_t E, int max_iter, float delta_thresh,
+                      float* dx, void* ws, size_t ws_bytes, void* stream) {
+    m3s_gn_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.mode = mode;
+    a.Twc = Twc; a.Xs = Xs; a.Cs = Cs; a.ii = ii; a.jj = jj;
+    a.idx = idx; a.valid = valid; a.Q = Q;
+    a.N = N; a.HW = HW; a.E_total = E; a.E_local = E; a.edge_offset = 0;
+    a.max_iter = max_iter; a.delta_thresh = delta_thresh;
+    a.dx = dx; a.ws = ws; a.ws_bytes = ws_bytes; a.stream = stream;
+    return a;
+}
+}  // namespace
+
+extern "C" int m3s_gauss_newton_points(float* Twc, const float* Xs, const float* Cs,
+                                       const int64_t* ii, const int64_t* jj, const int64_t* idx,
+                                       const uint8_t* valid, const float* Q, int64_t N, int64_t HW,
+                                       int64_t E, float sigma_point, float C_thresh,
+                                       float Q_thresh, int max_iter, float delta_thresh,
+                                       float* dx, void* ws, size_t ws_bytes, void* stream) {
+    m3s_gn_args a = base_args(M3S_GN_POINTS, Twc, Xs, Cs, ii, jj, idx, valid, Q, N, HW, E,
+                              max_iter, delta_thresh, dx, ws, ws_bytes, stream);
+    a.sigma0 = sigma_point;
+    a.C_thresh = C_thresh;
+    a.Q_thresh = Q_thresh;
+    return run(a);
+}
+
+extern "C" int m3s_gauss_newton_rays(float* Twc, const float* Xs, const float* Cs,
+                                     const int64_t* ii, const int64_t* jj, const int64_t* idx,
+                                     const uint8_t* valid, const float* Q, int64_t N, int64_t HW,
+                                     int64_t E, float sigma_ray, float sigma_dist, float C_thresh,
+                                     float Q_thresh, int max_iter, float delta_thresh, float* dx,
+                                     void* ws, size_t ws_bytes, void* stream) {
+    m3s_gn_args a = base_args(M3S_GN_RAYS, Twc, Xs, Cs, ii, jj, idx, valid, Q, N, HW, E, max_iter,
+                              delta_thresh, dx, ws, ws_bytes, stream);
+    a.sigma0 = sigma_ray;
+    a.sigma1 = sigma_dist;
+    a.C_thresh = C_thresh;
+    a.Q_thresh = Q_thresh;
+    return run(a);
+}
+
+extern "C" int m3s_gauss_newton_calib(float* Twc, const float* Xs, const float* Cs, const float* K,
+                                      const int64_t* ii, const int64_t* jj, const int64_t* idx,
+                                      const uint8_t* valid, const float* Q, int64_t N, int64_t HW,
+                                      int64_t E, int height, int width, int pixel_border,
+                                      float z_eps, float sigma_pixel, float sigma_depth,
+                                      float C_thresh, float Q_thresh, int max_iter,
+                                      float delta_thresh, float* dx, void* ws, size_t ws_bytes,
+                                      void* stream) {
+    m3s_gn_args a = base_args(M3S_GN_CALIB, Twc, Xs, Cs, ii, jj, idx, valid, Q, N, HW, E,
+                              max_iter, delta_thresh, dx, ws, ws_bytes, stream);
+    a.K = K;
+    a.height = height;
+    a.width = width;
+    a.pixel_border = pixel_border;
+    a.z_eps = z_eps;
+    a.sigma0 = sigma_pixel;
+    a.sigma1 = sigma_depth;
+    a.C_thresh = C_thresh;
+    a.Q_thresh = Q_thresh;
+    return run(a);
+}
+
+// ---- profiling (bench.py): phase times from HIP events on the GN stream ----
+extern "C" int m3s_prof_begin(void) {
+    for (hipEvent_t e : g_prof.marks) g_prof.pool.push_back(e);
+    g_prof.marks.clear();
+    g_prof.on = true;
+    return M3S_OK;
+}
+
+// out[0] accumulate-kernel ms, out[1] edge-reduce/compact/all-reduce ms, out[2] solve ms,
+// out[3] retract ms (sums over iterations); *n_iter = iterations recorded.
+extern "C" int m3s_prof_end(double* out, int* n_iter) {
+    g_prof.on = false;
+    const size_t per = 6;  // t0 [a0 a1] t1 t2 t3 (a0/a1 bracket the accumulate kernel)
+    double acc[4] = {0, 0, 0, 0};
+    int n = 0;
+    for (size_t k = 0; k + per <= g_prof.marks.size(); k += per) {
+        hipEvent_t* m = &g_prof.marks[k];
+        float ms[5];
+        for (int q = 0; q < 5; q++) {
+            M3S_HIP_CHECK(hipEventSynchronize(m[q + 1]));
+            M3S_HIP_CHECK(hipEventElapsedTime(&ms[q], m[q], m[q + 1]));
+        }
+        acc[0] += ms[1];
+        acc[1] += ms[0] + ms[2];
+        acc[2] += ms[3];
+        acc[3] += ms[4];
+        n++;
+    }
+    for (int q = 0; q < 4; q++) out[q] = acc[q];
+    *n_iter = n;
+    for (hipEvent_t e : g_prof.marks) g_prof.pool.push_back(e);
+    g_prof.marks.clear();
+    return M3S_OK;
+}

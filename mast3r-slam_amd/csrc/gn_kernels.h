@@ -1,0 +1,51 @@
+// gn_kernels.h -- shared constants / launcher declarations of the GN kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace m3s {
+
+enum { GN_POINTS = 0, GN_RAYS = 1, GN_CALIB = 2 };
+
+constexpr int kAccThreads = 256;
+constexpr int kNacc = 35;      // 28 (sym 7x7) + 7 (gradient)
+constexpr int kNaccPad = 36;   // partial record stride (floats)
+constexpr int kEdgeBlk = 36;   // per-edge record (doubles): Hjj packed 28 + vj 7 + pad
+constexpr int kCholTile = 64;  // dense Cholesky tile
+
+constexpr int kFlagDone = 0;   // set once ||dx|| < delta_thresh (skips later iterations)
+constexpr int kFlagFail = 1;   // set by the factorisation when a pivot <= 0
+constexpr int kNumFlags = 16;
+
+struct AccParams {
+    float s0_inv, s1_inv;  // 1/sigma0, 1/sigma1
+    float C_thresh, Q_thresh;
+    float fx, fy, cx, cy;
+    float pb_lo, pb_hi_u, pb_hi_v;  // calib border: (pb, W-1-pb, H-1-pb) as float
+    float z_eps;
+    float inv_width;
+    int width, height;
+    int HW;
+    int chunk;  // points per workgroup (multiple of 4)
+};
+
+hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
+                        const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
+                        const int64_t* idx, const uint8_t* valid, const float* Q,
+                        const AccParams& P, float* partials, const int* flags);
+hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
+                              const float* Twc, const int* ii_loc, double* edgeblk,
+                              const int* flags);
+hipError_t launch_compact(hipStream_t st, const double* edgeblk, const int* blk_ptr,
+                          const int* blk_ent, const int* grad_ptr, const int* grad_ent, int nblk,
+                          int npose, double* compact, const int* flags);
+hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
+                        int npose, int n, int npad, double* Hd, double* x, int* flags);
+hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,
+                            int npose, int n, int npad, double* Hd, const int* flags);
+hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
+                          float delta_thresh, int* flags);
+
+}  // namespace m3s

@@ -1,0 +1,717 @@
+// gn_kernels.hip -- MI355X (gfx950) kernels of the Sim3 Gauss-Newton backend.
+//
+// Per GN iteration (driver in gn_driver.cpp):
+//   gn_accum_kernel<MODE>   stream idx/valid/Q + Xs/Cs, accumulate the 28 unique entries of
+//                           M = sum w r r^T and g = sum w e r over RAW (pre-adjoint) Jacobian
+//                           rows.  Replaces ray_align / calib_proj / point_align
+//                           (reference gn_kernels.cu:813-1138, 1231-1543, 455-723).
+//   gn_edge_reduce_kernel   per directed edge: chunk partials summed in f64 (fixed order),
+//                           Hjj = A M A^T, vj = A g with A = the Sim3 adjoint map of
+//                           apply_Sim3_adj_inv (gn_kernels.cu:277-297).  Because
+//                           Ji = -Jj (gn_kernels.cu:1000) the reference's four blocks are
+//                           Hii = Hjj, Hij = Hji = -Hjj, vi = -vj.
+//   gn_compact_kernel       deterministic CSR sum of edge blocks into the compact
+//                           block-sparse system (the RCCL all-reduce payload).
+//   gn_fill_dense_kernel    compact -> dense f64 lower system + RHS border row.
+//   chol_panel / chol_update / back_step   blocked right-looking LL^T in f64 (T = 64),
+//                           SimplicialLLT failure semantics (pivot <= 0 => dx = 0).
+//   gn_retract_kernel       dx = -x, left retraction (gn_kernels.cu:415-453), ||dx|| test.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gn_kernels.h"
+#include "sim3.h"
+
+namespace m3s {
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+
+// Upper-triangle packing of a symmetric 7x7 block: index of (a,b), a <= b.
+__host__ __device__ constexpr int sym_idx(int a, int b) {
+    return a * 7 - a * (a - 1) / 2 + (b - a);
+}
+
+__device__ __forceinline__ float huber_w(float r) {
+    // gn_kernels.cu:172-175 (the 1.345 compare is exact in float)
+    const float r_abs = fabsf(r);
+    return r_abs < 1.345f ? 1.0f : 1.345f * __builtin_amdgcn_rcpf(r_abs);
+}
+
+// Accumulate one raw Jacobian row r (compile-time nonzero mask) with weight w, residual e.
+template <int MASK>
+__device__ __forceinline__ void acc_row(float* __restrict__ acc, const float* r, float w, float e) {
+    float wr[7];
+#pragma unroll
+    for (int a = 0; a < 7; a++) wr[a] = (MASK >> a & 1) ? w * r[a] : 0.0f;
+#pragma unroll
+    for (int a = 0; a < 7; a++) {
+        if (!(MASK >> a & 1)) continue;
+#pragma unroll
+        for (int b = a; b < 7; b++) {
+            if (!(MASK >> b & 1)) continue;
+            acc[sym_idx(a, b)] = fmaf(wr[a], r[b], acc[sym_idx(a, b)]);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 7; a++)
+        if (MASK >> a & 1) acc[28 + a] = fmaf(wr[a], e, acc[28 + a]);
+}
+
+struct PointIn {
+    float xi0, xi1, xi2, xj0, xj1, xj2, ci, cj, q;
+    int vm;
+    int ind;
+};
+
+// One point-edge: residuals, robust weights, raw rows.  tij/qij/sij = T_i^{-1} T_j.
+template <int MODE>
+__device__ __forceinline__ void point_body(const PointIn& p, const Sim3f& Tij, const AccParams& P,
+                                           float* __restrict__ acc) {
+    const float Xj[3] = {p.xj0, p.xj1, p.xj2};
+    float Y[3];
+    act_so3(Tij.q, Xj, Y);
+    const float X0 = Y[0] * Tij.s + Tij.t[0];
+    const float X1 = Y[1] * Tij.s + Tij.t[1];
+    const float X2 = Y[2] * Tij.s + Tij.t[2];
+    bool valid = p.vm && (p.q > P.Q_thresh) && (p.ci > P.C_thresh) && (p.cj > P.C_thresh);
+
+    if constexpr (MODE == GN_RAYS) {
+        // gn_kernels.cu:924-1089
+        const float n2i = (p.xi0 * p.xi0 + p.xi1 * p.xi1) + p.xi2 * p.xi2;
+        const float n1i = sqrtf(n2i);
+        const float n1i_inv = __builtin_amdgcn_rcpf(n1i);
+        const float n2j = (X0 * X0 + X1 * X1) + X2 * X2;
+        const float n1j = sqrtf(n2j);
+        const float n1j_inv = __builtin_amdgcn_rcpf(n1j);
+        const float rx = n1j_inv * X0, ry = n1j_inv * X1, rz = n1j_inv * X2;
+        const float e0 = rx - n1i_inv * p.xi0;
+        const float e1 = ry - n1i_inv * p.xi1;
+        const float e2 = rz - n1i_inv * p.xi2;
+        const float e3 = n1j - n1i;
+        const float sq = sqrtf(p.q);
+        const float swr = valid ? P.s0_inv * sq : 0.0f;
+        const float swd = valid ? P.s1_inv * sq : 0.0f;
+        const float wcr = swr * swr, wcd = swd * swd;
+        const float w0 = huber_w(swr * e0) * wcr;
+        const float w1 = huber_w(swr * e1) * wcr;
+        const float w2 = huber_w(swr * e2) * wcr;
+        const float w3 = huber_w(swd * e3) * wcd;
+        const float n3 = n1j_inv * __builtin_amdgcn_rcpf(n2j);
+        const float dxx = n1j_inv - X0 * X0 * n3;
+        const float dyy = n1j_inv - X1 * X1 * n3;
+        const float dzz = n1j_inv - X2 * X2 * n3;
+        const float dxy = -X0 * X1 * n3;
+        const float dxz = -X0 * X2 * n3;
+        const float dyz = -X1 * X2 * n3;
+        {
+            const float r[7] = {dxx, dxy, dxz, 0.f, rz, -ry, 0.f};
+            acc_row<0b0110111>(acc, r, w0, e0);
+        }
+        {
+            const float r[7] = {dxy, dyy, dyz, -rz, 0.f, rx, 0.f};
+            acc_row<0b0101111>(acc, r, w1, e1);
+        }
+        {
+            const float r[7] = {dxz, dyz, dzz, ry, -rx, 0.f, 0.f};
+            acc_row<0b0011111>(acc, r, w2, e2);
+        }
+        {
+            const float r[7] = {rx, ry, rz, 0.f, 0.f, 0.f, n1j};
+            acc_row<0b1000111>(acc, r, w3, e3);
+        }
+    } else if constexpr (MODE == GN_CALIB) {
+        // gn_kernels.cu:1360-1495
+        int vt = (int)((float)p.ind * P.inv_width);
+        int ut = p.ind - vt * P.width;
+        while (ut < 0) { vt--; ut += P.width; }
+        while (ut >= P.width) { vt++; ut -= P.width; }
+        const bool valid_z = (X2 > P.z_eps) && (p.xi2 > P.z_eps);
+        const float zj_inv = valid_z ? __builtin_amdgcn_rcpf(X2) : 0.0f;
+        const float zj_log = valid_z ? __logf(X2) : 0.0f;
+        const float zi_log = valid_z ? __logf(p.xi2) : 0.0f;
+        const float x = X0 * zj_inv, y = X1 * zj_inv;
+        const float u = P.fx * x + P.cx;
+        const float v = P.fy * y + P.cy;
+        const bool valid_u = (u > P.pb_lo) && (u < P.pb_hi_u);
+        const bool valid_v = (v > P.pb_lo) && (v < P.pb_hi_v);
+        valid = valid && valid_u && valid_v && valid_z;
+        const float e0 = u - (float)ut;
+        const float e1 = v - (float)vt;
+        const float e2 = zj_log - zi_log;
+        const float sq = sqrtf(p.q);
+        const float swp = valid ? P.s0_inv * sq : 0.0f;
+        const float swd = valid ? P.s1_inv * sq : 0.0f;
+        const float wcp = swp * swp, wcd = swd * swd;
+        const float w0 = huber_w(swp * e0) * wcp;
+        const float w1 = huber_w(swp * e1) * wcp;
+        const float w2 = huber_w(swd * e2) * wcd;
+        {
+            const float r[7] = {P.fx * zj_inv, 0.f, -P.fx * x * zj_inv, -P.fx * x * y,
+                                P.fx * (1.0f + x * x), -P.fx * y, 0.f};
+            acc_row<0b0111101>(acc, r, w0, e0);
+        }
+        {
+            const float r[7] = {0.f, P.fy * zj_inv, -P.fy * y * zj_inv, -P.fy * (1.0f + y * y),
+                                P.fy * x * y, P.fy * x, 0.f};
+            acc_row<0b0111110>(acc, r, w1, e1);
+        }
+        {
+            const float r[7] = {0.f, 0.f, zj_inv, y, -x, 0.f, 1.0f};
+            acc_row<0b1011100>(acc, r, w2, e2);
+        }
+    } else {
+        // point_align_kernel, gn_kernels.cu:564-674
+        const float e0 = X0 - p.xi0, e1 = X1 - p.xi1, e2 = X2 - p.xi2;
+        const float swp = valid ? P.s0_inv * sqrtf(p.q) : 0.0f;
+        const float wc = swp * swp;
+        const float w0 = huber_w(swp * e0) * wc;
+        const float w1 = huber_w(swp * e1) * wc;
+        const float w2 = huber_w(swp * e2) * wc;
+        {
+            const float r[7] = {1.f, 0.f, 0.f, 0.f, X2, -X1, X0};
+            acc_row<0b1110001>(acc, r, w0, e0);
+        }
+        {
+            const float r[7] = {0.f, 1.f, 0.f, -X2, 0.f, X0, X1};
+            acc_row<0b1101010>(acc, r, w1, e1);
+        }
+        {
+            const float r[7] = {0.f, 0.f, 1.f, X1, -X0, 0.f, X2};
+            acc_row<0b1011100>(acc, r, w2, e2);
+        }
+    }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Grid: x = point chunk, y = local directed edge.  256 threads, 4 points per lane per step
+// (VEC: 16-B loads of idx/Q/Xj/Cj/valid), fp32 register accumulators, wave + LDS tree,
+// one 36-float partial per workgroup.
+template <int MODE, bool VEC>
+__global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
+    const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
+    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int64_t* __restrict__ idx,
+    const uint8_t* __restrict__ valid, const float* __restrict__ Q, AccParams P,
+    float* __restrict__ partials, const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int e = blockIdx.y;
+    const int c = blockIdx.x;
+    const int ix = ii_loc[e], jx = jj_loc[e];
+    const Sim3f Ti = load_sim3(Twc + (int64_t)ix * 8);
+    const Sim3f Tj = load_sim3(Twc + (int64_t)jx * 8);
+    const Sim3f Tij = rel_sim3(Ti, Tj);
+
+    float acc[kNacc];
+#pragma unroll
+    for (int q = 0; q < kNacc; q++) acc[q] = 0.0f;
+
+    const int HW = P.HW;
+    const int64_t ebase = (int64_t)e * HW;
+    const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
+    const float* __restrict__ Ci_b = Cs + (int64_t)ix * HW;
+    const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
+    const float* __restrict__ Cj_b = Cs + (int64_t)jx * HW;
+    const int k0 = c * P.chunk;
+    const int k1 = min(k0 + P.chunk, HW);
+    const int tid = threadIdx.x;
+
+    if constexpr (VEC) {
+        for (int k = k0 + 4 * tid; k < k1; k += 4 * kAccThreads) {
+            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + ebase + k);
+            const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + ebase + k);
+            const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + ebase + k + 2);
+            const float4 q4 = *reinterpret_cast<const float4*>(Q + ebase + k);
+            const float4 xa = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
+            const float4 xb = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
+            const float4 xc = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
+            const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
+            const int vms[4] = {vm4.x, vm4.y, vm4.z, vm4.w};
+            const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
+            const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
+            const float xj[12] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w,
+                                  xc.x, xc.y, xc.z, xc.w};
+            const float cjs[4] = {cj4.x, cj4.y, cj4.z, cj4.w};
+            PointIn pin[4];
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                int64_t ind = vms[s] ? ids[s] : 0;
+                ind = ind < 0 ? 0 : (ind >= HW ? HW - 1 : ind);  // OOB guard
+                pin[s].ind = (int)ind;
+                pin[s].vm = vms[s] != 0;
+                pin[s].q = qs[s];
+                pin[s].xj0 = xj[3 * s];
+                pin[s].xj1 = xj[3 * s + 1];
+                pin[s].xj2 = xj[3 * s + 2];
+                pin[s].cj = cjs[s];
+            }
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const float* xi = Xi_b + (int64_t)pin[s].ind * 3;
+                pin[s].xi0 = xi[0];
+                pin[s].xi1 = xi[1];
+                pin[s].xi2 = xi[2];
+                pin[s].ci = Ci_b[pin[s].ind];
+            }
+#pragma unroll
+            for (int s = 0; s < 4; s++) point_body<MODE>(pin[s], Tij, P, acc);
+        }
+    } else {
+        for (int k = k0 + tid; k < k1; k += kAccThreads) {
+            PointIn p;
+            p.vm = valid[ebase + k] != 0;
+            int64_t ind = p.vm ? idx[ebase + k] : 0;
+            ind = ind < 0 ? 0 : (ind >= HW ? HW - 1 : ind);
+            p.ind = (int)ind;
+            p.q = Q[ebase + k];
+            p.xj0 = Xj_b[(int64_t)k * 3 + 0];
+            p.xj1 = Xj_b[(int64_t)k * 3 + 1];
+            p.xj2 = Xj_b[(int64_t)k * 3 + 2];
+            p.cj = Cj_b[k];
+            p.xi0 = Xi_b[ind * 3 + 0];
+            p.xi1 = Xi_b[ind * 3 + 1];
+            p.xi2 = Xi_b[ind * 3 + 2];
+            p.ci = Ci_b[ind];
+            point_body<MODE>(p, Tij, P, acc);
+        }
+    }
+
+    // deterministic block reduction: wave butterfly, then 4 waves in fixed order
+    __shared__ float red[kAccThreads / 64][kNacc];
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int q = 0; q < kNacc; q++) {
+        const float s = wave_sum(acc[q]);
+        if (lane == 0) red[wave][q] = s;
+    }
+    __syncthreads();
+    if (tid < kNacc) {
+        float s = red[0][tid];
+#pragma unroll
+        for (int w = 1; w < kAccThreads / 64; w++) s += red[w][tid];
+        partials[((int64_t)e * gridDim.x + c) * kNaccPad + tid] = s;
+    }
+}
+
+// Per local edge: f64 chunk sum (fixed order), Hjj = A M A^T, vj = A g.
+__global__ __launch_bounds__(64) void gn_edge_reduce_kernel(const float* __restrict__ partials,
+                                                            int nchunks,
+                                                            const float* __restrict__ Twc,
+                                                            const int* __restrict__ ii_loc,
+                                                            double* __restrict__ edgeblk,
+                                                            const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int e = blockIdx.x;
+    const int tid = threadIdx.x;
+    __shared__ double M[7][7];
+    __shared__ double g[7];
+    __shared__ double A[7][7];
+    __shared__ double AM[7][7];
+    if (tid < kNacc) {
+        const float* p = partials + (int64_t)e * nchunks * kNaccPad + tid;
+        double s = 0.0;
+        for (int c = 0; c < nchunks; c++) s += (double)p[(int64_t)c * kNaccPad];
+        if (tid < 28) {
+            int a = 0, r = tid;
+            while (r >= 7 - a) { r -= 7 - a; a++; }
+            const int b = a + r;
+            M[a][b] = s;
+            M[b][a] = s;
+        } else {
+            g[tid - 28] = s;
+        }
+    }
+    if (tid < 49) A[tid / 7][tid % 7] = 0.0;
+    __syncthreads();
+    if (tid < 3) {
+        // column tid of the adjoint map of apply_Sim3_adj_inv (gn_kernels.cu:277-297)
+        const float* Ti = Twc + (int64_t)ii_loc[e] * 8;
+        const double t0 = Ti[0], t1 = Ti[1], t2 = Ti[2];
+        const double qx = Ti[3], qy = Ti[4], qz = Ti[5], qw = Ti[6];
+        const double s_inv = 1.0 / (double)Ti[7];
+        // R e_c via the actSO3 formula
+        double X[3] = {0, 0, 0};
+        X[tid] = 1.0;
+        const double uv0 = 2.0 * (qy * X[2] - qz * X[1]);
+        const double uv1 = 2.0 * (qz * X[0] - qx * X[2]);
+        const double uv2 = 2.0 * (qx * X[1] - qy * X[0]);
+        const double R0 = X[0] + qw * uv0 + (qy * uv2 - qz * uv1);
+        const double R1 = X[1] + qw * uv1 + (qz * uv0 - qx * uv2);
+        const double R2 = X[2] + qw * uv2 + (qx * uv1 - qy * uv0);
+        A[0][tid] = s_inv * R0;
+        A[1][tid] = s_inv * R1;
+        A[2][tid] = s_inv * R2;
+        A[3][tid] = s_inv * (t1 * R2 - t2 * R1);
+        A[4][tid] = s_inv * (t2 * R0 - t0 * R2);
+        A[5][tid] = s_inv * (t0 * R1 - t1 * R0);
+        A[6][tid] = s_inv * (t0 * R0 + t1 * R1 + t2 * R2);
+        A[3][3 + tid] = R0;
+        A[4][3 + tid] = R1;
+        A[5][3 + tid] = R2;
+        if (tid == 0) A[6][6] = 1.0;
+    }
+    __syncthreads();
+    if (tid < 49) {
+        const int a = tid / 7, b = tid % 7;
+        double s = 0.0;
+#pragma unroll
+        for (int p = 0; p < 7; p++) s += A[a][p] * M[p][b];
+        AM[a][b] = s;
+    }
+    __syncthreads();
+    double* out = edgeblk + (int64_t)e * kEdgeBlk;
+    if (tid < 28) {
+        int a = 0, r = tid;
+        while (r >= 7 - a) { r -= 7 - a; a++; }
+        const int b = a + r;
+        double s = 0.0;
+#pragma unroll
+        for (int p = 0; p < 7; p++) s += AM[a][p] * A[b][p];
+        out[tid] = s;  // Hjj (upper packed)
+    } else if (tid < 35) {
+        const int a = tid - 28;
+        double s = 0.0;
+#pragma unroll
+        for (int p = 0; p < 7; p++) s += A[a][p] * g[p];
+        out[tid] = s;  // vj
+    }
+}
+
+// Compact block-sparse system: slots [0, nblk) hold 28 doubles each, followed by the
+// gradient (N-1)*7.  One 64-lane workgroup per block slot / gradient row.
+__global__ __launch_bounds__(64) void gn_compact_kernel(
+    const double* __restrict__ edgeblk, const int* __restrict__ blk_ptr,
+    const int* __restrict__ blk_ent, const int* __restrict__ grad_ptr,
+    const int* __restrict__ grad_ent, int nblk, int npose, double* __restrict__ compact,
+    const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (s < nblk) {
+        if (tid < 28) {
+            double acc = 0.0;
+            for (int k = blk_ptr[s]; k < blk_ptr[s + 1]; k++) {
+                const int code = blk_ent[k];
+                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + tid];
+                acc += (code & 1) ? -v : v;
+            }
+            compact[(int64_t)s * 28 + tid] = acc;
+        }
+    } else {
+        const int p = s - nblk;
+        if (p < npose && tid < 7) {
+            double acc = 0.0;
+            for (int k = grad_ptr[p]; k < grad_ptr[p + 1]; k++) {
+                const int code = grad_ent[k];
+                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + 28 + tid];
+                acc += (code & 1) ? -v : v;
+            }
+            compact[(int64_t)nblk * 28 + p * 7 + tid] = acc;
+        }
+    }
+}
+
+// Dense f64 matrix [npad + T rows][npad cols]: system in rows < npad (identity on the
+// padding), RHS b in row npad (the bordered row: the forward solve rides along with the
+// factorisation).
+__global__ __launch_bounds__(256) void gn_fill_dense_kernel(const double* __restrict__ compact,
+                                                            const int* __restrict__ slotmap,
+                                                            int nblk, int npose, int n, int npad,
+                                                            double* __restrict__ Hd,
+                                                            const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int64_t total = (int64_t)(npad + kCholTile) * npad;
+    for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(id / npad), c = (int)(id % npad);
+        double val;
+        if (r > npad) {
+            val = 0.0;  // unused rows of the border tile
+        } else if (r == npad) {
+            val = c < n ? compact[(int64_t)nblk * 28 + c] : 0.0;
+        } else if (r < n && c < n) {
+            const int br = r / 7, bc = c / 7;
+            const int slot = slotmap[(int64_t)br * npose + bc];
+            const int a = r % 7, b = c % 7;
+            val = slot >= 0 ? compact[(int64_t)slot * 28 + (a <= b ? sym_idx(a, b) : sym_idx(b, a))]
+                            : 0.0;
+        } else {
+            val = (r == c) ? 1.0 : 0.0;
+        }
+        Hd[id] = val;
+    }
+}
+
+// ---- blocked Cholesky, T = 64 --------------------------------------------------
+
+constexpr int T = kCholTile;
+constexpr int LD = T + 1;  // LDS row stride (doubles)
+
+// Factor the diagonal tile in LDS (right-looking), returns false if a pivot <= 0.
+__device__ bool factor_diag_lds(double (*L)[LD]) {
+    const int tid = threadIdx.x;
+    bool ok = true;
+    for (int c = 0; c < T; c++) {
+        __syncthreads();
+        const double d = L[c][c];
+        if (d <= 0.0) ok = false;  // SimplicialLLT: fails iff pivot <= 0 (NaN passes)
+        const double lcc = sqrt(d);
+        const double inv = 1.0 / lcc;
+        __syncthreads();
+        if (tid > c && tid < T) L[tid][c] *= inv;
+        if (tid == 0) L[c][c] = lcc;
+        __syncthreads();
+        const int m = T - 1 - c;
+        for (int k = tid; k < m * m; k += blockDim.x) {
+            const int rr = k / m, cc = k % m;
+            if (cc <= rr) L[c + 1 + rr][c + 1 + cc] -= L[c + 1 + rr][c] * L[c + 1 + cc][c];
+        }
+    }
+    __syncthreads();
+    return ok;
+}
+
+// Panel step k: WG 0 factors A_kk; WG m>0 computes L_{k+m,k} = A_{k+m,k} L_kk^{-T}
+// (tile row nt is the RHS border row).
+__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ Hd, int npad, int k,
+                                                         int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    __shared__ double L[T][LD];
+    __shared__ double X[T][LD];
+    const int tid = threadIdx.x;
+    const int m = blockIdx.x;
+    double* Akk = Hd + (int64_t)k * T * npad + (int64_t)k * T;
+    for (int id = tid; id < T * T; id += blockDim.x) {
+        const int r = id / T, c = id % T;
+        L[r][c] = (c <= r) ? Akk[(int64_t)r * npad + c] : 0.0;
+    }
+    const bool ok = factor_diag_lds(L);
+    if (m == 0) {
+        if (!ok && tid == 0) flags[kFlagFail] = 1;
+        for (int id = tid; id < T * T; id += blockDim.x) {
+            const int r = id / T, c = id % T;
+            if (c <= r) Akk[(int64_t)r * npad + c] = L[r][c];
+        }
+        return;
+    }
+    const int i = k + m;
+    double* Aik = Hd + (int64_t)i * T * npad + (int64_t)k * T;
+    for (int id = tid; id < T * T; id += blockDim.x) {
+        const int r = id / T, c = id % T;
+        X[r][c] = Aik[(int64_t)r * npad + c];
+    }
+    __syncthreads();
+    // X <- X L^{-T}: column-oriented forward substitution over the tile columns
+    for (int c = 0; c < T; c++) {
+        if (tid < T) X[tid][c] /= L[c][c];
+        __syncthreads();
+        const int m2 = T - 1 - c;
+        for (int id = tid; id < T * m2; id += blockDim.x) {
+            const int r = id / m2, cc = c + 1 + id % m2;
+            X[r][cc] -= X[r][c] * L[cc][c];
+        }
+        __syncthreads();
+    }
+    for (int id = tid; id < T * T; id += blockDim.x) {
+        const int r = id / T, c = id % T;
+        Aik[(int64_t)r * npad + c] = X[r][c];
+    }
+}
+
+// Trailing update after panel k: A_ij -= L_ik L_jk^T for k < j <= i <= nt, j < nt.
+__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ Hd, int npad,
+                                                          int nt, int k,
+                                                          const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    __shared__ double Li[T][LD];
+    __shared__ double Lj[T][LD];
+    // blockIdx.x -> (i, j): j = k+1.., i = j..nt
+    int rem = blockIdx.x;
+    int j = k + 1;
+    while (rem >= nt - j + 1) { rem -= nt - j + 1; j++; }
+    const int i = j + rem;
+    const int tid = threadIdx.x;
+    const double* Aik = Hd + (int64_t)i * T * npad + (int64_t)k * T;
+    const double* Ajk = Hd + (int64_t)j * T * npad + (int64_t)k * T;
+    for (int id = tid; id < T * T; id += blockDim.x) {
+        const int r = id / T, c = id % T;
+        Li[r][c] = Aik[(int64_t)r * npad + c];
+        Lj[r][c] = Ajk[(int64_t)r * npad + c];
+    }
+    __syncthreads();
+    const int r0 = (tid / 16) * 4, c0 = (tid % 16) * 4;
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
+    for (int p = 0; p < T; p++) {
+        double li[4], lj[4];
+#pragma unroll
+        for (int a = 0; a < 4; a++) li[a] = Li[r0 + a][p];
+#pragma unroll
+        for (int b = 0; b < 4; b++) lj[b] = Lj[c0 + b][p];
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] = fma(li[a], lj[b], acc[a][b]);
+    }
+    double* Aij = Hd + (int64_t)i * T * npad + (int64_t)j * T;
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) Aij[(int64_t)(r0 + a) * npad + c0 + b] -= acc[a][b];
+}
+
+// Back substitution step k (k = nt-1 .. 0) of L^T x = y, y in the border row.
+// Every WG solves L_kk^T x_k = y_k; WG k stores x_k, WG j < k updates y_j -= L_kj^T x_k.
+__global__ __launch_bounds__(64) void back_step_kernel(double* __restrict__ Hd, int npad, int k,
+                                                       double* __restrict__ x,
+                                                       const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    __shared__ double L[T][LD];
+    __shared__ double y[T];
+    const int tid = threadIdx.x;
+    const double* Akk = Hd + (int64_t)k * T * npad + (int64_t)k * T;
+    double* yrow = Hd + (int64_t)npad * npad;
+    for (int id = tid; id < T * T; id += blockDim.x) {
+        const int r = id / T, c = id % T;
+        L[r][c] = Akk[(int64_t)r * npad + c];
+    }
+    y[tid] = yrow[k * T + tid];
+    __syncthreads();
+    for (int c = T - 1; c >= 0; c--) {
+        if (tid == 0) y[c] = y[c] / L[c][c];
+        __syncthreads();
+        if (tid < c) y[tid] -= L[c][tid] * y[c];
+        __syncthreads();
+    }
+    const int j = blockIdx.x;
+    if (j == k) {
+        x[k * T + tid] = y[tid];
+        return;
+    }
+    // y_j[a] -= sum_b L_kj[b][a] x_k[b]
+    const double* Lkj = Hd + (int64_t)k * T * npad + (int64_t)j * T;
+    double s = 0.0;
+    for (int b = 0; b < T; b++) s += Lkj[(int64_t)b * npad + tid] * y[b];
+    yrow[j * T + tid] -= s;
+}
+
+// dx = -x (or 0 if the factorisation failed), in-place retraction of poses 1..N-1,
+// ||dx|| < delta_thresh => done (gn_kernels.cu:1209-1222).
+__global__ __launch_bounds__(256) void gn_retract_kernel(float* __restrict__ Twc,
+                                                         const double* __restrict__ x,
+                                                         float* __restrict__ dx, int N,
+                                                         float delta_thresh,
+                                                         int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int tid = threadIdx.x;
+    const bool fail = flags[kFlagFail] != 0;
+    double nrm = 0.0;
+    for (int p = 1 + tid; p < N; p += blockDim.x) {
+        float xi[7];
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+            const float v = fail ? 0.0f : -(float)x[(int64_t)(p - 1) * 7 + q];
+            xi[q] = v;
+            dx[(int64_t)(p - 1) * 7 + q] = v;
+            nrm += (double)v * (double)v;
+        }
+        retr_sim3(xi, Twc + (int64_t)p * 8);
+    }
+    __shared__ double red[256];
+    red[tid] = nrm;
+    __syncthreads();
+    for (int s = 128; s >= 1; s >>= 1) {
+        if (tid < s) red[tid] += red[tid + s];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        flags[kFlagFail] = 0;
+        if ((float)sqrt(red[0]) < delta_thresh) flags[kFlagDone] = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers (host)
+// ---------------------------------------------------------------------------
+
+hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
+                        const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
+                        const int64_t* idx, const uint8_t* valid, const float* Q,
+                        const AccParams& P, float* partials, const int* flags) {
+#define M3S_ACC(MODE, V)                                                                    \
+    hipLaunchKernelGGL((gn_accum_kernel<MODE, V>), grid, dim3(kAccThreads), 0, st, Twc, Xs, \
+                       Cs, ii_loc, jj_loc, idx, valid, Q, P, partials, flags)
+    if (mode == GN_RAYS) {
+        if (vec) M3S_ACC(GN_RAYS, true); else M3S_ACC(GN_RAYS, false);
+    } else if (mode == GN_CALIB) {
+        if (vec) M3S_ACC(GN_CALIB, true); else M3S_ACC(GN_CALIB, false);
+    } else {
+        if (vec) M3S_ACC(GN_POINTS, true); else M3S_ACC(GN_POINTS, false);
+    }
+#undef M3S_ACC
+    return hipGetLastError();
+}
+
+hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
+                              const float* Twc, const int* ii_loc, double* edgeblk,
+                              const int* flags) {
+    hipLaunchKernelGGL(gn_edge_reduce_kernel, dim3(E_local), dim3(64), 0, st, partials, nchunks,
+                       Twc, ii_loc, edgeblk, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(hipStream_t st, const double* edgeblk, const int* blk_ptr,
+                          const int* blk_ent, const int* grad_ptr, const int* grad_ent, int nblk,
+                          int npose, double* compact, const int* flags) {
+    hipLaunchKernelGGL(gn_compact_kernel, dim3(nblk + npose), dim3(64), 0, st, edgeblk, blk_ptr,
+                       blk_ent, grad_ptr, grad_ent, nblk, npose, compact, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
+                        int npose, int n, int npad, double* Hd, double* x, int* flags) {
+    const int64_t total = (int64_t)(npad + kCholTile) * npad;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(gn_fill_dense_kernel, dim3(blocks), dim3(256), 0, st, compact, slotmap,
+                       nblk, npose, n, npad, Hd, flags);
+    const int nt = npad / T;
+    for (int k = 0; k < nt; k++) {
+        hipLaunchKernelGGL(chol_panel_kernel, dim3(nt - k + 1), dim3(256), 0, st, Hd, npad, k,
+                           flags);
+        int nupd = 0;
+        for (int j = k + 1; j < nt; j++) nupd += nt - j + 1;
+        if (nupd > 0)
+            hipLaunchKernelGGL(chol_update_kernel, dim3(nupd), dim3(256), 0, st, Hd, npad, nt, k,
+                               flags);
+    }
+    for (int k = nt - 1; k >= 0; k--)
+        hipLaunchKernelGGL(back_step_kernel, dim3(k + 1), dim3(64), 0, st, Hd, npad, k, x, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,
+                            int npose, int n, int npad, double* Hd, const int* flags) {
+    const int64_t total = (int64_t)(npad + kCholTile) * npad;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(gn_fill_dense_kernel, dim3(blocks), dim3(256), 0, st, compact, slotmap,
+                       nblk, npose, n, npad, Hd, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
+                          float delta_thresh, int* flags) {
+    hipLaunchKernelGGL(gn_retract_kernel, dim3(1), dim3(256), 0, st, Twc, x, dx, N, delta_thresh,
+                       flags);
+    return hipGetLastError();
+}
+
+}  // namespace m3s

@@ -1,0 +1,333 @@
+// matching.hip -- MI355X (gfx950) kernels for the iterative projective matcher.
+//
+//   iter_proj       : per-pixel Levenberg-Marquardt projection of a target ray onto a
+//                     9-channel ray+gradient image (reference matching_kernels.cu:119-275)
+//   refine_matches  : dilated-window descriptor argmax with c10::Half per-op rounding
+//                     (reference matching_kernels.cu:25-81)
+//
+// Parity contract: bit-exact with the CPU oracle (oracle/m3s_oracle.c).  FMA contraction
+// is OFF for this whole file (also -ffp-contract=off in the Makefile) and every double
+// literal promotion of the reference source is an explicit double operation.
+//
+// Launch shape (MI355X-first, not the reference's 16-thread blocks): 256-thread
+// workgroups (4 wave64s), one point per lane, consecutive lanes on consecutive pixels
+// so the bilinear / window gathers of a wave hit the same L1/L2 lines.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/m3s_backend.h"
+#include "m3s_common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ float clamp_ref(float x, float lo, float hi) {
+    return fminf(fmaxf(x, lo), hi);  // matching_kernels.cu:21-23
+}
+
+// 1.0/x in double, rounded to float (the reference writes `1.0/r_norm`).
+__device__ __forceinline__ float inv_d(float x) { return (float)(1.0 / (double)x); }
+
+// Bilinear weights and texel base pointers (matching_kernels.cu:155-170 and :225-239).
+struct Bilin {
+    float w11, w12, w21, w22;
+    const float *r11, *r12, *r21, *r22;
+};
+
+__device__ __forceinline__ Bilin make_bilin(const float* __restrict__ img, int W, float u, float v) {
+    Bilin b;
+    const int u11 = (int)floorf(u);
+    const int v11 = (int)floorf(v);
+    const float du = u - (float)u11;
+    const float dv = v - (float)v11;
+    b.w11 = du * dv;
+    b.w12 = (float)((1.0 - (double)du) * (double)dv);
+    b.w21 = (float)((double)du * (1.0 - (double)dv));
+    b.w22 = (float)((1.0 - (double)du) * (1.0 - (double)dv));
+    const int64_t row0 = (int64_t)v11 * W;
+    const int64_t row1 = (int64_t)(v11 + 1) * W;
+    b.r11 = img + (row1 + u11 + 1) * 9;
+    b.r12 = img + (row1 + u11) * 9;
+    b.r21 = img + (row0 + u11 + 1) * 9;
+    b.r22 = img + (row0 + u11) * 9;
+    return b;
+}
+
+__device__ __forceinline__ float interp(const Bilin& b, int j) {
+    const float a = b.w11 * b.r11[j];
+    const float c = b.w12 * b.r12[j];
+    const float d = b.w21 * b.r21[j];
+    const float e = b.w22 * b.r22[j];
+    return ((a + c) + d) + e;
+}
+
+__global__ __launch_bounds__(kBlock) void iter_proj_kernel(
+    const float* __restrict__ rays, const float* __restrict__ pts, const float* __restrict__ p_init,
+    float* __restrict__ p_new, uint8_t* __restrict__ converged, int H, int W, int64_t N,
+    int64_t total, int max_iter, float lambda_init, float cost_thresh) {
+    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= total) return;
+    const int64_t b = g / N;
+    const float* __restrict__ img = rays + b * (int64_t)H * W * 9;
+
+    const float2 pi = *reinterpret_cast<const float2*>(p_init + g * 2);
+    float u = clamp_ref(pi.x, 1.0f, (float)(W - 2));
+    float v = clamp_ref(pi.y, 1.0f, (float)(H - 2));
+    const float px = pts[g * 3 + 0], py = pts[g * 3 + 1], pz = pts[g * 3 + 2];
+    const float umax = (float)(W - 2), vmax = (float)(H - 2);
+
+    float lambda = lambda_init;
+    uint8_t conv = 0;
+    for (int it = 0; it < max_iter; it++) {
+        const Bilin bl = make_bilin(img, W, u, v);
+        float r0 = interp(bl, 0), r1 = interp(bl, 1), r2 = interp(bl, 2);
+        const float gx0 = interp(bl, 3), gx1 = interp(bl, 4), gx2 = interp(bl, 5);
+        const float gy0 = interp(bl, 6), gy1 = interp(bl, 7), gy2 = interp(bl, 8);
+
+        const float r_norm = sqrtf((r0 * r0 + r1 * r1) + r2 * r2);
+        const float r_norm_inv = inv_d(r_norm);
+        r0 *= r_norm_inv;
+        r1 *= r_norm_inv;
+        r2 *= r_norm_inv;
+        const float e0 = r0 - px, e1 = r1 - py, e2 = r2 - pz;
+        const float cost = (e0 * e0 + e1 * e1) + e2 * e2;
+
+        float A00 = (gx0 * gx0 + gx1 * gx1) + gx2 * gx2;
+        const float A01 = (gx0 * gy0 + gx1 * gy1) + gx2 * gy2;
+        float A11 = (gy0 * gy0 + gy1 * gy1) + gy2 * gy2;
+        const float b0 = -((e0 * gx0 + e1 * gx1) + e2 * gx2);
+        const float b1 = -((e0 * gy0 + e1 * gy1) + e2 * gy2);
+        A00 += lambda;
+        A11 += lambda;
+
+        const float det_inv = inv_d(A00 * A11 - A01 * A01);
+        const float delta_u = det_inv * (A11 * b0 - A01 * b1);
+        const float delta_v = det_inv * ((-A01) * b0 + A00 * b1);
+
+        const float u_new = clamp_ref(u + delta_u, 1.0f, umax);
+        const float v_new = clamp_ref(v + delta_v, 1.0f, vmax);
+
+        const Bilin bn = make_bilin(img, W, u_new, v_new);
+        const float t0 = interp(bn, 0), t1 = interp(bn, 1), t2 = interp(bn, 2);
+        const float n2 = sqrtf((t0 * t0 + t1 * t1) + t2 * t2);
+        const float n2_inv = inv_d(n2);
+        const float f0 = t0 * n2_inv - px, f1 = t1 * n2_inv - py, f2 = t2 * n2_inv - pz;
+        const float new_cost = (f0 * f0 + f1 * f1) + f2 * f2;
+
+        if (new_cost < cost) {
+            u = u_new;
+            v = v_new;
+            lambda = (float)((double)lambda * 0.1);  // `lambda *= 0.1` is a double multiply
+            conv = new_cost < cost_thresh;
+        } else {
+            lambda = (float)((double)lambda * 10.0);
+            conv = cost < cost_thresh;
+        }
+    }
+    *reinterpret_cast<float2*>(p_new + g * 2) = make_float2(u, v);
+    converged[g] = conv;
+}
+
+// ---------------------------------------------------------------------------------
+// refine_matches
+// ---------------------------------------------------------------------------------
+
+// cuda::std::numeric_limits<c10::Half>::min() is value-initialised (no libcu++
+// specialisation for c10::Half) => 0.0.  Single named constant, see DESIGN.md.
+constexpr float kRefineHalfMaxInit = 0.0f;
+// For float the limits are specialised: FLT_MIN.
+constexpr float kRefineFloatMaxInit = 1.17549435e-38f;
+
+__device__ __forceinline__ bool inside_image(int64_t u, int64_t v, int W, int H) {
+    return v >= 0 && v < H && u >= 0 && u < W;  // matching_kernels.cu:17-19
+}
+
+typedef _Float16 half_t;
+
+// F = 24 fp16 fast path: the query descriptor lives in registers (3 x 16 B loads),
+// each candidate row is 48 B = 3 x dwordx4.  Sequential fp16 accumulation exactly as
+// c10::Half: round after every * and after every +=.
+template <int F>
+__global__ __launch_bounds__(kBlock) void refine_f16_kernel(
+    const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21,
+    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int H, int W, int64_t N,
+    int64_t total, int radius, int dilation_max) {
+    static_assert(F % 8 == 0, "vector path needs F % 8 == 0");
+    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= total) return;
+    const int64_t b = g / N;
+
+    half_t q[F];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
+#pragma unroll
+        for (int c = 0; c < F / 8; c++) {
+            uint4 w = src[c];
+            const half_t* hp = reinterpret_cast<const half_t*>(&w);
+#pragma unroll
+            for (int k = 0; k < 8; k++) q[c * 8 + k] = hp[k];
+        }
+    }
+    const uint16_t* __restrict__ img = D11 + b * (int64_t)H * W * F;
+
+    int64_t u0 = p1[g * 2 + 0];
+    int64_t v0 = p1[g * 2 + 1];
+    half_t max_score = (half_t)kRefineHalfMaxInit;
+    int64_t u_new = u0, v_new = v0;
+    const int S = 2 * radius + 1;
+    for (int d = dilation_max; d > 0; d--) {
+        const int rd = radius * d;
+        for (int i = 0; i < S; i++) {          // u offset outer (matching_kernels.cu:54)
+            const int64_t u = u0 - rd + (int64_t)i * d;
+            for (int j = 0; j < S; j++) {      // v offset inner (:55)
+                const int64_t v = v0 - rd + (int64_t)j * d;
+                if (inside_image(u, v, W, H)) {
+                    const uint4* src = reinterpret_cast<const uint4*>(img + (v * W + u) * F);
+                    half_t score = (half_t)0.0f;
+#pragma unroll
+                    for (int c = 0; c < F / 8; c++) {
+                        uint4 w = src[c];
+                        const half_t* hp = reinterpret_cast<const half_t*>(&w);
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            const half_t p = q[c * 8 + k] * hp[k];
+                            score = score + p;
+                        }
+                    }
+                    if (score > max_score) {
+                        max_score = score;
+                        u_new = u;
+                        v_new = v;
+                    }
+                }
+            }
+        }
+        u0 = u_new;
+        v0 = v_new;
+    }
+    p1_new[g * 2 + 0] = u_new;
+    p1_new[g * 2 + 1] = v_new;
+}
+
+// Generic F (any descriptor width), fp16 or f32, scalar loads.
+template <typename T>
+__device__ __forceinline__ T zero_score();
+template <>
+__device__ __forceinline__ half_t zero_score<half_t>() { return (half_t)0.0f; }
+template <>
+__device__ __forceinline__ float zero_score<float>() { return 0.0f; }
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void refine_generic_kernel(
+    const T* __restrict__ D11, const T* __restrict__ D21, const int64_t* __restrict__ p1,
+    int64_t* __restrict__ p1_new, int H, int W, int64_t N, int64_t F, int64_t total, int radius,
+    int dilation_max, float max_init) {
+    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= total) return;
+    const int64_t b = g / N;
+    const T* __restrict__ q = D21 + g * F;
+    const T* __restrict__ img = D11 + b * (int64_t)H * W * F;
+    int64_t u0 = p1[g * 2 + 0];
+    int64_t v0 = p1[g * 2 + 1];
+    T max_score = (T)max_init;
+    int64_t u_new = u0, v_new = v0;
+    const int S = 2 * radius + 1;
+    for (int d = dilation_max; d > 0; d--) {
+        const int rd = radius * d;
+        for (int i = 0; i < S; i++) {
+            const int64_t u = u0 - rd + (int64_t)i * d;
+            for (int j = 0; j < S; j++) {
+                const int64_t v = v0 - rd + (int64_t)j * d;
+                if (inside_image(u, v, W, H)) {
+                    const T* row = img + (v * W + u) * F;
+                    T score = zero_score<T>();
+                    for (int64_t k = 0; k < F; k++) {
+                        const T p = q[k] * row[k];
+                        score = score + p;
+                    }
+                    if (score > max_score) {
+                        max_score = score;
+                        u_new = u;
+                        v_new = v;
+                    }
+                }
+            }
+        }
+        u0 = u_new;
+        v0 = v_new;
+    }
+    p1_new[g * 2 + 0] = u_new;
+    p1_new[g * 2 + 1] = v_new;
+}
+
+inline unsigned grid_for(int64_t total) { return (unsigned)((total + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+extern "C" int m3s_iter_proj(const float* rays, const float* pts, const float* p_init,
+                             float* p_new, uint8_t* converged, int64_t B, int64_t H, int64_t W,
+                             int64_t N, int max_iter, float lambda_init, float cost_thresh,
+                             void* stream) {
+    M3S_REQUIRE(B >= 0 && N >= 0, "iter_proj: negative sizes");
+    M3S_REQUIRE(H >= 3 && W >= 3, "iter_proj: ray image must be at least 3x3 (got %lldx%lld)",
+                (long long)H, (long long)W);
+    M3S_REQUIRE(H * W < (int64_t)1 << 31, "iter_proj: image too large");
+    const int64_t total = B * N;
+    if (total == 0) return M3S_OK;
+    M3S_REQUIRE(rays && pts && p_init && p_new && converged, "iter_proj: null pointer");
+    hipLaunchKernelGGL(iter_proj_kernel, dim3(grid_for(total)), dim3(kBlock), 0,
+                       (hipStream_t)stream, rays, pts, p_init, p_new, converged, (int)H, (int)W, N,
+                       total, max_iter, lambda_init, cost_thresh);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+}
+
+static int refine_checks(const void* D11, const void* D21, const void* p1, void* out, int64_t B,
+                         int64_t H, int64_t W, int64_t N, int64_t F, int radius,
+                         int dilation_max) {
+    M3S_REQUIRE(B >= 0 && N >= 0 && H >= 0 && W >= 0 && F >= 0, "refine_matches: negative sizes");
+    M3S_REQUIRE(H * W < (int64_t)1 << 31, "refine_matches: image too large");
+    M3S_REQUIRE(radius >= 0 && dilation_max >= 0, "refine_matches: negative radius/dilation");
+    if (B * N > 0) M3S_REQUIRE(D11 && D21 && p1 && out, "refine_matches: null pointer");
+    return M3S_OK;
+}
+
+extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
+                                      int64_t* p1_new, int64_t B, int64_t H, int64_t W, int64_t N,
+                                      int64_t F, int radius, int dilation_max, void* stream) {
+    int rc = refine_checks(D11, D21, p1, p1_new, B, H, W, N, F, radius, dilation_max);
+    if (rc) return rc;
+    const int64_t total = B * N;
+    if (total == 0) return M3S_OK;
+    const bool aligned = ((uintptr_t)D11 % 16 == 0) && ((uintptr_t)D21 % 16 == 0);
+    if (F == 24 && aligned) {
+        hipLaunchKernelGGL(refine_f16_kernel<24>, dim3(grid_for(total)), dim3(kBlock), 0,
+                           (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, total,
+                           radius, dilation_max);
+    } else {
+        hipLaunchKernelGGL(refine_generic_kernel<half_t>, dim3(grid_for(total)), dim3(kBlock), 0,
+                           (hipStream_t)stream, reinterpret_cast<const half_t*>(D11),
+                           reinterpret_cast<const half_t*>(D21), p1, p1_new, (int)H, (int)W, N, F,
+                           total, radius, dilation_max, kRefineHalfMaxInit);
+    }
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+}
+
+extern "C" int m3s_refine_matches_f32(const float* D11, const float* D21, const int64_t* p1,
+                                      int64_t* p1_new, int64_t B, int64_t H, int64_t W, int64_t N,
+                                      int64_t F, int radius, int dilation_max, void* stream) {
+    int rc = refine_checks(D11, D21, p1, p1_new, B, H, W, N, F, radius, dilation_max);
+    if (rc) return rc;
+    const int64_t total = B * N;
+    if (total == 0) return M3S_OK;
+    hipLaunchKernelGGL(refine_generic_kernel<float>, dim3(grid_for(total)), dim3(kBlock), 0,
+                       (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, F, total,
+                       radius, dilation_max, kRefineFloatMaxInit);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+}

@@ -1,0 +1,145 @@
+// sim3.h -- device Sim3 math for the GN kernels (float, reference formulas).
+//
+// Restates the reference's device library gn_kernels.cu:172-413 (quat_comp, actSO3,
+// actSim3, relSim3, expSO3, expSim3, retrSim3), keeping its double-literal promotions
+// so the retraction tracks the CPU oracle to a few ulp (sin/cos/exp ulp aside).
+// Layout: t(3), q(4: x,y,z,w), s; tangent order tau(3), phi(3), sigma(1).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace m3s {
+
+struct Sim3f {
+    float t[3];
+    float q[4];
+    float s;
+};
+
+__device__ __forceinline__ Sim3f load_sim3(const float* __restrict__ p) {
+    Sim3f T;
+    T.t[0] = p[0]; T.t[1] = p[1]; T.t[2] = p[2];
+    T.q[0] = p[3]; T.q[1] = p[4]; T.q[2] = p[5]; T.q[3] = p[6];
+    T.s = p[7];
+    return T;
+}
+
+// gn_kernels.cu:178-184
+__device__ __forceinline__ void quat_comp(const float* qi, const float* qj, float* out) {
+    const float o0 = ((qi[3] * qj[0] + qi[0] * qj[3]) + qi[1] * qj[2]) - qi[2] * qj[1];
+    const float o1 = ((qi[3] * qj[1] - qi[0] * qj[2]) + qi[1] * qj[3]) + qi[2] * qj[0];
+    const float o2 = ((qi[3] * qj[2] + qi[0] * qj[1]) - qi[1] * qj[0]) + qi[2] * qj[3];
+    const float o3 = ((qi[3] * qj[3] - qi[0] * qj[0]) - qi[1] * qj[1]) - qi[2] * qj[2];
+    out[0] = o0; out[1] = o1; out[2] = o2; out[3] = o3;
+}
+
+// gn_kernels.cu:195-205 (alias-safe)
+__device__ __forceinline__ void act_so3(const float* q, const float* X, float* Y) {
+    const float uv0 = (float)(2.0 * (double)(q[1] * X[2] - q[2] * X[1]));
+    const float uv1 = (float)(2.0 * (double)(q[2] * X[0] - q[0] * X[2]));
+    const float uv2 = (float)(2.0 * (double)(q[0] * X[1] - q[1] * X[0]));
+    const float y0 = (X[0] + q[3] * uv0) + (q[1] * uv2 - q[2] * uv1);
+    const float y1 = (X[1] + q[3] * uv1) + (q[2] * uv0 - q[0] * uv2);
+    const float y2 = (X[2] + q[3] * uv2) + (q[0] * uv1 - q[1] * uv0);
+    Y[0] = y0; Y[1] = y1; Y[2] = y2;
+}
+
+// gn_kernels.cu:252-272: T_ij = T_i^{-1} T_j
+__device__ __forceinline__ Sim3f rel_sim3(const Sim3f& Ti, const Sim3f& Tj) {
+    Sim3f R;
+    const float si_inv = (float)(1.0 / (double)Ti.s);
+    R.s = si_inv * Tj.s;
+    const float qi_inv[4] = {-Ti.q[0], -Ti.q[1], -Ti.q[2], Ti.q[3]};
+    quat_comp(qi_inv, Tj.q, R.q);
+    float t[3] = {Tj.t[0] - Ti.t[0], Tj.t[1] - Ti.t[1], Tj.t[2] - Ti.t[2]};
+    act_so3(qi_inv, t, t);
+    R.t[0] = t[0] * si_inv; R.t[1] = t[1] * si_inv; R.t[2] = t[2] * si_inv;
+    return R;
+}
+
+// gn_kernels.cu:229-240: b <- a x b
+__device__ __forceinline__ void cross_inplace(const float* a, float* b) {
+    const float x0 = a[1] * b[2] - a[2] * b[1];
+    const float x1 = a[2] * b[0] - a[0] * b[2];
+    const float x2 = a[0] * b[1] - a[1] * b[0];
+    b[0] = x0; b[1] = x1; b[2] = x2;
+}
+
+// gn_kernels.cu:299-321
+__device__ __forceinline__ void exp_so3(const float* phi, float* q) {
+    const float theta_sq = (phi[0] * phi[0] + phi[1] * phi[1]) + phi[2] * phi[2];
+    float imag, real;
+    if ((double)theta_sq < 1e-6) {
+        const float theta_p4 = theta_sq * theta_sq;
+        imag = (float)((0.5 - (1.0 / 48.0) * (double)theta_sq) + (1.0 / 3840.0) * (double)theta_p4);
+        real = (float)((1.0 - (1.0 / 8.0) * (double)theta_sq) + (1.0 / 384.0) * (double)theta_p4);
+    } else {
+        const float theta = sqrtf(theta_sq);
+        imag = sinf((float)(0.5 * (double)theta)) / theta;
+        real = cosf((float)(0.5 * (double)theta));
+    }
+    q[0] = imag * phi[0];
+    q[1] = imag * phi[1];
+    q[2] = imag * phi[2];
+    q[3] = real;
+}
+
+// gn_kernels.cu:323-390 (as written, including B = (C - ...)/theta^2 at :371)
+__device__ __forceinline__ void exp_sim3(const float* xi, float* t, float* q, float* s) {
+    float tau[3] = {xi[0], xi[1], xi[2]};
+    const float phi[3] = {xi[3], xi[4], xi[5]};
+    const float sigma = xi[6];
+    const float scale = expf(sigma);
+    exp_so3(phi, q);
+    s[0] = scale;
+    const float theta_sq = (phi[0] * phi[0] + phi[1] * phi[1]) + phi[2] * phi[2];
+    const float theta = sqrtf(theta_sq);
+    float A, B, C;
+    const float one = 1.0f, half = 0.5f;
+    if ((double)fabsf(sigma) < 1e-6) {
+        C = one;
+        if ((double)fabsf(theta) < 1e-6) {
+            A = half;
+            B = (float)(1.0 / 6.0);
+        } else {
+            A = (one - cosf(theta)) / theta_sq;
+            B = (theta - sinf(theta)) / (theta_sq * theta);
+        }
+    } else {
+        C = (scale - one) / sigma;
+        if ((double)fabsf(theta) < 1e-6) {
+            const float sigma_sq = sigma * sigma;
+            A = ((sigma - one) * scale + one) / sigma_sq;
+            B = ((((scale * half) * sigma_sq + scale) - one) - sigma * scale) / (sigma_sq * sigma);
+        } else {
+            const float a = scale * sinf(theta);
+            const float b = scale * cosf(theta);
+            const float c = theta_sq + sigma * sigma;
+            A = (a * sigma + (one - b) * theta) / (theta * c);
+            B = (C - ((b - one) * sigma + a * theta) / c) / theta_sq;
+        }
+    }
+    t[0] = C * tau[0]; t[1] = C * tau[1]; t[2] = C * tau[2];
+    cross_inplace(phi, tau);
+    t[0] += A * tau[0]; t[1] += A * tau[1]; t[2] += A * tau[2];
+    cross_inplace(phi, tau);
+    t[0] += B * tau[0]; t[1] += B * tau[1]; t[2] += B * tau[2];
+}
+
+// gn_kernels.cu:392-413 (left composition)
+__device__ __forceinline__ void retr_sim3(const float* xi, float* p /* [8], in/out */) {
+    float dt[3] = {0, 0, 0}, dq[4] = {0, 0, 0, 1}, ds = 0;
+    exp_sim3(xi, dt, dq, &ds);
+    const float t[3] = {p[0], p[1], p[2]};
+    const float q[4] = {p[3], p[4], p[5], p[6]};
+    float q1[4], t1[3];
+    quat_comp(dq, q, q1);
+    act_so3(dq, t, t1);
+    t1[0] *= ds; t1[1] *= ds; t1[2] *= ds;
+    t1[0] += dt[0]; t1[1] += dt[1]; t1[2] += dt[2];
+    p[0] = t1[0]; p[1] = t1[1]; p[2] = t1[2];
+    p[3] = q1[0]; p[4] = q1[1]; p[5] = q1[2]; p[6] = q1[3];
+    p[7] = ds * p[7];
+}
+
+}  // namespace m3s

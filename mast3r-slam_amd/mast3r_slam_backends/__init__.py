@@ -1,0 +1,298 @@
+"""mast3r_slam_backends -- MI355X-native drop-in for the reference's pybind11 module.
+
+Same module name, same five ops, same positional signatures and return lists as the
+reference (``/root/reference/mast3r_slam/backend/src/gn.cpp:116-123``; prototypes in
+``gn.h:22-117``), so ``mast3r_slam/matching.py:60,79`` and ``global_opt.py:140,190``
+call it unchanged.  Every op runs the hand-written gfx950 HIP kernels of
+``libm3s_backend.so`` (C ABI: ``include/m3s_backend.h``) on torch's current HIP stream.
+
+There is no CPU fallback: CPU tensors raise ``RuntimeError`` (the reference dispatches
+unconditionally to ``*_cuda`` as well), and a missing library raises ``ImportError`` at
+import time.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+__all__ = [
+    "iter_proj",
+    "refine_matches",
+    "gauss_newton_points",
+    "gauss_newton_rays",
+    "gauss_newton_calib",
+    "library_path",
+    "lib",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+library_path = os.environ.get(
+    "M3S_BACKEND_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libm3s_backend.so")
+)
+
+if not os.path.exists(library_path):
+    raise ImportError(
+        f"mast3r_slam_backends: HIP backend library not found at {library_path}; "
+        "build it with `make -C mast3r-slam_amd` (or __graft_entry__.build())"
+    )
+
+lib = ctypes.CDLL(library_path)
+
+_c_int64 = ctypes.c_int64
+_vp = ctypes.c_void_p
+_f = ctypes.c_float
+_i = ctypes.c_int
+
+lib.m3s_last_error.restype = ctypes.c_char_p
+lib.m3s_version.restype = ctypes.c_char_p
+lib.m3s_iter_proj.argtypes = [_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _vp]
+lib.m3s_refine_matches_f16.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
+lib.m3s_refine_matches_f32.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
+lib.m3s_gn_workspace_bytes.restype = ctypes.c_size_t
+lib.m3s_gn_workspace_bytes.argtypes = [_i, _c_int64, _c_int64, _c_int64, _c_int64]
+
+
+class GNArgs(ctypes.Structure):
+    """Mirror of ``m3s_gn_args`` (include/m3s_backend.h)."""
+
+    _fields_ = [
+        ("mode", _i),
+        ("Twc", _vp),
+        ("Xs", _vp),
+        ("Cs", _vp),
+        ("ii", _vp),
+        ("jj", _vp),
+        ("idx", _vp),
+        ("valid", _vp),
+        ("Q", _vp),
+        ("N", _c_int64),
+        ("HW", _c_int64),
+        ("E_total", _c_int64),
+        ("E_local", _c_int64),
+        ("edge_offset", _c_int64),
+        ("sigma0", _f),
+        ("sigma1", _f),
+        ("C_thresh", _f),
+        ("Q_thresh", _f),
+        ("K", _vp),
+        ("height", _i),
+        ("width", _i),
+        ("pixel_border", _i),
+        ("z_eps", _f),
+        ("max_iter", _i),
+        ("delta_thresh", _f),
+        ("dx", _vp),
+        ("ws", _vp),
+        ("ws_bytes", ctypes.c_size_t),
+        ("comm", _vp),
+        ("stream", _vp),
+    ]
+
+
+lib.m3s_gauss_newton.argtypes = [ctypes.POINTER(GNArgs)]
+lib.m3s_gn_build_system.argtypes = [ctypes.POINTER(GNArgs), _vp, _vp]
+lib.m3s_comm_get_unique_id.argtypes = [_vp]
+lib.m3s_comm_init.argtypes = [_vp, _i, _i, ctypes.POINTER(_vp)]
+lib.m3s_comm_destroy.argtypes = [_vp]
+
+GN_POINTS, GN_RAYS, GN_CALIB = 0, 1, 2
+
+# ---------------------------------------------------------------------------------
+# argument checks (the reference's TORCH_CHECK / packed_accessor32 behaviour)
+# ---------------------------------------------------------------------------------
+
+_DT_NAME = {
+    torch.float32: "Float",
+    torch.float16: "Half",
+    torch.float64: "Double",
+    torch.int64: "Long",
+    torch.int32: "Int",
+    torch.bool: "Bool",
+    torch.uint8: "Byte",
+}
+
+
+def _check(t, name, dtype, ndim, device=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_contiguous():  # CHECK_CONTIGUOUS (gn.h:5)
+        raise RuntimeError(f"{name} must be contiguous")
+    dts = dtype if isinstance(dtype, tuple) else (dtype,)
+    if t.dtype not in dts:
+        raise RuntimeError(
+            f"expected scalar type {_DT_NAME.get(dts[0], dts[0])} but found "
+            f"{_DT_NAME.get(t.dtype, t.dtype)} ({name})"
+        )
+    if t.dim() != ndim:
+        raise RuntimeError(f"packed_accessor32 expects {ndim} dims but tensor has {t.dim()} ({name})")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{name} must be a HIP (cuda) tensor: mast3r_slam_backends has no CPU path"
+        )
+    if device is not None and t.device != device:
+        raise RuntimeError(f"{name} must be on {device}, got {t.device}")
+
+
+def _raise(rc, what):
+    if rc != 0:
+        msg = lib.m3s_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg} (code {rc})")
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+# ---------------------------------------------------------------------------------
+# matching ops
+# ---------------------------------------------------------------------------------
+
+
+def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh):
+    """gn.cpp:84-99 / matching_kernels.cu:279-316 -> [p_new f32[B,N,2], converged bool[B,N]]."""
+    _check(rays_img_with_grad, "rays_img_with_grad", torch.float32, 4)
+    dev = rays_img_with_grad.device
+    _check(pts_3d_norm, "pts_3d_norm", torch.float32, 3, dev)
+    _check(p_init, "p_init", torch.float32, 3, dev)
+    B, H, W, C = rays_img_with_grad.shape
+    if C != 9:
+        raise RuntimeError(f"rays_img_with_grad must have 9 channels (ray, d/du, d/dv), got {C}")
+    Bp, N = p_init.shape[0], p_init.shape[1]
+    if p_init.shape[2] != 2 or pts_3d_norm.shape[2] != 3:
+        raise RuntimeError("p_init must be [B,N,2] and pts_3d_norm [B,N,3]")
+    if pts_3d_norm.shape[:2] != p_init.shape[:2] or Bp != B:
+        raise RuntimeError("batch / point counts of rays_img_with_grad, pts_3d_norm, p_init differ")
+    p_new = torch.zeros((Bp, N, 2), dtype=p_init.dtype, device=dev)
+    converged = torch.zeros((Bp, N), dtype=torch.bool, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.m3s_iter_proj(
+            _ptr(rays_img_with_grad), _ptr(pts_3d_norm), _ptr(p_init), _ptr(p_new),
+            _ptr(converged), B, H, W, N, int(max_iter), float(lambda_init),
+            float(cost_thresh), _stream(dev),
+        )
+    _raise(rc, "iter_proj")
+    return [p_new, converged]
+
+
+def refine_matches(D11, D21, p1, window_size, dilation_max):
+    """gn.cpp:101-114 / matching_kernels.cu:84-116 -> [p1_new i64[B,N,2]].
+
+    ``window_size`` is the search radius (config ``matching.radius``)."""
+    _check(D11, "D11", (torch.float16, torch.float32), 4)
+    dev = D11.device
+    _check(D21, "D21", D11.dtype, 3, dev)
+    _check(p1, "p1", torch.int64, 3, dev)
+    B, H, W, F = D11.shape
+    Bq, N = p1.shape[0], p1.shape[1]
+    if p1.shape[2] != 2 or D21.shape[0] != Bq or D21.shape[1] != N or D21.shape[2] != F or Bq != B:
+        raise RuntimeError("refine_matches: expected D11 [B,H,W,F], D21 [B,N,F], p1 [B,N,2]")
+    p1_new = torch.zeros((Bq, N, 2), dtype=p1.dtype, device=dev)
+    fn = lib.m3s_refine_matches_f16 if D11.dtype == torch.float16 else lib.m3s_refine_matches_f32
+    with torch.cuda.device(dev):
+        rc = fn(
+            _ptr(D11), _ptr(D21), _ptr(p1), _ptr(p1_new), B, H, W, N, F,
+            int(window_size), int(dilation_max), _stream(dev),
+        )
+    _raise(rc, "refine_matches")
+    return [p1_new]
+
+
+# ---------------------------------------------------------------------------------
+# Gauss-Newton ops
+# ---------------------------------------------------------------------------------
+
+
+def _gn_common_checks(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, edge_local=None):
+    _check(Twc, "Twc", torch.float32, 2)
+    dev = Twc.device
+    _check(Xs, "Xs", torch.float32, 3, dev)
+    _check(Cs, "Cs", torch.float32, 3, dev)
+    _check(ii, "ii", torch.int64, 1, dev)
+    _check(jj, "jj", torch.int64, 1, dev)
+    _check(idx_ii2jj, "idx_ii2jj", torch.int64, 2, dev)
+    _check(valid_match, "valid_match", torch.bool, 3, dev)
+    _check(Q, "Q", torch.float32, 3, dev)
+    N, HW = Xs.shape[0], Xs.shape[1]
+    E = ii.shape[0]
+    El = E if edge_local is None else edge_local
+    if Twc.shape != (N, 8) or Xs.shape[2] != 3 or Cs.shape != (N, HW, 1):
+        raise RuntimeError("gauss_newton: expected Twc [N,8], Xs [N,HW,3], Cs [N,HW,1]")
+    if jj.shape[0] != E:
+        raise RuntimeError("gauss_newton: ii and jj differ in length")
+    if idx_ii2jj.shape != (El, HW) or valid_match.shape != (El, HW, 1) or Q.shape != (El, HW, 1):
+        raise RuntimeError(
+            "gauss_newton: expected idx_ii2jj [E,HW], valid_match [E,HW,1], Q [E,HW,1]"
+        )
+    return dev, N, HW, E
+
+
+def _run_gn(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter, delta_thresh,
+            sigma0, sigma1, C_thresh, Q_thresh, K=None, height=0, width=0, pixel_border=0,
+            z_eps=0.0, comm=None, edge_offset=0, edge_total=None):
+    E_local = idx_ii2jj.shape[0]
+    dev, N, HW, E = _gn_common_checks(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, E_local)
+    if edge_total is not None and edge_total != E:
+        raise RuntimeError("gauss_newton: edge_total must equal len(ii)")
+    if K is not None:
+        _check(K, "K", torch.float32, 2, dev)
+        if K.shape != (3, 3):
+            raise RuntimeError("K must be [3,3]")
+    max_iter = int(max_iter)
+    dx = torch.zeros((max(N - 1, 0), 7), dtype=torch.float32, device=dev)
+    ws_bytes = lib.m3s_gn_workspace_bytes(mode, N, HW, E, E_local)
+    ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
+    a = GNArgs()
+    a.mode = mode
+    a.Twc, a.Xs, a.Cs = Twc.data_ptr(), Xs.data_ptr(), Cs.data_ptr()
+    a.ii, a.jj = ii.data_ptr(), jj.data_ptr()
+    a.idx, a.valid, a.Q = idx_ii2jj.data_ptr(), valid_match.data_ptr(), Q.data_ptr()
+    a.N, a.HW, a.E_total, a.E_local, a.edge_offset = N, HW, E, E_local, int(edge_offset)
+    a.sigma0, a.sigma1 = float(sigma0), float(sigma1)
+    a.C_thresh, a.Q_thresh = float(C_thresh), float(Q_thresh)
+    a.K = K.data_ptr() if K is not None else None
+    a.height, a.width, a.pixel_border = int(height), int(width), int(pixel_border)
+    a.z_eps = float(z_eps)
+    a.max_iter = max_iter
+    a.delta_thresh = float(delta_thresh)
+    a.dx = dx.data_ptr()
+    a.ws, a.ws_bytes = ws.data_ptr(), ws_bytes
+    a.comm = comm
+    with torch.cuda.device(dev):
+        a.stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = lib.m3s_gauss_newton(ctypes.byref(a))
+    _raise(rc, "gauss_newton")
+    # the reference returns an undefined tensor when no iteration ran
+    return [dx if max_iter > 0 else None]
+
+
+def gauss_newton_points(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, sigma_point, C_thresh,
+                        Q_thresh, max_iter, delta_thresh):
+    """gn.cpp:3-26 -> [dx].  Twc is updated in place."""
+    return _run_gn(GN_POINTS, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter,
+                   delta_thresh, sigma_point, 0.0, C_thresh, Q_thresh)
+
+
+def gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, sigma_ray, sigma_dist,
+                      C_thresh, Q_thresh, max_iter, delta_thresh):
+    """gn.cpp:28-52 -> [dx].  Twc is updated in place."""
+    return _run_gn(GN_RAYS, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter,
+                   delta_thresh, sigma_ray, sigma_dist, C_thresh, Q_thresh)
+
+
+def gauss_newton_calib(Twc, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q, height, width,
+                       pixel_border, z_eps, sigma_pixel, sigma_depth, C_thresh, Q_thresh,
+                       max_iter, delta_thresh):
+    """gn.cpp:54-82 -> [dx].  Twc is updated in place."""
+    return _run_gn(GN_CALIB, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter,
+                   delta_thresh, sigma_pixel, sigma_depth, C_thresh, Q_thresh, K=K,
+                   height=height, width=width, pixel_border=pixel_border, z_eps=z_eps)
+
+
+def version() -> str:
+    return lib.m3s_version().decode()

@@ -1,0 +1,851 @@
+/*
+ * m3s_oracle.c -- CPU restatement of the MASt3R-SLAM backend hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (parity checker + timed CPU baseline); see
+ * m3s_oracle.h for the parity status and the numerics convention.
+ * Built by oracle/Makefile with -ffp-contract=off.
+ *
+ * Every function cites the reference lines it restates
+ * (/root/reference/mast3r_slam/backend/src/...).
+ */
+#include "m3s_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define EPS 1e-6 /* gn_kernels.cu:34 (a double literal) */
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* ------------------------------------------------------------------------ */
+/* fp16 (c10::Half) helpers                                                 */
+/* ------------------------------------------------------------------------ */
+
+float oracle_f16_to_f32(uint16_t h) {
+    uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t ex = (h >> 10) & 0x1fu;
+    uint32_t man = h & 0x3ffu;
+    uint32_t bits;
+    if (ex == 0x1f) {
+        bits = sign | 0x7f800000u | (man << 13);
+    } else if (ex == 0) {
+        /* zero or subnormal: value = man * 2^-24, exact in float */
+        float v = (float)man * 5.9604644775390625e-8f;
+        memcpy(&bits, &v, 4);
+        bits |= sign;
+    } else {
+        bits = sign | ((ex + 112u) << 23) | (man << 13);
+    }
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+
+uint16_t oracle_f32_to_f16(float f) {
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    uint16_t sign = (uint16_t)((x >> 16) & 0x8000u);
+    uint32_t ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) { /* inf / nan */
+        if (ax == 0x7f800000u) return sign | 0x7c00u;
+        return sign | 0x7e00u | (uint16_t)((ax >> 13) & 0x3ffu);
+    }
+    if (ax >= 0x477ff000u) return sign | 0x7c00u; /* >= 65520 rounds to inf */
+    if (ax < 0x38800000u) {                       /* below 2^-14: subnormal half */
+        float a;
+        memcpy(&a, &ax, 4);
+        float m = nearbyintf(a * 16777216.0f); /* exact scaling, RNE */
+        return sign | (uint16_t)m;
+    }
+    uint32_t man = ax & 0x7fffffu;
+    uint32_t ex = (ax >> 23) - 112u;
+    uint32_t h = (ex << 10) | (man >> 13);
+    uint32_t rem = man & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return sign | (uint16_t)h;
+}
+
+/* c10::Half a*b and a+b: compute in float, round to half (exact products). */
+static inline uint16_t hmul(uint16_t a, uint16_t b) {
+    return oracle_f32_to_f16(oracle_f16_to_f32(a) * oracle_f16_to_f32(b));
+}
+static inline uint16_t hadd(uint16_t a, uint16_t b) {
+    return oracle_f32_to_f16(oracle_f16_to_f32(a) + oracle_f16_to_f32(b));
+}
+
+/* ------------------------------------------------------------------------ */
+/* iter_proj  (matching_kernels.cu:119-275)                                 */
+/* ------------------------------------------------------------------------ */
+
+/* matching_kernels.cu:21-23 */
+static inline float clampf_ref(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+/* matching_kernels.cu:155-183 (bilinear interpolation of C channels) */
+static inline void bilinear(const float* img, int64_t W, float u, float v, int C, float* out) {
+    int u11 = (int)floorf(u);
+    int v11 = (int)floorf(v);
+    float du = u - (float)u11;
+    float dv = v - (float)v11;
+    /* double literal 1.0 promotes these three weights (matching_kernels.cu:161-164) */
+    float w11 = du * dv;
+    float w12 = (float)((1.0 - (double)du) * (double)dv);
+    float w21 = (float)((double)du * (1.0 - (double)dv));
+    float w22 = (float)((1.0 - (double)du) * (1.0 - (double)dv));
+    /* "Pixels are opposite the area calc" (matching_kernels.cu:166-170) */
+    const float* r11 = img + ((int64_t)(v11 + 1) * W + (u11 + 1)) * 9;
+    const float* r12 = img + ((int64_t)(v11 + 1) * W + u11) * 9;
+    const float* r21 = img + ((int64_t)v11 * W + (u11 + 1)) * 9;
+    const float* r22 = img + ((int64_t)v11 * W + u11) * 9;
+    for (int j = 0; j < C; j++) {
+        float a = w11 * r11[j];
+        float b = w12 * r12[j];
+        float c = w21 * r21[j];
+        float d = w22 * r22[j];
+        out[j] = ((a + b) + c) + d;
+    }
+}
+
+void oracle_iter_proj(const float* rays, const float* pts, const float* p_init,
+                      float* p_new, uint8_t* converged,
+                      int64_t B, int64_t H, int64_t W, int64_t N,
+                      int max_iter, float lambda_init, float cost_thresh) {
+    const int64_t total = B * N;
+#pragma omp parallel for schedule(static)
+    for (int64_t g = 0; g < total; g++) {
+        const int64_t b = g / N;
+        const float* img = rays + b * H * W * 9;
+        float u = p_init[g * 2 + 0];
+        float v = p_init[g * 2 + 1];
+        u = clampf_ref(u, 1.0f, (float)(W - 2)); /* :143-144 */
+        v = clampf_ref(v, 1.0f, (float)(H - 2));
+        const float px = pts[g * 3 + 0], py = pts[g * 3 + 1], pz = pts[g * 3 + 2];
+        float lambda = lambda_init;
+        uint8_t conv = 0; /* torch::zeros init (:300-301) */
+        for (int i = 0; i < max_iter; i++) {
+            float s[9];
+            bilinear(img, W, u, v, 9, s);
+            float r0 = s[0], r1 = s[1], r2 = s[2];
+            const float gx0 = s[3], gx1 = s[4], gx2 = s[5];
+            const float gy0 = s[6], gy1 = s[7], gy2 = s[8];
+            /* :186-191 normalise */
+            float r_norm = sqrtf((r0 * r0 + r1 * r1) + r2 * r2);
+            float r_norm_inv = (float)(1.0 / (double)r_norm);
+            r0 *= r_norm_inv;
+            r1 *= r_norm_inv;
+            r2 *= r_norm_inv;
+            /* :194-198 error + cost */
+            float e0 = r0 - px, e1 = r1 - py, e2 = r2 - pz;
+            float cost = (e0 * e0 + e1 * e1) + e2 * e2;
+            /* :202-210 normal equations */
+            float A00 = (gx0 * gx0 + gx1 * gx1) + gx2 * gx2;
+            float A01 = (gx0 * gy0 + gx1 * gy1) + gx2 * gy2;
+            float A11 = (gy0 * gy0 + gy1 * gy1) + gy2 * gy2;
+            float b0 = -((e0 * gx0 + e1 * gx1) + e2 * gx2);
+            float b1 = -((e0 * gy0 + e1 * gy1) + e2 * gy2);
+            A00 += lambda;
+            A11 += lambda;
+            /* :213-215 */
+            float det_inv = (float)(1.0 / (double)(A00 * A11 - A01 * A01));
+            float delta_u = det_inv * (A11 * b0 - A01 * b1);
+            float delta_v = det_inv * ((-A01) * b0 + A00 * b1);
+            /* :218-221 */
+            float u_new = clampf_ref(u + delta_u, 1.0f, (float)(W - 2));
+            float v_new = clampf_ref(v + delta_v, 1.0f, (float)(H - 2));
+            /* :225-256 cost at the new pixel (ray channels only) */
+            float t[3];
+            bilinear(img, W, u_new, v_new, 3, t);
+            float n2 = sqrtf((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2]);
+            float n2_inv = (float)(1.0 / (double)n2);
+            float f0 = t[0] * n2_inv - px, f1 = t[1] * n2_inv - py, f2 = t[2] * n2_inv - pz;
+            float new_cost = (f0 * f0 + f1 * f1) + f2 * f2;
+            /* :259-268  lambda *= 0.1 is a DOUBLE multiply (0.1 != 0.1f) */
+            if (new_cost < cost) {
+                u = u_new;
+                v = v_new;
+                lambda = (float)((double)lambda * 0.1);
+                conv = new_cost < cost_thresh;
+            } else {
+                lambda = (float)((double)lambda * 10.0);
+                conv = cost < cost_thresh;
+            }
+        }
+        p_new[g * 2 + 0] = u;
+        p_new[g * 2 + 1] = v;
+        converged[g] = conv;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* refine_matches  (matching_kernels.cu:25-81)                              */
+/* ------------------------------------------------------------------------ */
+
+/* The reference initialises max_score with cuda::std::numeric_limits<c10::Half>::min();
+ * libcu++ has no specialisation for c10::Half, so that is a value-initialised Half:
+ * 0.0 (SURVEY.md §7.3 hard part 1).  Only strictly positive scores can move a match. */
+#define REFINE_MAX_SCORE_INIT 0.0f
+
+static inline int inside_image(int64_t u, int64_t v, int64_t W, int64_t H) {
+    return v >= 0 && v < H && u >= 0 && u < W; /* matching_kernels.cu:17-19 */
+}
+
+void oracle_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
+                               const int64_t* p1, int64_t* p1_new,
+                               int64_t B, int64_t H, int64_t W, int64_t N,
+                               int64_t F, int radius, int dilation_max) {
+    const int64_t total = B * N;
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t g = 0; g < total; g++) {
+        const int64_t b = g / N;
+        const uint16_t* d21 = D21 + g * F;
+        int64_t u0 = p1[g * 2 + 0];
+        int64_t v0 = p1[g * 2 + 1];
+        uint16_t max_score = oracle_f32_to_f16(REFINE_MAX_SCORE_INIT);
+        int64_t u_new = u0, v_new = v0;
+        for (int d = dilation_max; d > 0; d--) {
+            const int rd = radius * d;
+            const int diam = 2 * rd + 1;
+            for (int i = 0; i < diam; i += d) {     /* u offset outer */
+                for (int j = 0; j < diam; j += d) { /* v offset inner */
+                    const int64_t u = u0 - rd + i;
+                    const int64_t v = v0 - rd + j;
+                    if (inside_image(u, v, W, H)) {
+                        const uint16_t* d11 = D11 + ((b * H + v) * W + u) * F;
+                        uint16_t score = 0; /* scalar_t score = 0.0 */
+                        for (int64_t k = 0; k < F; k++) score = hadd(score, hmul(d21[k], d11[k]));
+                        if (oracle_f16_to_f32(score) > oracle_f16_to_f32(max_score)) {
+                            max_score = score;
+                            u_new = u;
+                            v_new = v;
+                        }
+                    }
+                }
+            }
+            u0 = u_new; /* :75-76 the window re-centres on the winner */
+            v0 = v_new;
+        }
+        p1_new[g * 2 + 0] = u_new;
+        p1_new[g * 2 + 1] = v_new;
+    }
+}
+
+void oracle_refine_matches_f32(const float* D11, const float* D21,
+                               const int64_t* p1, int64_t* p1_new,
+                               int64_t B, int64_t H, int64_t W, int64_t N,
+                               int64_t F, int radius, int dilation_max) {
+    const int64_t total = B * N;
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t g = 0; g < total; g++) {
+        const int64_t b = g / N;
+        const float* d21 = D21 + g * F;
+        int64_t u0 = p1[g * 2 + 0];
+        int64_t v0 = p1[g * 2 + 1];
+        /* For scalar_t = float the limits ARE specialised: min() = FLT_MIN. */
+        float max_score = 1.17549435e-38f;
+        int64_t u_new = u0, v_new = v0;
+        for (int d = dilation_max; d > 0; d--) {
+            const int rd = radius * d;
+            const int diam = 2 * rd + 1;
+            for (int i = 0; i < diam; i += d) {
+                for (int j = 0; j < diam; j += d) {
+                    const int64_t u = u0 - rd + i;
+                    const int64_t v = v0 - rd + j;
+                    if (inside_image(u, v, W, H)) {
+                        const float* d11 = D11 + ((b * H + v) * W + u) * F;
+                        float score = 0.0f;
+                        for (int64_t k = 0; k < F; k++) score += d21[k] * d11[k];
+                        if (score > max_score) {
+                            max_score = score;
+                            u_new = u;
+                            v_new = v;
+                        }
+                    }
+                }
+            }
+            u0 = u_new;
+            v0 = v_new;
+        }
+        p1_new[g * 2 + 0] = u_new;
+        p1_new[g * 2 + 1] = v_new;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Sim3 device library (gn_kernels.cu:172-413), restated in float           */
+/* ------------------------------------------------------------------------ */
+
+/* gn_kernels.cu:172-175 (double literal 1.345) */
+static inline float huber(float r) {
+    const float r_abs = fabsf(r);
+    return (double)r_abs < 1.345 ? 1.0f : (float)(1.345 / (double)r_abs);
+}
+
+/* :178-184  qi * qj, quaternion [x,y,z,w] */
+static inline void quat_comp(const float* qi, const float* qj, float* out) {
+    float o0 = ((qi[3] * qj[0] + qi[0] * qj[3]) + qi[1] * qj[2]) - qi[2] * qj[1];
+    float o1 = ((qi[3] * qj[1] - qi[0] * qj[2]) + qi[1] * qj[3]) + qi[2] * qj[0];
+    float o2 = ((qi[3] * qj[2] + qi[0] * qj[1]) - qi[1] * qj[0]) + qi[2] * qj[3];
+    float o3 = ((qi[3] * qj[3] - qi[0] * qj[0]) - qi[1] * qj[1]) - qi[2] * qj[2];
+    out[0] = o0; out[1] = o1; out[2] = o2; out[3] = o3;
+}
+
+static inline void quat_inv(const float* q, float* out) { /* :187-193 */
+    out[0] = -q[0]; out[1] = -q[1]; out[2] = -q[2]; out[3] = q[3];
+}
+
+/* :195-205; safe for X == Y (each Y[k] reads only X[k] and uv) */
+static inline void actSO3(const float* q, const float* X, float* Y) {
+    float uv0 = (float)(2.0 * (double)(q[1] * X[2] - q[2] * X[1]));
+    float uv1 = (float)(2.0 * (double)(q[2] * X[0] - q[0] * X[2]));
+    float uv2 = (float)(2.0 * (double)(q[0] * X[1] - q[1] * X[0]));
+    float y0 = (X[0] + q[3] * uv0) + (q[1] * uv2 - q[2] * uv1);
+    float y1 = (X[1] + q[3] * uv1) + (q[2] * uv0 - q[0] * uv2);
+    float y2 = (X[2] + q[3] * uv2) + (q[0] * uv1 - q[1] * uv0);
+    Y[0] = y0; Y[1] = y1; Y[2] = y2;
+}
+
+/* :207-219 */
+static inline void actSim3(const float* t, const float* q, const float* s, const float* X, float* Y) {
+    actSO3(q, X, Y);
+    Y[0] *= s[0]; Y[1] *= s[0]; Y[2] *= s[0];
+    Y[0] += t[0]; Y[1] += t[1]; Y[2] += t[2];
+}
+
+/* :229-240 b <- a x b */
+static inline void crossInplace(const float* a, float* b) {
+    float x0 = a[1] * b[2] - a[2] * b[1];
+    float x1 = a[2] * b[0] - a[0] * b[2];
+    float x2 = a[0] * b[1] - a[1] * b[0];
+    b[0] = x0; b[1] = x1; b[2] = x2;
+}
+
+static inline float dot3(const float* t, const float* s) { return (t[0] * s[0] + t[1] * s[1]) + t[2] * s[2]; }
+static inline float squared_norm3(const float* v) { return (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]; }
+
+/* :252-272  T_ij = T_i^{-1} T_j */
+static void relSim3(const float* ti, const float* qi, const float* si,
+                    const float* tj, const float* qj, const float* sj,
+                    float* tij, float* qij, float* sij) {
+    float si_inv = (float)(1.0 / (double)si[0]);
+    sij[0] = si_inv * sj[0];
+    float qi_inv[4];
+    quat_inv(qi, qi_inv);
+    quat_comp(qi_inv, qj, qij);
+    tij[0] = tj[0] - ti[0];
+    tij[1] = tj[1] - ti[1];
+    tij[2] = tj[2] - ti[2];
+    actSO3(qi_inv, tij, tij);
+    tij[0] *= si_inv; tij[1] *= si_inv; tij[2] *= si_inv;
+}
+
+/* :277-297  Y = X * Adj(T)^{-1} for a row vector X (tangent order tau, phi, sigma) */
+void oracle_apply_sim3_adj_inv(const float* t, const float* q, const float* s, const float* X, float* Y) {
+    const float s_inv = (float)(1.0 / (double)s[0]);
+    float Ra[3];
+    actSO3(q, &X[0], Ra);
+    Y[0] = s_inv * Ra[0];
+    Y[1] = s_inv * Ra[1];
+    Y[2] = s_inv * Ra[2];
+    actSO3(q, &X[3], &Y[3]);
+    Y[3] += s_inv * (t[1] * Ra[2] - t[2] * Ra[1]);
+    Y[4] += s_inv * (t[2] * Ra[0] - t[0] * Ra[2]);
+    Y[5] += s_inv * (t[0] * Ra[1] - t[1] * Ra[0]);
+    Y[6] = X[6] + (s_inv * dot3(t, Ra));
+}
+
+/* :299-321 */
+static void expSO3(const float* phi, float* q) {
+    float theta_sq = (phi[0] * phi[0] + phi[1] * phi[1]) + phi[2] * phi[2];
+    float imag, real;
+    if ((double)theta_sq < EPS) {
+        float theta_p4 = theta_sq * theta_sq;
+        imag = (float)((0.5 - (1.0 / 48.0) * (double)theta_sq) + (1.0 / 3840.0) * (double)theta_p4);
+        real = (float)((1.0 - (1.0 / 8.0) * (double)theta_sq) + (1.0 / 384.0) * (double)theta_p4);
+    } else {
+        float theta = sqrtf(theta_sq);
+        imag = sinf((float)(0.5 * (double)theta)) / theta;
+        real = cosf((float)(0.5 * (double)theta));
+    }
+    q[0] = imag * phi[0];
+    q[1] = imag * phi[1];
+    q[2] = imag * phi[2];
+    q[3] = real;
+}
+
+/* :323-390 (including the as-written "B = (C - ...)" at :371) */
+void oracle_exp_sim3(const float* xi, float* t, float* q, float* s) {
+    float tau[3] = {xi[0], xi[1], xi[2]};
+    float phi[3] = {xi[3], xi[4], xi[5]};
+    float sigma = xi[6];
+    float scale = expf(sigma);
+    expSO3(phi, q);
+    s[0] = scale;
+    float theta_sq = (phi[0] * phi[0] + phi[1] * phi[1]) + phi[2] * phi[2];
+    float theta = sqrtf(theta_sq);
+    float A, B, C;
+    const float one = 1.0f;
+    const float half = 0.5f;
+    if ((double)fabsf(sigma) < EPS) {
+        C = one;
+        if ((double)fabsf(theta) < EPS) {
+            A = half;
+            B = (float)(1.0 / 6.0);
+        } else {
+            A = (one - cosf(theta)) / theta_sq;
+            B = (theta - sinf(theta)) / (theta_sq * theta);
+        }
+    } else {
+        C = (scale - one) / sigma;
+        if ((double)fabsf(theta) < EPS) {
+            float sigma_sq = sigma * sigma;
+            A = ((sigma - one) * scale + one) / sigma_sq;
+            B = ((((scale * half) * sigma_sq + scale) - one) - sigma * scale) / (sigma_sq * sigma);
+        } else {
+            float a = scale * sinf(theta);
+            float b = scale * cosf(theta);
+            float c = theta_sq + sigma * sigma;
+            A = (a * sigma + (one - b) * theta) / (theta * c);
+            B = (C - ((b - one) * sigma + a * theta) / (c)) / (theta_sq);
+        }
+    }
+    t[0] = C * tau[0];
+    t[1] = C * tau[1];
+    t[2] = C * tau[2];
+    crossInplace(phi, tau);
+    t[0] += A * tau[0];
+    t[1] += A * tau[1];
+    t[2] += A * tau[2];
+    crossInplace(phi, tau);
+    t[0] += B * tau[0];
+    t[1] += B * tau[1];
+    t[2] += B * tau[2];
+}
+
+/* :392-413 left-composition retraction */
+void oracle_retr_sim3(const float* xi, const float* t, const float* q, const float* s,
+                      float* t1, float* q1, float* s1) {
+    float dt[3] = {0, 0, 0};
+    float dq[4] = {0, 0, 0, 1};
+    float ds[1] = {0};
+    oracle_exp_sim3(xi, dt, dq, ds);
+    quat_comp(dq, q, q1);
+    actSO3(dq, t, t1);
+    t1[0] *= ds[0]; t1[1] *= ds[0]; t1[2] *= ds[0];
+    t1[0] += dt[0]; t1[1] += dt[1]; t1[2] += dt[2];
+    s1[0] = ds[0] * s[0];
+}
+
+/* :415-453 */
+void oracle_pose_retr(float* Twc, const float* dx, int64_t N, int num_fix) {
+    for (int64_t k = num_fix; k < N; k++) {
+        float* p = Twc + k * 8;
+        float t[3] = {p[0], p[1], p[2]};
+        float q[4] = {p[3], p[4], p[5], p[6]};
+        float s[1] = {p[7]};
+        float xi[7];
+        for (int n = 0; n < 7; n++) xi[n] = dx[(k - num_fix) * 7 + n];
+        float t1[3], q1[4], s1[1];
+        oracle_retr_sim3(xi, t, q, s, t1, q1, s1);
+        p[0] = t1[0]; p[1] = t1[1]; p[2] = t1[2];
+        p[3] = q1[0]; p[4] = q1[1]; p[5] = q1[2]; p[6] = q1[3];
+        p[7] = s1[0];
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Alignment kernels (gn_kernels.cu:455-723, 813-1138, 1231-1543)           */
+/* ------------------------------------------------------------------------ */
+
+#define THREADS 256
+#define HDIM 105 /* 14*15/2 */
+#define NACC (HDIM + 14)
+
+/* blockReduce + warpReduce (gn_kernels.cu:36-55): 256 -> 128 -> 64 -> 32, then a
+ * lock-step warp tree (every lane reads before any lane writes). */
+static float block_reduce(float* s) {
+    for (int t = 0; t < 128; t++) s[t] += s[t + 128];
+    for (int t = 0; t < 64; t++) s[t] += s[t + 64];
+    for (int t = 0; t < 32; t++) s[t] += s[t + 32];
+    for (int o = 16; o >= 1; o >>= 1) {
+        float tmp[32];
+        for (int t = 0; t < 32; t++) tmp[t] = s[t] + s[t + o];
+        for (int t = 0; t < 32; t++) s[t] = tmp[t];
+    }
+    return s[0];
+}
+
+/* Accumulate one residual row: Jx = [Ji, Jj], Ji = -Jj after the adjoint
+ * (gn_kernels.cu:999-1013). */
+static inline void accum_row(float* acc, const float* ti, const float* qi, const float* si,
+                             float* Jx, float w, float err) {
+    float* Ji = &Jx[0];
+    float* Jj = &Jx[7];
+    oracle_apply_sim3_adj_inv(ti, qi, si, Ji, Jj);
+    for (int n = 0; n < 7; n++) Ji[n] = -Jj[n];
+    int l = 0;
+    for (int n = 0; n < 14; n++) {
+        for (int m = 0; m <= n; m++) {
+            acc[l] += (w * Jx[n]) * Jx[m];
+            l++;
+        }
+    }
+    float* vi = acc + HDIM;
+    float* vj = acc + HDIM + 7;
+    for (int n = 0; n < 7; n++) {
+        vi[n] += (w * err) * Ji[n];
+        vj[n] += (w * err) * Jj[n];
+    }
+}
+
+static void align_point(const oracle_gn_params* P, const float* ti, const float* qi, const float* si,
+                        const float* tij, const float* qij, const float* sij,
+                        const float* Xi, const float* Xj, float q, float ci, float cj,
+                        int valid_match_ind, int64_t ind_Xi, float* acc) {
+    float Xj_Ci[3];
+    float Jx[14];
+    float* Ji = &Jx[0];
+    actSim3(tij, qij, sij, Xj, Xj_Ci);
+    if (P->mode == ORACLE_GN_RAYS) {
+        /* gn_kernels.cu:924-1089 */
+        const float sigma_ray_inv = (float)(1.0 / (double)P->sigma0);
+        const float sigma_dist_inv = (float)(1.0 / (double)P->sigma1);
+        const float norm2_i = squared_norm3(Xi);
+        const float norm1_i = sqrtf(norm2_i);
+        const float norm1_i_inv = (float)(1.0 / (double)norm1_i);
+        float ri[3];
+        for (int i = 0; i < 3; i++) ri[i] = norm1_i_inv * Xi[i];
+        const float norm2_j = squared_norm3(Xj_Ci);
+        const float norm1_j = sqrtf(norm2_j);
+        const float norm1_j_inv = (float)(1.0 / (double)norm1_j);
+        float rj[3];
+        for (int i = 0; i < 3; i++) rj[i] = norm1_j_inv * Xj_Ci[i];
+        float err[4], w[4];
+        err[0] = rj[0] - ri[0];
+        err[1] = rj[1] - ri[1];
+        err[2] = rj[2] - ri[2];
+        err[3] = norm1_j - norm1_i;
+        const int valid = valid_match_ind & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh);
+        const float sqrt_w_ray = valid ? sigma_ray_inv * sqrtf(q) : 0.0f;
+        const float sqrt_w_dist = valid ? sigma_dist_inv * sqrtf(q) : 0.0f;
+        w[0] = huber(sqrt_w_ray * err[0]);
+        w[1] = huber(sqrt_w_ray * err[1]);
+        w[2] = huber(sqrt_w_ray * err[2]);
+        w[3] = huber(sqrt_w_dist * err[3]);
+        const float w_const_ray = sqrt_w_ray * sqrt_w_ray;
+        const float w_const_dist = sqrt_w_dist * sqrt_w_dist;
+        w[0] *= w_const_ray;
+        w[1] *= w_const_ray;
+        w[2] *= w_const_ray;
+        w[3] *= w_const_dist;
+        const float norm3_j_inv = norm1_j_inv / norm2_j;
+        const float drx_dPx = norm1_j_inv - (Xj_Ci[0] * Xj_Ci[0]) * norm3_j_inv;
+        const float dry_dPy = norm1_j_inv - (Xj_Ci[1] * Xj_Ci[1]) * norm3_j_inv;
+        const float drz_dPz = norm1_j_inv - (Xj_Ci[2] * Xj_Ci[2]) * norm3_j_inv;
+        const float drx_dPy = ((-Xj_Ci[0]) * Xj_Ci[1]) * norm3_j_inv;
+        const float drx_dPz = ((-Xj_Ci[0]) * Xj_Ci[2]) * norm3_j_inv;
+        const float dry_dPz = ((-Xj_Ci[1]) * Xj_Ci[2]) * norm3_j_inv;
+        Ji[0] = drx_dPx; Ji[1] = drx_dPy; Ji[2] = drx_dPz;
+        Ji[3] = 0.0f; Ji[4] = rj[2]; Ji[5] = -rj[1]; Ji[6] = 0.0f;
+        accum_row(acc, ti, qi, si, Jx, w[0], err[0]);
+        Ji[0] = drx_dPy; Ji[1] = dry_dPy; Ji[2] = dry_dPz;
+        Ji[3] = -rj[2]; Ji[4] = 0.0f; Ji[5] = rj[0]; Ji[6] = 0.0f;
+        accum_row(acc, ti, qi, si, Jx, w[1], err[1]);
+        Ji[0] = drx_dPz; Ji[1] = dry_dPz; Ji[2] = drz_dPz;
+        Ji[3] = rj[1]; Ji[4] = -rj[0]; Ji[5] = 0.0f; Ji[6] = 0.0f;
+        accum_row(acc, ti, qi, si, Jx, w[2], err[2]);
+        Ji[0] = rj[0]; Ji[1] = rj[1]; Ji[2] = rj[2];
+        Ji[3] = 0.0f; Ji[4] = 0.0f; Ji[5] = 0.0f; Ji[6] = norm1_j;
+        accum_row(acc, ti, qi, si, Jx, w[3], err[3]);
+    } else if (P->mode == ORACLE_GN_CALIB) {
+        /* gn_kernels.cu:1360-1495 */
+        const float fx = P->K[0], fy = P->K[4], cx = P->K[2], cy = P->K[5];
+        const float sigma_pixel_inv = (float)(1.0 / (double)P->sigma0);
+        const float sigma_depth_inv = (float)(1.0 / (double)P->sigma1);
+        const int u_target = (int)(ind_Xi % P->width);
+        const int v_target = (int)(ind_Xi / P->width);
+        const int valid_z = (Xj_Ci[2] > P->z_eps) && (Xi[2] > P->z_eps);
+        const float zj_inv = valid_z ? (float)(1.0 / (double)Xj_Ci[2]) : 0.0f;
+        const float zj_log = valid_z ? logf(Xj_Ci[2]) : 0.0f;
+        const float zi_log = valid_z ? logf(Xi[2]) : 0.0f;
+        const float x_div_z = Xj_Ci[0] * zj_inv;
+        const float y_div_z = Xj_Ci[1] * zj_inv;
+        const float u = fx * x_div_z + cx;
+        const float v = fy * y_div_z + cy;
+        const int valid_u = (u > (float)P->pixel_border) && (u < (float)(P->width - 1 - P->pixel_border));
+        const int valid_v = (v > (float)P->pixel_border) && (v < (float)(P->height - 1 - P->pixel_border));
+        float err[3], w[3];
+        err[0] = u - (float)u_target;
+        err[1] = v - (float)v_target;
+        err[2] = zj_log - zi_log;
+        const int valid = valid_match_ind & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh) &
+                          valid_u & valid_v & valid_z;
+        const float sqrt_w_pixel = valid ? sigma_pixel_inv * sqrtf(q) : 0.0f;
+        const float sqrt_w_depth = valid ? sigma_depth_inv * sqrtf(q) : 0.0f;
+        w[0] = huber(sqrt_w_pixel * err[0]);
+        w[1] = huber(sqrt_w_pixel * err[1]);
+        w[2] = huber(sqrt_w_depth * err[2]);
+        const float w_const_pixel = sqrt_w_pixel * sqrt_w_pixel;
+        const float w_const_depth = sqrt_w_depth * sqrt_w_depth;
+        w[0] *= w_const_pixel;
+        w[1] *= w_const_pixel;
+        w[2] *= w_const_depth;
+        Ji[0] = fx * zj_inv; Ji[1] = 0.0f; Ji[2] = ((-fx) * x_div_z) * zj_inv;
+        Ji[3] = ((-fx) * x_div_z) * y_div_z; Ji[4] = fx * (1.0f + x_div_z * x_div_z);
+        Ji[5] = (-fx) * y_div_z; Ji[6] = 0.0f;
+        accum_row(acc, ti, qi, si, Jx, w[0], err[0]);
+        Ji[0] = 0.0f; Ji[1] = fy * zj_inv; Ji[2] = ((-fy) * y_div_z) * zj_inv;
+        Ji[3] = (-fy) * (1.0f + y_div_z * y_div_z); Ji[4] = (fy * x_div_z) * y_div_z;
+        Ji[5] = fy * x_div_z; Ji[6] = 0.0f;
+        accum_row(acc, ti, qi, si, Jx, w[1], err[1]);
+        Ji[0] = 0.0f; Ji[1] = 0.0f; Ji[2] = zj_inv;
+        Ji[3] = y_div_z; Ji[4] = -x_div_z; Ji[5] = 0.0f; Ji[6] = 1.0f;
+        accum_row(acc, ti, qi, si, Jx, w[2], err[2]);
+    } else {
+        /* point_align_kernel, gn_kernels.cu:564-674 */
+        const float sigma_point_inv = (float)(1.0 / (double)P->sigma0);
+        float err[3], w[3];
+        err[0] = Xj_Ci[0] - Xi[0];
+        err[1] = Xj_Ci[1] - Xi[1];
+        err[2] = Xj_Ci[2] - Xi[2];
+        const int valid = valid_match_ind & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh);
+        const float sqrt_w_point = valid ? sigma_point_inv * sqrtf(q) : 0.0f;
+        w[0] = huber(sqrt_w_point * err[0]);
+        w[1] = huber(sqrt_w_point * err[1]);
+        w[2] = huber(sqrt_w_point * err[2]);
+        const float w_const_point = sqrt_w_point * sqrt_w_point;
+        w[0] *= w_const_point;
+        w[1] *= w_const_point;
+        w[2] *= w_const_point;
+        Ji[0] = 1.0f; Ji[1] = 0.0f; Ji[2] = 0.0f; Ji[3] = 0.0f;
+        Ji[4] = Xj_Ci[2]; Ji[5] = -Xj_Ci[1]; Ji[6] = Xj_Ci[0];
+        accum_row(acc, ti, qi, si, Jx, w[0], err[0]);
+        Ji[0] = 0.0f; Ji[1] = 1.0f; Ji[2] = 0.0f; Ji[3] = -Xj_Ci[2];
+        Ji[4] = 0.0f; Ji[5] = Xj_Ci[0]; Ji[6] = Xj_Ci[1];
+        accum_row(acc, ti, qi, si, Jx, w[1], err[1]);
+        Ji[0] = 0.0f; Ji[1] = 0.0f; Ji[2] = 1.0f; Ji[3] = Xj_Ci[1];
+        Ji[4] = -Xj_Ci[0]; Ji[5] = 0.0f; Ji[6] = Xj_Ci[2];
+        accum_row(acc, ti, qi, si, Jx, w[2], err[2]);
+    }
+}
+
+void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* Xs,
+                     const float* Cs, const int64_t* ii_edge, const int64_t* jj_edge,
+                     const int64_t* idx, const uint8_t* valid, const float* Q,
+                     int64_t N, int64_t HW, int64_t E, float* Hs, float* gs) {
+    (void)N;
+#pragma omp parallel
+    {
+        float* acc = (float*)malloc(sizeof(float) * THREADS * NACC);
+        float* sdata = (float*)malloc(sizeof(float) * THREADS);
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t e = 0; e < E; e++) {
+            const int64_t ix = ii_edge[e], jx = jj_edge[e];
+            const float* Ti = Twc + ix * 8;
+            const float* Tj = Twc + jx * 8;
+            float ti[3] = {Ti[0], Ti[1], Ti[2]}, qi[4] = {Ti[3], Ti[4], Ti[5], Ti[6]}, si[1] = {Ti[7]};
+            float tj[3] = {Tj[0], Tj[1], Tj[2]}, qj[4] = {Tj[3], Tj[4], Tj[5], Tj[6]}, sj[1] = {Tj[7]};
+            float tij[3], qij[4], sij[1];
+            relSim3(ti, qi, si, tj, qj, sj, tij, qij, sij);
+            memset(acc, 0, sizeof(float) * THREADS * NACC);
+            for (int t = 0; t < THREADS; t++) {
+                float* a = acc + (int64_t)t * NACC;
+                for (int64_t k = t; k < HW; k += THREADS) { /* GPU_1D_KERNEL_LOOP (:31-32) */
+                    const int64_t pe = e * HW + k;
+                    const int vm = valid[pe] != 0;
+                    const int64_t ind = vm ? idx[pe] : 0;
+                    const float* Xi = Xs + (ix * HW + ind) * 3;
+                    const float* Xj = Xs + (jx * HW + k) * 3;
+                    align_point(P, ti, qi, si, tij, qij, sij, Xi, Xj, Q[pe], Cs[ix * HW + ind],
+                                Cs[jx * HW + k], vm, ind, a);
+                }
+            }
+            /* gs (gn_kernels.cu:1097-1112) */
+            for (int n = 0; n < 14; n++) {
+                for (int t = 0; t < THREADS; t++) sdata[t] = acc[(int64_t)t * NACC + HDIM + n];
+                float v = block_reduce(sdata);
+                if (n < 7) gs[(0 * E + e) * 7 + n] = v;
+                else gs[(1 * E + e) * 7 + (n - 7)] = v;
+            }
+            /* Hs (gn_kernels.cu:1114-1137) */
+            int l = 0;
+            for (int n = 0; n < 14; n++) {
+                for (int m = 0; m <= n; m++) {
+                    for (int t = 0; t < THREADS; t++) sdata[t] = acc[(int64_t)t * NACC + l];
+                    float v = block_reduce(sdata);
+                    if (n < 7 && m < 7) {
+                        Hs[((0 * E + e) * 7 + n) * 7 + m] = v;
+                        Hs[((0 * E + e) * 7 + m) * 7 + n] = v;
+                    } else if (n >= 7 && m < 7) {
+                        Hs[((1 * E + e) * 7 + m) * 7 + (n - 7)] = v;
+                        Hs[((2 * E + e) * 7 + (n - 7)) * 7 + m] = v;
+                    } else {
+                        Hs[((3 * E + e) * 7 + (n - 7)) * 7 + (m - 7)] = v;
+                        Hs[((3 * E + e) * 7 + (m - 7)) * 7 + (n - 7)] = v;
+                    }
+                    l++;
+                }
+            }
+        }
+        free(acc);
+        free(sdata);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* SparseBlock assembly + SimplicialLLT semantics (gn_kernels.cu:57-159)    */
+/* ------------------------------------------------------------------------ */
+
+void oracle_gn_assemble(const float* Hs, const float* gs, const int64_t* ii_opt,
+                        const int64_t* jj_opt, int64_t N, int64_t E,
+                        double* H, double* b) {
+    const int64_t n = 7 * (N - 1);
+    memset(H, 0, sizeof(double) * n * n);
+    memset(b, 0, sizeof(double) * n);
+    /* update_lhs: rows cat(ii,ii,jj,jj), cols cat(ii,jj,ii,jj), triplet order */
+    for (int blk = 0; blk < 4; blk++) {
+        const int64_t* rows = (blk < 2) ? ii_opt : jj_opt;
+        const int64_t* cols = (blk == 0 || blk == 2) ? ii_opt : jj_opt;
+        for (int64_t e = 0; e < E; e++) {
+            const int64_t i = rows[e], j = cols[e];
+            if (i >= 0 && j >= 0) {
+                const float* A = Hs + ((int64_t)blk * E + e) * 49;
+                for (int k = 0; k < 7; k++)
+                    for (int l = 0; l < 7; l++) H[(7 * i + k) * n + 7 * j + l] += (double)A[k * 7 + l];
+            }
+        }
+    }
+    /* update_rhs: cat(ii,jj) */
+    for (int blk = 0; blk < 2; blk++) {
+        const int64_t* rows = blk == 0 ? ii_opt : jj_opt;
+        for (int64_t e = 0; e < E; e++) {
+            const int64_t i = rows[e];
+            if (i >= 0) {
+                const float* g = gs + ((int64_t)blk * E + e) * 7;
+                for (int j = 0; j < 7; j++) b[i * 7 + j] += (double)g[j];
+            }
+        }
+    }
+}
+
+/* Dense LL^T in double on the lower triangle.  SimplicialLLT fails iff a pivot
+ * d <= 0 (a NaN pivot does not fail); then the caller uses dx = 0
+ * (gn_kernels.cu:142-150).  Eigen factorises the AMD-permuted matrix; the
+ * solution is the same up to double rounding. */
+int oracle_cholesky_solve(double* L, const double* b, double* x, int64_t n) {
+    for (int64_t k = 0; k < n; k++) {
+        double d = L[k * n + k];
+        for (int64_t p = 0; p < k; p++) d -= L[k * n + p] * L[k * n + p];
+        if (d <= 0.0) {
+            for (int64_t i = 0; i < n; i++) x[i] = 0.0;
+            return 1;
+        }
+        const double lkk = sqrt(d);
+        L[k * n + k] = lkk;
+#pragma omp parallel for schedule(static) if (n - k > 256)
+        for (int64_t i = k + 1; i < n; i++) {
+            double s = L[i * n + k];
+            const double* Li = L + i * n;
+            const double* Lk = L + k * n;
+            for (int64_t p = 0; p < k; p++) s -= Li[p] * Lk[p];
+            L[i * n + k] = s / lkk;
+        }
+    }
+    /* forward L y = b */
+    for (int64_t i = 0; i < n; i++) {
+        double s = b[i];
+        for (int64_t p = 0; p < i; p++) s -= L[i * n + p] * x[p];
+        x[i] = s / L[i * n + i];
+    }
+    /* backward L^T x = y */
+    for (int64_t i = n - 1; i >= 0; i--) {
+        double s = x[i];
+        for (int64_t p = i + 1; p < n; p++) s -= L[p * n + i] * x[p];
+        x[i] = s / L[i * n + i];
+    }
+    return 0;
+}
+
+static int cmp_i64(const void* a, const void* b) {
+    int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+    return (x > y) - (x < y);
+}
+
+static int64_t searchsorted_left(const int64_t* u, int64_t n, int64_t v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) / 2;
+        if (u[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+/* get_unique_kf_idx + create_inds (gn_kernels.cu:161-170), pin = 0 */
+int64_t oracle_remap(const int64_t* ii, const int64_t* jj, int64_t E, int64_t* ii_edge, int64_t* jj_edge) {
+    int64_t* u = (int64_t*)malloc(sizeof(int64_t) * (2 * E + 1));
+    for (int64_t e = 0; e < E; e++) {
+        u[e] = ii[e];
+        u[E + e] = jj[e];
+    }
+    qsort(u, (size_t)(2 * E), sizeof(int64_t), cmp_i64);
+    int64_t nu = 0;
+    for (int64_t k = 0; k < 2 * E; k++)
+        if (nu == 0 || u[k] != u[nu - 1]) u[nu++] = u[k];
+    for (int64_t e = 0; e < E; e++) {
+        ii_edge[e] = searchsorted_left(u, nu, ii[e]);
+        jj_edge[e] = searchsorted_left(u, nu, jj[e]);
+    }
+    free(u);
+    return nu;
+}
+
+/* gauss_newton_*_cuda drivers */
+int oracle_gauss_newton(const oracle_gn_params* P, float* Twc, const float* Xs,
+                        const float* Cs, const int64_t* ii, const int64_t* jj,
+                        const int64_t* idx, const uint8_t* valid, const float* Q,
+                        int64_t N, int64_t HW, int64_t E, float* dx) {
+    const int num_fix = 1;
+    const int64_t n = 7 * (N - num_fix);
+    int64_t* ii_edge = (int64_t*)malloc(sizeof(int64_t) * (E + 1));
+    int64_t* jj_edge = (int64_t*)malloc(sizeof(int64_t) * (E + 1));
+    int64_t* ii_opt = (int64_t*)malloc(sizeof(int64_t) * (E + 1));
+    int64_t* jj_opt = (int64_t*)malloc(sizeof(int64_t) * (E + 1));
+    oracle_remap(ii, jj, E, ii_edge, jj_edge);
+    for (int64_t e = 0; e < E; e++) {
+        ii_opt[e] = ii_edge[e] - num_fix;
+        jj_opt[e] = jj_edge[e] - num_fix;
+    }
+    float* Hs = (float*)malloc(sizeof(float) * 4 * E * 49 + 4);
+    float* gs = (float*)malloc(sizeof(float) * 2 * E * 7 + 4);
+    double* H = (double*)malloc(sizeof(double) * (n * n + 1));
+    double* b = (double*)malloc(sizeof(double) * (n + 1));
+    double* x = (double*)malloc(sizeof(double) * (n + 1));
+    int itr;
+    for (itr = 0; itr < P->max_iter; itr++) {
+        oracle_gn_align(P, Twc, Xs, Cs, ii_edge, jj_edge, idx, valid, Q, N, HW, E, Hs, gs);
+        oracle_gn_assemble(Hs, gs, ii_opt, jj_opt, N, E, H, b);
+        oracle_cholesky_solve(H, b, x, n);
+        double nrm = 0.0;
+        for (int64_t k = 0; k < n; k++) {
+            dx[k] = -(float)x[k]; /* "dx = -A.solve()" (:1209), solve() returns float */
+            nrm += (double)dx[k] * (double)dx[k];
+        }
+        oracle_pose_retr(Twc, dx, N, num_fix);
+        if ((float)sqrt(nrm) < P->delta_thresh) { /* :1219-1222 */
+            itr++;
+            break;
+        }
+    }
+    free(ii_edge); free(jj_edge); free(ii_opt); free(jj_opt);
+    free(Hs); free(gs); free(H); free(b); free(x);
+    return itr;
+}
