@@ -114,7 +114,7 @@ _DT_NAME = {
 }
 
 
-def _check(t, name, dtype, ndim, device=None):
+def _check(t, name, dtype, ndim):
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
     if not t.is_contiguous():  # CHECK_CONTIGUOUS (gn.h:5)
@@ -127,12 +127,23 @@ def _check(t, name, dtype, ndim, device=None):
         )
     if t.dim() != ndim:
         raise RuntimeError(f"packed_accessor32 expects {ndim} dims but tensor has {t.dim()} ({name})")
-    if t.device.type != "cuda":
-        raise RuntimeError(
-            f"{name} must be a HIP (cuda) tensor: mast3r_slam_backends has no CPU path"
-        )
-    if device is not None and t.device != device:
-        raise RuntimeError(f"{name} must be on {device}, got {t.device}")
+
+
+def _on_device(**tensors):
+    """All tensors on one HIP device (checked after dtype/shape, like the accessors)."""
+    dev = None
+    for name, t in tensors.items():
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                f"{name} must be a HIP (cuda) tensor: mast3r_slam_backends has no CPU path"
+            )
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"{name} must be on {dev}, got {t.device}")
+    return dev
 
 
 def _raise(rc, what):
@@ -157,9 +168,9 @@ def _ptr(t):
 def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh):
     """gn.cpp:84-99 / matching_kernels.cu:279-316 -> [p_new f32[B,N,2], converged bool[B,N]]."""
     _check(rays_img_with_grad, "rays_img_with_grad", torch.float32, 4)
-    dev = rays_img_with_grad.device
-    _check(pts_3d_norm, "pts_3d_norm", torch.float32, 3, dev)
-    _check(p_init, "p_init", torch.float32, 3, dev)
+    _check(pts_3d_norm, "pts_3d_norm", torch.float32, 3)
+    _check(p_init, "p_init", torch.float32, 3)
+    dev = _on_device(rays_img_with_grad=rays_img_with_grad, pts_3d_norm=pts_3d_norm, p_init=p_init)
     B, H, W, C = rays_img_with_grad.shape
     if C != 9:
         raise RuntimeError(f"rays_img_with_grad must have 9 channels (ray, d/du, d/dv), got {C}")
@@ -185,9 +196,9 @@ def refine_matches(D11, D21, p1, window_size, dilation_max):
 
     ``window_size`` is the search radius (config ``matching.radius``)."""
     _check(D11, "D11", (torch.float16, torch.float32), 4)
-    dev = D11.device
-    _check(D21, "D21", D11.dtype, 3, dev)
-    _check(p1, "p1", torch.int64, 3, dev)
+    _check(D21, "D21", D11.dtype, 3)
+    _check(p1, "p1", torch.int64, 3)
+    dev = _on_device(D11=D11, D21=D21, p1=p1)
     B, H, W, F = D11.shape
     Bq, N = p1.shape[0], p1.shape[1]
     if p1.shape[2] != 2 or D21.shape[0] != Bq or D21.shape[1] != N or D21.shape[2] != F or Bq != B:
@@ -210,14 +221,15 @@ def refine_matches(D11, D21, p1, window_size, dilation_max):
 
 def _gn_common_checks(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, edge_local=None):
     _check(Twc, "Twc", torch.float32, 2)
-    dev = Twc.device
-    _check(Xs, "Xs", torch.float32, 3, dev)
-    _check(Cs, "Cs", torch.float32, 3, dev)
-    _check(ii, "ii", torch.int64, 1, dev)
-    _check(jj, "jj", torch.int64, 1, dev)
-    _check(idx_ii2jj, "idx_ii2jj", torch.int64, 2, dev)
-    _check(valid_match, "valid_match", torch.bool, 3, dev)
-    _check(Q, "Q", torch.float32, 3, dev)
+    _check(Xs, "Xs", torch.float32, 3)
+    _check(Cs, "Cs", torch.float32, 3)
+    _check(ii, "ii", torch.int64, 1)
+    _check(jj, "jj", torch.int64, 1)
+    _check(idx_ii2jj, "idx_ii2jj", torch.int64, 2)
+    _check(valid_match, "valid_match", torch.bool, 3)
+    _check(Q, "Q", torch.float32, 3)
+    dev = _on_device(Twc=Twc, Xs=Xs, Cs=Cs, ii=ii, jj=jj, idx_ii2jj=idx_ii2jj,
+                     valid_match=valid_match, Q=Q)
     N, HW = Xs.shape[0], Xs.shape[1]
     E = ii.shape[0]
     El = E if edge_local is None else edge_local
@@ -240,7 +252,8 @@ def _run_gn(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter, delt
     if edge_total is not None and edge_total != E:
         raise RuntimeError("gauss_newton: edge_total must equal len(ii)")
     if K is not None:
-        _check(K, "K", torch.float32, 2, dev)
+        _check(K, "K", torch.float32, 2)
+        _on_device(Twc=Twc, K=K)
         if K.shape != (3, 3):
             raise RuntimeError("K must be [3,3]")
     max_iter = int(max_iter)

@@ -106,7 +106,7 @@ class _KF:
 
 class _Frames:
     def __init__(self, Xs, Ts, Cs, h, w):
-        self.kfs = [_KF(Xs[k], Ts[k : k + 1], Cs[k], torch.zeros(3, h, w)) for k in range(len(Xs))]
+        self.kfs = [_KF(Xs[k], Ts[k], Cs[k], torch.zeros(3, h, w)) for k in range(len(Xs))]
 
     def __getitem__(self, idx):
         return self.kfs[int(idx)]
