@@ -88,7 +88,7 @@ int chunk_points(int64_t HW, int nchunks) {
 
 struct Layout {
     size_t partials, edgeblk, compact, dense, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent,
-        grad_ptr, grad_ent, slotmap, total;
+        grad_ptr, grad_ent, slotmap, linv, total;
     int nchunks, npad, nblk_max;
 };
 
@@ -118,6 +118,7 @@ Layout make_layout(int64_t N, int64_t HW, int64_t E_total, int64_t E_local) {
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
     L.slotmap = take(sizeof(int) * (size_t)npose * npose);
+    L.linv = take(sizeof(double) * (size_t)L.npad * kCholTile);
     L.total = off;
     return L;
 }
@@ -231,6 +232,9 @@ int validate(const m3s_gn_args& a) {
                 "gauss_newton: bad edge range");
     M3S_REQUIRE(a.HW < ((int64_t)1 << 31) && a.E_local < (1 << 30),
                 "gauss_newton: sizes exceed int32 indexing");
+    M3S_REQUIRE(7 * (a.N - 1) <= kMaxNpad,
+                "gauss_newton: %lld poses exceed the dense solve limit (%d unknowns)",
+                (long long)a.N, kMaxNpad);
     M3S_REQUIRE(a.mode != M3S_GN_CALIB || (a.K != nullptr && a.width > 0 && a.height > 0),
                 "gauss_newton_calib: K / image size required");
     M3S_REQUIRE(a.Twc && a.Xs && a.Cs && a.dx, "gauss_newton: null pointer");
@@ -343,7 +347,7 @@ int run(const m3s_gn_args& a) {
         g_prof.mark(c.st);
         M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.at<int>(L.slotmap),
                                    c.plan.nblk, npose, 7 * npose, L.npad, c.at<double>(L.dense),
-                                   c.at<double>(L.x), flags));
+                                   c.at<double>(L.linv), c.at<double>(L.x), flags));
         g_prof.mark(c.st);
         M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
                                      a.delta_thresh, flags));

@@ -42,7 +42,9 @@ hipError_t launch_compact(hipStream_t st, const double* edgeblk, const int* blk_
                           const int* blk_ent, const int* grad_ptr, const int* grad_ent, int nblk,
                           int npose, double* compact, const int* flags);
 hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
-                        int npose, int n, int npad, double* Hd, double* x, int* flags);
+                        int npose, int n, int npad, double* Hd, double* Linv, double* x,
+                        int* flags);
+constexpr int kMaxNpad = 8192;  // dense solve limit: N <= 1171 keyframes
 hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                             int npose, int n, int npad, double* Hd, const int* flags);
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,

@@ -449,159 +449,315 @@ __global__ __launch_bounds__(256) void gn_fill_dense_kernel(const double* __rest
 }
 
 // ---- blocked Cholesky, T = 64 --------------------------------------------------
+//
+// Right-looking tile LL^T of the dense f64 system (rows < npad) with the RHS as a border
+// row (row npad), so the forward substitution y = L^{-1} b rides along.  Per panel k:
+//   chol_potrf_kernel  (1 WG)      : L_kk and its inverse Li_k (doubling) in LDS
+//   chol_trsm_kernel   (nt-k WGs)  : L_ik = A_ik Li_k^T as a 64^3 GEMM (tile nt = border)
+//   chol_update_kernel (tiles)     : A_ij -= L_ik L_jk^T
+// then chol_backsolve_kernel (1 WG) solves L^T x = y with the stored Li_k.
 
 constexpr int T = kCholTile;
-constexpr int LD = T + 1;  // LDS row stride (doubles)
 
-// Factor the diagonal tile in LDS (right-looking), returns false if a pivot <= 0.
-__device__ bool factor_diag_lds(double (*L)[LD]) {
-    const int tid = threadIdx.x;
-    bool ok = true;
-    for (int c = 0; c < T; c++) {
-        __syncthreads();
-        const double d = L[c][c];
-        if (d <= 0.0) ok = false;  // SimplicialLLT: fails iff pivot <= 0 (NaN passes)
-        const double lcc = sqrt(d);
-        const double inv = 1.0 / lcc;
-        __syncthreads();
-        if (tid > c && tid < T) L[tid][c] *= inv;
-        if (tid == 0) L[c][c] = lcc;
-        __syncthreads();
-        const int m = T - 1 - c;
-        for (int k = tid; k < m * m; k += blockDim.x) {
-            const int rr = k / m, cc = k % m;
-            if (cc <= rr) L[c + 1 + rr][c + 1 + cc] -= L[c + 1 + rr][c] * L[c + 1 + cc][c];
-        }
-    }
-    __syncthreads();
-    return ok;
+// 1/d to ~1 ulp: v_rcp_f64 + two Newton steps (the solve is not a bit-exact path).
+__device__ __forceinline__ double rcp_f64(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = r * (2.0 - d * r);
+    r = r * (2.0 - d * r);
+    return r;
 }
 
-// Panel step k: WG 0 factors A_kk; WG m>0 computes L_{k+m,k} = A_{k+m,k} L_kk^{-T}
-// (tile row nt is the RHS border row).
-__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ Hd, int npad, int k,
-                                                         int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
-    __shared__ double L[T][LD];
-    __shared__ double X[T][LD];
-    const int tid = threadIdx.x;
-    const int m = blockIdx.x;
-    double* Akk = Hd + (int64_t)k * T * npad + (int64_t)k * T;
-    for (int id = tid; id < T * T; id += blockDim.x) {
-        const int r = id / T, c = id % T;
-        L[r][c] = (c <= r) ? Akk[(int64_t)r * npad + c] : 0.0;
-    }
-    const bool ok = factor_diag_lds(L);
-    if (m == 0) {
-        if (!ok && tid == 0) flags[kFlagFail] = 1;
-        for (int id = tid; id < T * T; id += blockDim.x) {
-            const int r = id / T, c = id % T;
-            if (c <= r) Akk[(int64_t)r * npad + c] = L[r][c];
-        }
-        return;
-    }
-    const int i = k + m;
-    double* Aik = Hd + (int64_t)i * T * npad + (int64_t)k * T;
-    for (int id = tid; id < T * T; id += blockDim.x) {
-        const int r = id / T, c = id % T;
-        X[r][c] = Aik[(int64_t)r * npad + c];
+// potrf of one 64x64 tile + its inverse, one 1024-thread workgroup, LDS-resident.
+// Blocked in 8-column sub-panels (16 barriers instead of 64):
+//   phase 1 (one wave, lane = row): every lane factors the 8x8 diagonal block in registers
+//            (redundantly -- no cross-lane traffic) and solves its own row of the panel;
+//   phase 2 (all threads): rank-8 trailing update of the lower triangle.
+// Then Li = L^{-1} by doubling, [[A,0],[B,C]]^{-1} = [[Ai,0],[-Ci B Ai, Ci]] (12 barriers).
+constexpr int kPotrfThreads = 512;
+constexpr int LDP = T + 1;
+
+__device__ __forceinline__ double rsqrt_f64(double d) {
+    double r = __builtin_amdgcn_rsq(d);
+    r = r * (1.5 - 0.5 * d * r * r);
+    r = r * (1.5 - 0.5 * d * r * r);
+    return r;
+}
+
+template <int S>
+__device__ __forceinline__ void inverse_stage(const double (*L)[LDP], double (*Li)[LDP],
+                                              double (*Tm)[LDP], int tid) {
+    constexpr int P = T / (2 * S);
+    constexpr int NOUT = P * S * S;
+    // Tm = B Ai   (B = L[p+S.., p..], Ai lower)
+    for (int id = tid; id < NOUT; id += kPotrfThreads) {
+        const int pi = id / (S * S), rem = id % (S * S);
+        const int a = rem / S, bb = rem % S;
+        const int p = pi * 2 * S;
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < S; m++)
+            if (m >= bb) acc = fma(L[p + S + a][p + m], Li[p + m][p + bb], acc);
+        Tm[p + S + a][p + bb] = acc;
     }
     __syncthreads();
-    // X <- X L^{-T}: column-oriented forward substitution over the tile columns
-    for (int c = 0; c < T; c++) {
-        if (tid < T) X[tid][c] /= L[c][c];
+    // Li[p+S.., p..] = -Ci Tm
+    for (int id = tid; id < NOUT; id += kPotrfThreads) {
+        const int pi = id / (S * S), rem = id % (S * S);
+        const int a = rem / S, bb = rem % S;
+        const int p = pi * 2 * S;
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < S; m++)
+            if (m <= a) acc = fma(Li[p + S + a][p + S + m], Tm[p + S + m][p + bb], acc);
+        Li[p + S + a][p + bb] = -acc;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kPotrfThreads) void chol_potrf_kernel(double* __restrict__ Hd,
+                                                                   int npad, int k,
+                                                                   double* __restrict__ Linv,
+                                                                   int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    __shared__ double A[T][LDP];
+    __shared__ double Li[T][LDP];
+    __shared__ double Tm[T][LDP];
+    __shared__ int fail;
+    const int tid = threadIdx.x;
+    double* Akk = Hd + (int64_t)k * T * npad + (int64_t)k * T;
+    for (int id = tid; id < T * T; id += kPotrfThreads) {
+        const int r = id >> 6, c = id & 63;
+        A[r][c] = (c <= r) ? Akk[(int64_t)r * npad + c] : 0.0;
+        Li[r][c] = 0.0;
+    }
+    if (tid == 0) fail = 0;
+    __syncthreads();
+    const int tx = tid & 31, ty = tid >> 5;  // ty in [0, 16)
+    for (int s = 0; s < T / 8; s++) {
+        const int c0 = 8 * s;
+        if (tid < T && tid >= c0) {
+            const int r = tid;
+            // all LDS operands first (one latency), then register-only math
+            double D[8][8], arow[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int p = 0; p <= i; p++) D[i][p] = A[c0 + i][c0 + p];
+#pragma unroll
+            for (int p = 0; p < 8; p++) arow[p] = A[r][c0 + p];
+            double l[8][8];
+            bool bad = false;
+#pragma unroll
+            for (int p = 0; p < 8; p++) {
+                double dpp = D[p][p];
+#pragma unroll
+                for (int q = 0; q < p; q++) dpp = fma(-l[p][q], l[p][q], dpp);
+                if (dpp <= 0.0) bad = true;  // SimplicialLLT: fails iff a pivot <= 0
+                const double inv = rsqrt_f64(dpp);
+                l[p][p] = dpp * inv;
+#pragma unroll
+                for (int i = p + 1; i < 8; i++) {
+                    double a_ = D[i][p];
+#pragma unroll
+                    for (int q = 0; q < p; q++) a_ = fma(-l[i][q], l[p][q], a_);
+                    l[i][p] = a_ * inv;
+                }
+            }
+            if (r < c0 + 8) {
+                const int i = r - c0;
+#pragma unroll
+                for (int ii = 0; ii < 8; ii++) {
+                    if (ii == i) {
+#pragma unroll
+                        for (int p = 0; p <= ii; p++) A[r][c0 + p] = l[ii][p];
+                    }
+                }
+                if (bad && r == c0) fail = 1;
+            } else {
+                double x[8];
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    double a_ = arow[p];
+#pragma unroll
+                    for (int q = 0; q < p; q++) a_ = fma(-x[q], l[p][q], a_);
+                    x[p] = a_ * rcp_f64(l[p][p]);
+                }
+#pragma unroll
+                for (int p = 0; p < 8; p++) A[r][c0 + p] = x[p];
+            }
+        }
         __syncthreads();
-        const int m2 = T - 1 - c;
-        for (int id = tid; id < T * m2; id += blockDim.x) {
-            const int r = id / m2, cc = c + 1 + id % m2;
-            X[r][cc] -= X[r][c] * L[cc][c];
+        // rank-8 update of the lower trailing block (rows/cols >= c0 + 8)
+        const int lo = c0 + 8;
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+            const int r = ty + 16 * a;
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                const int cc = tx + 32 * b;
+                if (cc >= lo && cc <= r) {
+                    double acc = A[r][cc];
+#pragma unroll
+                    for (int p = 0; p < 8; p++) acc = fma(-A[r][c0 + p], A[cc][c0 + p], acc);
+                    A[r][cc] = acc;
+                }
+            }
         }
         __syncthreads();
     }
-    for (int id = tid; id < T * T; id += blockDim.x) {
-        const int r = id / T, c = id % T;
-        Aik[(int64_t)r * npad + c] = X[r][c];
+    // inverse by doubling
+    if (tid < T) Li[tid][tid] = 1.0 / A[tid][tid];
+    __syncthreads();
+    inverse_stage<1>(A, Li, Tm, tid);
+    inverse_stage<2>(A, Li, Tm, tid);
+    inverse_stage<4>(A, Li, Tm, tid);
+    inverse_stage<8>(A, Li, Tm, tid);
+    inverse_stage<16>(A, Li, Tm, tid);
+    inverse_stage<32>(A, Li, Tm, tid);
+    double* Lk = Linv + (int64_t)k * T * T;
+    for (int id = tid; id < T * T; id += kPotrfThreads) {
+        const int r = id >> 6, c = id & 63;
+        if (c <= r) Akk[(int64_t)r * npad + c] = A[r][c];
+        Lk[id] = (c <= r) ? Li[r][c] : 0.0;
     }
+    if (fail && tid == 0) flags[kFlagFail] = 1;
+}
+
+// 64x64x64 tile product from LDS (row stride LD2 doubles, 16-B aligned rows): 512 threads,
+// each a 4 (rows) x 2 (cols) block, m consumed in pairs (ds_read_b128).
+constexpr int LD2 = T + 2;
+constexpr int kGemmThreads = 512;
+__device__ __forceinline__ void tile_nt(const double (*X)[LD2], const double (*Y)[LD2], int r0,
+                                        int c0, double acc[4][2]) {
+#pragma unroll 4
+    for (int m = 0; m < T; m += 2) {
+        double2 xa[4], yb[2];
+#pragma unroll
+        for (int a = 0; a < 4; a++) xa[a] = *reinterpret_cast<const double2*>(&X[r0 + a][m]);
+#pragma unroll
+        for (int b = 0; b < 2; b++) yb[b] = *reinterpret_cast<const double2*>(&Y[c0 + b][m]);
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                acc[a][b] = fma(xa[a].x, yb[b].x, acc[a][b]);
+                acc[a][b] = fma(xa[a].y, yb[b].y, acc[a][b]);
+            }
+    }
+}
+
+__device__ __forceinline__ void load_tile(double (*dst)[LD2], const double* __restrict__ src,
+                                          int64_t ld, int tid) {
+#pragma unroll 4
+    for (int id = tid; id < T * T / 2; id += kGemmThreads) {
+        const int r = id >> 5, c2 = (id & 31) * 2;
+        *reinterpret_cast<double2*>(&dst[r][c2]) =
+            *reinterpret_cast<const double2*>(src + (int64_t)r * ld + c2);
+    }
+}
+
+// L_ik = A_ik Li_k^T for tile rows i = k+1 .. nt (nt = the RHS border tile).
+__global__ __launch_bounds__(kGemmThreads) void chol_trsm_kernel(double* __restrict__ Hd, int npad,
+                                                                 int k,
+                                                                 const double* __restrict__ Linv,
+                                                                 const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    __shared__ __attribute__((aligned(16))) double Xs_[T][LD2];
+    __shared__ __attribute__((aligned(16))) double Li[T][LD2];
+    const int tid = threadIdx.x;
+    const int i = k + 1 + blockIdx.x;
+    double* Aik = Hd + (int64_t)i * T * npad + (int64_t)k * T;
+    load_tile(Xs_, Aik, npad, tid);
+    load_tile(Li, Linv + (int64_t)k * T * T, T, tid);
+    __syncthreads();
+    const int r0 = (tid >> 5) * 4, c0 = (tid & 31) * 2;
+    double acc[4][2] = {};
+    tile_nt(Xs_, Li, r0, c0, acc);
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+        *reinterpret_cast<double2*>(Aik + (int64_t)(r0 + a) * npad + c0) =
+            make_double2(acc[a][0], acc[a][1]);
 }
 
 // Trailing update after panel k: A_ij -= L_ik L_jk^T for k < j <= i <= nt, j < nt.
-__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ Hd, int npad,
-                                                          int nt, int k,
-                                                          const int* __restrict__ flags) {
+__global__ __launch_bounds__(kGemmThreads) void chol_update_kernel(double* __restrict__ Hd,
+                                                                   int npad, int nt, int k,
+                                                                   const int* __restrict__ flags) {
     if (flags[kFlagDone]) return;
-    __shared__ double Li[T][LD];
-    __shared__ double Lj[T][LD];
-    // blockIdx.x -> (i, j): j = k+1.., i = j..nt
-    int rem = blockIdx.x;
+    __shared__ __attribute__((aligned(16))) double Li[T][LD2];
+    __shared__ __attribute__((aligned(16))) double Lj[T][LD2];
+    int rem = blockIdx.x;  // -> (i, j): j = k+1.., i = j..nt
     int j = k + 1;
     while (rem >= nt - j + 1) { rem -= nt - j + 1; j++; }
     const int i = j + rem;
     const int tid = threadIdx.x;
-    const double* Aik = Hd + (int64_t)i * T * npad + (int64_t)k * T;
-    const double* Ajk = Hd + (int64_t)j * T * npad + (int64_t)k * T;
-    for (int id = tid; id < T * T; id += blockDim.x) {
-        const int r = id / T, c = id % T;
-        Li[r][c] = Aik[(int64_t)r * npad + c];
-        Lj[r][c] = Ajk[(int64_t)r * npad + c];
-    }
+    load_tile(Li, Hd + (int64_t)i * T * npad + (int64_t)k * T, npad, tid);
+    load_tile(Lj, Hd + (int64_t)j * T * npad + (int64_t)k * T, npad, tid);
     __syncthreads();
-    const int r0 = (tid / 16) * 4, c0 = (tid % 16) * 4;
-    double acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
-    for (int p = 0; p < T; p++) {
-        double li[4], lj[4];
-#pragma unroll
-        for (int a = 0; a < 4; a++) li[a] = Li[r0 + a][p];
-#pragma unroll
-        for (int b = 0; b < 4; b++) lj[b] = Lj[c0 + b][p];
-#pragma unroll
-        for (int a = 0; a < 4; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc[a][b] = fma(li[a], lj[b], acc[a][b]);
-    }
+    const int r0 = (tid >> 5) * 4, c0 = (tid & 31) * 2;
+    double acc[4][2] = {};
+    tile_nt(Li, Lj, r0, c0, acc);
     double* Aij = Hd + (int64_t)i * T * npad + (int64_t)j * T;
 #pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) Aij[(int64_t)(r0 + a) * npad + c0 + b] -= acc[a][b];
+    for (int a = 0; a < 4; a++) {
+        double2* p = reinterpret_cast<double2*>(Aij + (int64_t)(r0 + a) * npad + c0);
+        double2 o = *p;
+        o.x -= acc[a][0];
+        o.y -= acc[a][1];
+        *p = o;
+    }
 }
 
-// Back substitution step k (k = nt-1 .. 0) of L^T x = y, y in the border row.
-// Every WG solves L_kk^T x_k = y_k; WG k stores x_k, WG j < k updates y_j -= L_kj^T x_k.
-__global__ __launch_bounds__(64) void back_step_kernel(double* __restrict__ Hd, int npad, int k,
-                                                       double* __restrict__ x,
-                                                       const int* __restrict__ flags) {
+// L^T x = y (y = forward-substituted border row), one 1024-thread workgroup:
+// for k = nt-1..0: x_k = Li_k^T y_k, then y_j -= L_kj^T x_k for every column left of k.
+constexpr int kBackThreads = 1024;
+constexpr int kMaxNpadBack = 8192;
+
+__global__ __launch_bounds__(kBackThreads) void chol_backsolve_kernel(
+    const double* __restrict__ Hd, int npad, const double* __restrict__ Linv,
+    double* __restrict__ x, const int* __restrict__ flags) {
     if (flags[kFlagDone]) return;
-    __shared__ double L[T][LD];
-    __shared__ double y[T];
+    __shared__ double y[kMaxNpadBack];
+    __shared__ double Li[T][T + 1];
+    __shared__ double part[16][T];
+    __shared__ double xk[T];
     const int tid = threadIdx.x;
-    const double* Akk = Hd + (int64_t)k * T * npad + (int64_t)k * T;
-    double* yrow = Hd + (int64_t)npad * npad;
-    for (int id = tid; id < T * T; id += blockDim.x) {
-        const int r = id / T, c = id % T;
-        L[r][c] = Akk[(int64_t)r * npad + c];
-    }
-    y[tid] = yrow[k * T + tid];
-    __syncthreads();
-    for (int c = T - 1; c >= 0; c--) {
-        if (tid == 0) y[c] = y[c] / L[c][c];
+    const int nt = npad / T;
+    const double* yrow = Hd + (int64_t)npad * npad;
+    for (int c = tid; c < npad; c += kBackThreads) y[c] = yrow[c];
+    for (int k = nt - 1; k >= 0; k--) {
+        const double* Lk = Linv + (int64_t)k * T * T;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int id = tid + q * kBackThreads;
+            Li[id >> 6][id & 63] = Lk[id];
+        }
         __syncthreads();
-        if (tid < c) y[tid] -= L[c][tid] * y[c];
+        {   // x_k[c] = sum_r Li[r][c] y_k[r]: 16 partial sums of 4 rows per column
+            const int c = tid & 63, g = tid >> 6;
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc += Li[g * 4 + q][c] * y[k * T + g * 4 + q];
+            part[g][c] = acc;
+        }
+        __syncthreads();
+        if (tid < T) {
+            double acc = 0.0;
+#pragma unroll
+            for (int g = 0; g < 16; g++) acc += part[g][tid];
+            xk[tid] = acc;
+            x[k * T + tid] = acc;
+        }
+        __syncthreads();
+        const double* Lrow = Hd + (int64_t)k * T * npad;  // row panel k: tiles (k, j<k)
+        for (int c = tid; c < k * T; c += kBackThreads) {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 16
+            for (int b = 0; b < T; b++) acc[b & 3] = fma(Lrow[(int64_t)b * npad + c], xk[b], acc[b & 3]);
+            y[c] -= (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        }
         __syncthreads();
     }
-    const int j = blockIdx.x;
-    if (j == k) {
-        x[k * T + tid] = y[tid];
-        return;
-    }
-    // y_j[a] -= sum_b L_kj[b][a] x_k[b]
-    const double* Lkj = Hd + (int64_t)k * T * npad + (int64_t)j * T;
-    double s = 0.0;
-    for (int b = 0; b < T; b++) s += Lkj[(int64_t)b * npad + tid] * y[b];
-    yrow[j * T + tid] -= s;
 }
 
 // dx = -x (or 0 if the factorisation failed), in-place retraction of poses 1..N-1,
@@ -678,23 +834,26 @@ hipError_t launch_compact(hipStream_t st, const double* edgeblk, const int* blk_
 }
 
 hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
-                        int npose, int n, int npad, double* Hd, double* x, int* flags) {
+                        int npose, int n, int npad, double* Hd, double* Linv, double* x,
+                        int* flags) {
     const int64_t total = (int64_t)(npad + kCholTile) * npad;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     hipLaunchKernelGGL(gn_fill_dense_kernel, dim3(blocks), dim3(256), 0, st, compact, slotmap,
                        nblk, npose, n, npad, Hd, flags);
     const int nt = npad / T;
     for (int k = 0; k < nt; k++) {
-        hipLaunchKernelGGL(chol_panel_kernel, dim3(nt - k + 1), dim3(256), 0, st, Hd, npad, k,
+        hipLaunchKernelGGL(chol_potrf_kernel, dim3(1), dim3(kPotrfThreads), 0, st, Hd, npad, k, Linv,
+                           flags);
+        hipLaunchKernelGGL(chol_trsm_kernel, dim3(nt - k), dim3(kGemmThreads), 0, st, Hd, npad, k, Linv,
                            flags);
         int nupd = 0;
         for (int j = k + 1; j < nt; j++) nupd += nt - j + 1;
         if (nupd > 0)
-            hipLaunchKernelGGL(chol_update_kernel, dim3(nupd), dim3(256), 0, st, Hd, npad, nt, k,
+            hipLaunchKernelGGL(chol_update_kernel, dim3(nupd), dim3(kGemmThreads), 0, st, Hd, npad, nt, k,
                                flags);
     }
-    for (int k = nt - 1; k >= 0; k--)
-        hipLaunchKernelGGL(back_step_kernel, dim3(k + 1), dim3(64), 0, st, Hd, npad, k, x, flags);
+    hipLaunchKernelGGL(chol_backsolve_kernel, dim3(1), dim3(kBackThreads), 0, st, Hd, npad, Linv,
+                       x, flags);
     return hipGetLastError();
 }
 
