@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -70,11 +71,21 @@ namespace {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Number of point chunks per directed edge: enough workgroups to fill 256 CUs several
-// times over, at least 1024 points (one 4-point step of every lane) per workgroup.
+// Number of point chunks per directed edge: chunks of ~kChunkTarget points (the per-XCD
+// working set of a chunk-major schedule is ~16 keyframes x chunk x 16 B), and at least
+// ~4096 workgroups overall when the edge count is small.
+int chunk_target() {
+    static int t = [] {
+        const char* e = getenv("M3S_ACC_CHUNK");
+        return e ? std::max(1024, atoi(e)) : 8192;
+    }();
+    return t;
+}
+
 int choose_nchunks(int64_t HW, int64_t E_local) {
-    const int64_t target_wgs = 8192;
-    int64_t nc = (target_wgs + std::max<int64_t>(E_local, 1) - 1) / std::max<int64_t>(E_local, 1);
+    int64_t nc = (HW + chunk_target() - 1) / chunk_target();
+    const int64_t want = (4096 + std::max<int64_t>(E_local, 1) - 1) / std::max<int64_t>(E_local, 1);
+    nc = std::max(nc, want);
     const int64_t max_nc = std::max<int64_t>(1, (HW + 1023) / 1024);
     nc = std::min(std::max<int64_t>(nc, 1), max_nc);
     int64_t chunk = align_up((size_t)((HW + nc - 1) / nc), 4);
@@ -88,7 +99,7 @@ int chunk_points(int64_t HW, int nchunks) {
 
 struct Layout {
     size_t partials, edgeblk, compact, dense, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent,
-        grad_ptr, grad_ent, slotmap, linv, total;
+        grad_ptr, grad_ent, slotmap, linv, sched, total;
     int nchunks, npad, nblk_max;
 };
 
@@ -119,6 +130,7 @@ Layout make_layout(int64_t N, int64_t HW, int64_t E_total, int64_t E_local) {
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
     L.slotmap = take(sizeof(int) * (size_t)npose * npose);
     L.linv = take(sizeof(double) * (size_t)L.npad * kCholTile);
+    L.sched = take(sizeof(int) * (size_t)E_local * L.nchunks);
     L.total = off;
     return L;
 }
@@ -130,8 +142,52 @@ struct Plan {
     std::vector<int> blk_ptr, blk_ent;            // CSR: slot -> (edge<<1 | neg)
     std::vector<int> grad_ptr, grad_ent;          // CSR: pose -> (edge<<1 | neg)
     std::vector<int> slotmap;                     // (npose x npose) -> slot or -1
+    std::vector<int> sched;                       // accumulate task order: e * nchunks + c
     float K[4] = {0, 0, 0, 0};
 };
+
+// XCD-aware order of the accumulate tasks (a performance heuristic only: results do not
+// depend on it).  Local directed edges sorted by (jx, ix) are split into 8 contiguous
+// groups, one per XCD (blocks b, b+8, ... share an XCD under round-robin dispatch); inside a
+// group tasks run chunk-major, so the few keyframes of a group stay L2-resident while all
+// of their edges stream the same point range.
+void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_loc, int nchunks,
+                    std::vector<int>& sched) {
+    const int E = (int)ii_loc.size();
+    sched.clear();
+    sched.reserve((size_t)E * nchunks);
+    static const bool off = [] {
+        const char* e = getenv("M3S_ACC_SCHED");
+        return e && atoi(e) == 0;
+    }();
+    if (off) {
+        for (int e = 0; e < E; e++)
+            for (int c = 0; c < nchunks; c++) sched.push_back(e * nchunks + c);
+        return;
+    }
+    std::vector<int> order(E);
+    for (int e = 0; e < E; e++) order[e] = e;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return jj_loc[a] != jj_loc[b] ? jj_loc[a] < jj_loc[b] : ii_loc[a] < ii_loc[b];
+    });
+    const int G = 8;
+    std::vector<std::vector<int>> lists(G);
+    for (int g = 0; g < G; g++) {
+        const int lo = (int)((int64_t)E * g / G), hi = (int)((int64_t)E * (g + 1) / G);
+        for (int c = 0; c < nchunks; c++)
+            for (int q = lo; q < hi; q++) lists[g].push_back(order[q] * nchunks + c);
+    }
+    std::vector<size_t> pos(G, 0);
+    for (bool any = true; any;) {
+        any = false;
+        for (int g = 0; g < G; g++) {
+            if (pos[g] < lists[g].size()) {
+                sched.push_back(lists[g][pos[g]++]);
+                any = true;
+            }
+        }
+    }
+}
 
 int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     const int64_t E = a.E_total;
@@ -265,6 +321,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     c.L = make_layout(a.N, a.HW, a.E_total, a.E_local);
     rc = build_plan(a, c.st, c.plan);
     if (rc) return rc;
+    build_schedule(c.plan.ii_loc, c.plan.jj_loc, c.L.nchunks, c.plan.sched);
     const Layout& L = c.L;
     const Plan& p = c.plan;
     auto up = [&](size_t off, const std::vector<int>& v) -> hipError_t {
@@ -278,6 +335,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     M3S_HIP_CHECK(up(L.grad_ptr, p.grad_ptr));
     M3S_HIP_CHECK(up(L.grad_ent, p.grad_ent));
     M3S_HIP_CHECK(up(L.slotmap, p.slotmap));
+    M3S_HIP_CHECK(up(L.sched, p.sched));
     M3S_HIP_CHECK(hipMemsetAsync(c.ws + L.flags, 0, sizeof(int) * kNumFlags, c.st));
     // the host vectors die with this call: wait for the (pageable) uploads
     M3S_HIP_CHECK(hipStreamSynchronize(c.st));
@@ -300,6 +358,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     P.inv_width = 1.0f / (float)P.width;
     P.HW = (int)a.HW;
     P.chunk = chunk_points(a.HW, L.nchunks);
+    P.nchunks = L.nchunks;
     auto al16 = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
     c.vec = (a.HW % 4 == 0) && al16(a.Xs) && al16(a.Cs) && al16(a.idx) && al16(a.valid) &&
             al16(a.Q);
@@ -312,9 +371,10 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
     int* flags = c.at<int>(L.flags);
     if (a.E_local > 0) {
         g_prof.mark(c.st);
-        M3S_HIP_CHECK(launch_accum(a.mode, c.vec, dim3(L.nchunks, (unsigned)a.E_local), c.st,
+        M3S_HIP_CHECK(launch_accum(a.mode, c.vec, dim3((unsigned)(L.nchunks * a.E_local)), c.st,
                                    a.Twc, a.Xs, a.Cs, c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
-                                   a.idx, a.valid, a.Q, c.P, c.at<float>(L.partials), flags));
+                                   a.idx, a.valid, a.Q, c.P, c.at<int>(L.sched),
+                                   c.at<float>(L.partials), flags));
         g_prof.mark(c.st);
         M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
                                          a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));

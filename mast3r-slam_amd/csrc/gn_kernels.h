@@ -28,13 +28,14 @@ struct AccParams {
     float inv_width;
     int width, height;
     int HW;
-    int chunk;  // points per workgroup (multiple of 4)
+    int chunk;    // points per workgroup (multiple of 4)
+    int nchunks;  // chunks per directed edge
 };
 
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
                         const int64_t* idx, const uint8_t* valid, const float* Q,
-                        const AccParams& P, float* partials, const int* flags);
+                        const AccParams& P, const int* sched, float* partials, const int* flags);
 hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
                               const float* Twc, const int* ii_loc, double* edgeblk,
                               const int* flags);

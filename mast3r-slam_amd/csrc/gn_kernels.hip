@@ -199,10 +199,12 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int64_t* __restrict__ idx,
     const uint8_t* __restrict__ valid, const float* __restrict__ Q, AccParams P,
-    float* __restrict__ partials, const int* __restrict__ flags) {
+    const int* __restrict__ sched, float* __restrict__ partials, const int* __restrict__ flags) {
     if (flags[kFlagDone]) return;
-    const int e = blockIdx.y;
-    const int c = blockIdx.x;
+    // XCD-aware task order (built by the driver): block b -> (edge, chunk)
+    const int task = sched[blockIdx.x];
+    const int e = task / P.nchunks;
+    const int c = task - e * P.nchunks;
     const int ix = ii_loc[e], jx = jj_loc[e];
     const Sim3f Ti = load_sim3(Twc + (int64_t)ix * 8);
     const Sim3f Tj = load_sim3(Twc + (int64_t)jx * 8);
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
         float s = red[0][tid];
 #pragma unroll
         for (int w = 1; w < kAccThreads / 64; w++) s += red[w][tid];
-        partials[((int64_t)e * gridDim.x + c) * kNaccPad + tid] = s;
+        partials[((int64_t)e * P.nchunks + c) * kNaccPad + tid] = s;
     }
 }
 
@@ -802,10 +804,10 @@ __global__ __launch_bounds__(256) void gn_retract_kernel(float* __restrict__ Twc
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
                         const int64_t* idx, const uint8_t* valid, const float* Q,
-                        const AccParams& P, float* partials, const int* flags) {
+                        const AccParams& P, const int* sched, float* partials, const int* flags) {
 #define M3S_ACC(MODE, V)                                                                    \
     hipLaunchKernelGGL((gn_accum_kernel<MODE, V>), grid, dim3(kAccThreads), 0, st, Twc, Xs, \
-                       Cs, ii_loc, jj_loc, idx, valid, Q, P, partials, flags)
+                       Cs, ii_loc, jj_loc, idx, valid, Q, P, sched, partials, flags)
     if (mode == GN_RAYS) {
         if (vec) M3S_ACC(GN_RAYS, true); else M3S_ACC(GN_RAYS, false);
     } else if (mode == GN_CALIB) {
