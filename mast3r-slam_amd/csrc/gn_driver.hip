@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <utility>
 #include <vector>
@@ -143,6 +144,7 @@ struct Plan {
     std::vector<int> grad_ptr, grad_ent;          // CSR: pose -> (edge<<1 | neg)
     std::vector<int> slotmap;                     // (npose x npose) -> slot or -1
     std::vector<int> sched;                       // accumulate task order: e * nchunks + c
+    std::vector<std::pair<int, int>> pairs;       // slot nblk0.. -> unordered pose pair (a<b)
     float K[4] = {0, 0, 0, 0};
 };
 
@@ -271,11 +273,193 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     }
     plan.slotmap.assign((size_t)std::max(npose, 0) * std::max(npose, 0), -1);
     for (int p = 0; p < npose; p++) plan.slotmap[(size_t)p * npose + p] = p;
+    plan.pairs.assign(plan.nblk - npose, std::make_pair(0, 0));
     for (auto& kv : slot_of) {
         const int r = kv.first.first, c = kv.first.second;
         plan.slotmap[(size_t)r * npose + c] = kv.second;
         plan.slotmap[(size_t)c * npose + r] = kv.second;
+        plan.pairs[kv.second - npose] = kv.first;
     }
+    return M3S_OK;
+}
+
+
+// ---------------------------------------------------------------------------------
+// Block-sparse elimination plan (gn_sparse.hip): rounds of independent low-degree poses,
+// then a dense core.  Built once per GN call (the pose graph is fixed across iterations).
+// ---------------------------------------------------------------------------------
+struct SpRound {
+    int node_begin, nnodes, tbeg, nbt, rbeg, nrt;
+};
+
+struct SparsePlan {
+    bool enabled = false;
+    int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0;
+    std::vector<SpRound> rounds;
+    std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
+    // device (one stream-ordered allocation per call)
+    char* dbuf = nullptr;
+    size_t o_A = 0, o_b = 0, o_y = 0, o_L = 0, o_W = 0, o_xd = 0, o_int = 0;
+    size_t i_nodes = 0, i_fptr = 0, i_fronts = 0, i_tg = 0, i_tc = 0, i_rtg = 0, i_rc = 0,
+           i_tail = 0, i_tmap = 0;
+    template <typename T>
+    T* dptr(size_t off) const { return reinterpret_cast<T*>(dbuf + off); }
+    const int* iptr(size_t i) const { return reinterpret_cast<const int*>(dbuf + o_int) + i; }
+};
+
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+void build_sparse_plan(const Plan& p, int npose, SparsePlan& sp) {
+    const int dcap = env_int("M3S_SPARSE_DCAP", 16);
+    const int rmin = env_int("M3S_SPARSE_RMIN", 2);
+    const int rmax = env_int("M3S_SPARSE_RMAX", 64);
+    std::vector<std::set<int>> adj(npose);
+    std::map<std::pair<int, int>, int> bid;
+    for (size_t k = 0; k < p.pairs.size(); k++) {
+        const int a = p.pairs[k].first, b = p.pairs[k].second;
+        adj[a].insert(b);
+        adj[b].insert(a);
+        bid[p.pairs[k]] = npose + (int)k;
+    }
+    sp.nblocks = p.nblk;
+    auto block_of = [&](int x, int y) -> int {
+        if (x == y) return x;
+        const auto key = std::make_pair(std::min(x, y), std::max(x, y));
+        auto it = bid.find(key);
+        if (it != bid.end()) return it->second;
+        bid[key] = sp.nblocks;
+        return sp.nblocks++;
+    };
+    std::vector<char> alive(npose, 1);
+    int nalive = npose;
+    sp.fptr.assign(1, 0);
+    for (int round = 0; round < rmax && nalive > 0; round++) {
+        std::vector<int> cand;
+        for (int v = 0; v < npose; v++)
+            if (alive[v] && (int)adj[v].size() <= dcap) cand.push_back(v);
+        std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) {
+            return adj[a].size() != adj[b].size() ? adj[a].size() < adj[b].size() : a < b;
+        });
+        std::vector<char> blocked(npose, 0);
+        std::vector<int> chosen;
+        for (int v : cand) {
+            if (blocked[v]) continue;
+            chosen.push_back(v);
+            blocked[v] = 1;
+            for (int r : adj[v]) blocked[r] = 1;
+        }
+        if ((int)chosen.size() < rmin && (int)chosen.size() != nalive) break;
+        std::sort(chosen.begin(), chosen.end());
+        SpRound R;
+        R.node_begin = (int)sp.nodes.size();
+        R.nnodes = (int)chosen.size();
+        std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> tgt;
+        std::map<int, std::vector<std::pair<int, int>>> rtgt;
+        std::vector<std::vector<int>> F(chosen.size());
+        for (size_t q = 0; q < chosen.size(); q++) {
+            const int v = chosen[q];
+            F[q].assign(adj[v].begin(), adj[v].end());
+            sp.nodes.push_back(v);
+            std::map<int, int> wof;
+            for (int r : F[q]) {
+                const int blk = block_of(r, v);
+                const int wid = sp.nW++;
+                sp.fronts.insert(sp.fronts.end(), {r, blk, r > v ? 1 : 0, wid});
+                wof[r] = wid;
+            }
+            sp.fptr.push_back((int)sp.fronts.size() / 4);
+            for (size_t i = 0; i < F[q].size(); i++)
+                for (size_t j = i; j < F[q].size(); j++) {
+                    const int r = F[q][i], s2 = F[q][j];  // r <= s2 (sorted)
+                    tgt[std::make_pair(r, s2)].push_back(std::make_pair(wof[r], wof[s2]));
+                }
+            for (int r : F[q]) rtgt[r].push_back(std::make_pair(wof[r], v));
+        }
+        R.tbeg = (int)sp.tg.size() / 3;
+        for (auto& kv : tgt) {
+            const int blk = block_of(kv.first.first, kv.first.second);
+            const int c0 = (int)sp.tc.size() / 2;
+            for (auto& pr : kv.second) sp.tc.insert(sp.tc.end(), {pr.first, pr.second});
+            sp.tg.insert(sp.tg.end(), {blk, c0, (int)sp.tc.size() / 2});
+        }
+        R.nbt = (int)tgt.size();
+        R.rbeg = (int)sp.rtg.size() / 3;
+        for (auto& kv : rtgt) {
+            const int c0 = (int)sp.rc.size() / 2;
+            for (auto& pr : kv.second) sp.rc.insert(sp.rc.end(), {pr.first, pr.second});
+            sp.rtg.insert(sp.rtg.end(), {kv.first, c0, (int)sp.rc.size() / 2});
+        }
+        R.nrt = (int)rtgt.size();
+        sp.rounds.push_back(R);
+        // eliminate: drop the poses, connect each front into a clique (fill)
+        for (size_t q = 0; q < chosen.size(); q++) {
+            const int v = chosen[q];
+            for (int r : F[q]) adj[r].erase(v);
+            for (int r : F[q])
+                for (int s2 : F[q])
+                    if (r != s2) adj[r].insert(s2);
+            adj[v].clear();
+            alive[v] = 0;
+            nalive--;
+        }
+    }
+    for (int v = 0; v < npose; v++)
+        if (alive[v]) sp.tail.push_back(v);
+    sp.ntail = (int)sp.tail.size();
+    sp.npad_tail = sp.ntail > 0 ? (int)align_up((size_t)sp.ntail * 7, kCholTile) : 0;
+    sp.tmap.assign((size_t)sp.ntail * sp.ntail, -1);
+    for (int i = 0; i < sp.ntail; i++)
+        for (int j = 0; j < sp.ntail; j++) {
+            const int x = sp.tail[i], y = sp.tail[j];
+            int code = -1;
+            if (x == y) {
+                code = 2 * x;
+            } else {
+                auto it = bid.find(std::make_pair(std::min(x, y), std::max(x, y)));
+                if (it != bid.end()) code = 2 * it->second + (x > y ? 1 : 0);
+            }
+            sp.tmap[(size_t)i * sp.ntail + j] = code;
+        }
+    sp.enabled = true;
+}
+
+int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + std::max<size_t>(bytes, 8), 256);
+        return o;
+    };
+    sp.o_A = take(sizeof(double) * 49 * (size_t)sp.nblocks);
+    sp.o_b = take(sizeof(double) * 7 * (size_t)npose);
+    sp.o_y = take(sizeof(double) * 7 * (size_t)npose);
+    sp.o_L = take(sizeof(double) * 49 * sp.nodes.size());
+    sp.o_W = take(sizeof(double) * 49 * (size_t)sp.nW);
+    sp.o_xd = take(sizeof(double) * (size_t)std::max(sp.npad_tail, 1));
+    std::vector<int> ints;
+    auto put = [&](const std::vector<int>& v) {
+        size_t i = ints.size();
+        ints.insert(ints.end(), v.begin(), v.end());
+        return i;
+    };
+    sp.i_nodes = put(sp.nodes);
+    sp.i_fptr = put(sp.fptr);
+    sp.i_fronts = put(sp.fronts);
+    sp.i_tg = put(sp.tg);
+    sp.i_tc = put(sp.tc);
+    sp.i_rtg = put(sp.rtg);
+    sp.i_rc = put(sp.rc);
+    sp.i_tail = put(sp.tail);
+    sp.i_tmap = put(sp.tmap);
+    sp.o_int = take(sizeof(int) * std::max<size_t>(ints.size(), 1));
+    M3S_HIP_CHECK(hipMallocAsync((void**)&sp.dbuf, off, st));
+    if (!ints.empty())
+        M3S_HIP_CHECK(hipMemcpyAsync(sp.dbuf + sp.o_int, ints.data(), sizeof(int) * ints.size(),
+                                     hipMemcpyHostToDevice, st));
+    M3S_HIP_CHECK(hipStreamSynchronize(st));  // the host vector dies with this call
     return M3S_OK;
 }
 
@@ -305,6 +489,7 @@ int validate(const m3s_gn_args& a) {
 struct Ctx {
     Layout L;
     Plan plan;
+    SparsePlan sp;
     AccParams P;
     bool vec;
     char* ws;
@@ -392,6 +577,41 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
     return M3S_OK;
 }
 
+int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
+    const Layout& L = c.L;
+    const int npose = (int)(a.N - 1);
+    int* flags = c.at<int>(L.flags);
+    if (!c.sp.enabled) {
+        M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.at<int>(L.slotmap), c.plan.nblk,
+                                   npose, 7 * npose, L.npad, c.at<double>(L.dense),
+                                   c.at<double>(L.linv), c.at<double>(L.x), flags));
+        return M3S_OK;
+    }
+    SparsePlan& sp = c.sp;
+    double* A = sp.dptr<double>(sp.o_A);
+    double* b = sp.dptr<double>(sp.o_b);
+    double* y = sp.dptr<double>(sp.o_y);
+    double* Ls = sp.dptr<double>(sp.o_L);
+    double* W = sp.dptr<double>(sp.o_W);
+    double* x = c.at<double>(L.x);
+    M3S_HIP_CHECK(launch_sp_init(c.st, c.at<double>(L.compact), c.plan.nblk, sp.nblocks, npose, A, b,
+                                 flags));
+    for (const SpRound& R : sp.rounds) {
+        M3S_HIP_CHECK(launch_sp_factor(c.st, R.nnodes, sp.iptr(sp.i_nodes), sp.iptr(sp.i_fptr),
+                                       sp.iptr(sp.i_fronts), R.node_begin, A, b, Ls, W, y, flags));
+        M3S_HIP_CHECK(launch_sp_schur(c.st, sp.iptr(sp.i_tg), sp.iptr(sp.i_tc), R.tbeg, R.nbt,
+                                      sp.iptr(sp.i_rtg), sp.iptr(sp.i_rc), R.rbeg, R.nrt, W, y, A, b,
+                                      flags));
+    }
+    M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
+                                 sp.npad_tail, c.at<double>(L.dense), c.at<double>(L.linv),
+                                 sp.dptr<double>(sp.o_xd), x, flags));
+    for (auto it = sp.rounds.rbegin(); it != sp.rounds.rend(); ++it)
+        M3S_HIP_CHECK(launch_sp_back(c.st, it->nnodes, sp.iptr(sp.i_nodes), sp.iptr(sp.i_fptr),
+                                     sp.iptr(sp.i_fronts), it->node_begin, Ls, W, y, x, flags));
+    return M3S_OK;
+}
+
 int run(const m3s_gn_args& a) {
     Ctx c;
     int rc = setup(a, c);
@@ -400,19 +620,24 @@ int run(const m3s_gn_args& a) {
     if (npose <= 0) return M3S_OK;  // nothing to optimise (all poses pinned)
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
+    if (env_int("M3S_SOLVER_DENSE", 0) == 0) {
+        build_sparse_plan(c.plan, npose, c.sp);
+        rc = upload_sparse_plan(c.sp, npose, c.st);
+        if (rc) return rc;
+    }
     for (int itr = 0; itr < a.max_iter; itr++) {
         g_prof.mark(c.st);
         rc = enqueue_system(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
-        M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.at<int>(L.slotmap),
-                                   c.plan.nblk, npose, 7 * npose, L.npad, c.at<double>(L.dense),
-                                   c.at<double>(L.linv), c.at<double>(L.x), flags));
+        rc = enqueue_solve(a, c);
+        if (rc) return rc;
         g_prof.mark(c.st);
         M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
                                      a.delta_thresh, flags));
         g_prof.mark(c.st);
     }
+    if (c.sp.dbuf) M3S_HIP_CHECK(hipFreeAsync(c.sp.dbuf, c.st));
     return M3S_OK;
 }
 

@@ -835,13 +835,8 @@ hipError_t launch_compact(hipStream_t st, const double* edgeblk, const int* blk_
     return hipGetLastError();
 }
 
-hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
-                        int npose, int n, int npad, double* Hd, double* Linv, double* x,
-                        int* flags) {
-    const int64_t total = (int64_t)(npad + kCholTile) * npad;
-    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(gn_fill_dense_kernel, dim3(blocks), dim3(256), 0, st, compact, slotmap,
-                       nblk, npose, n, npad, Hd, flags);
+hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
+                                     double* x, int* flags) {
     const int nt = npad / T;
     for (int k = 0; k < nt; k++) {
         hipLaunchKernelGGL(chol_potrf_kernel, dim3(1), dim3(kPotrfThreads), 0, st, Hd, npad, k, Linv,
@@ -857,6 +852,18 @@ hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotma
     hipLaunchKernelGGL(chol_backsolve_kernel, dim3(1), dim3(kBackThreads), 0, st, Hd, npad, Linv,
                        x, flags);
     return hipGetLastError();
+}
+
+hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
+                        int npose, int n, int npad, double* Hd, double* Linv, double* x,
+                        int* flags) {
+    const int64_t total = (int64_t)(npad + kCholTile) * npad;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(gn_fill_dense_kernel, dim3(blocks), dim3(256), 0, st, compact, slotmap,
+                       nblk, npose, n, npad, Hd, flags);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_dense_factor_solve(st, npad, Hd, Linv, x, flags);
 }
 
 hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,

@@ -30,6 +30,11 @@ for s in $STEPS; do
         timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
         rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -n 5 gpurun_out/bench.err
         ok_or_fail $rc bench ;;
+    benchdense)
+        M3S_SOLVER_DENSE=1 timeout -k 10 600 python bench.py --no-cpu-baseline \
+            > gpurun_out/bench_dense.json 2> gpurun_out/bench_dense.err
+        rc=$?; echo "bench (dense solver) rc=$rc"; cat gpurun_out/bench_dense.json
+        ok_or_fail $rc benchdense ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
             -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline \
