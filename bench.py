@@ -11,9 +11,12 @@ N > 1 (torchrun, one process per GPU): the SAME graph is edge-sharded across ran
 per-iteration compact Hessian is summed with an RCCL all-reduce inside the op -> strong
 scaling; value = total pair-iterations / max-over-ranks wall time.
 
-Extra fields: ``roofline`` for the dominant kernel (the accumulate kernel, HBM-bound,
-45 algorithmic bytes per directed point-edge, timed with HIP events on its stream during
-the timed steps) and ``cpu_baseline`` (the CPU oracle -- a restatement of the reference
+Extra fields: ``roofline`` for the dominant kernel (the per-iteration accumulate kernel,
+HBM-bound, timed with HIP events on its stream during the timed steps).  Its algorithmic bytes
+are those of the packed formulation it runs: per directed point-edge the 8-B
+iteration-invariant record {match | invalid bit, sqrt q} + Xj 12 B + the matched point (calib:
+its depth, 4 B; rays: Xi, 12 B) = 24 / 32 B; the reference formulation's 45 B
+is reported beside it as ``ref_formulation_*`` and ``cpu_baseline`` (the CPU oracle -- a restatement of the reference
 backend, which has no CPU implementation -- on a bounded sample, rank 0, N = 1 only).
 """
 from __future__ import annotations
@@ -33,7 +36,9 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "keyframe-pair GN iters/sec @512×384, 256 edges; ATE-RMSE vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-BYTES_PER_POINT_EDGE = 45  # Xj 12 + Xi 12 + Cj 4 + Ci 4 + Q 4 + idx 8 + valid 1
+REF_BYTES_PER_POINT_EDGE = 45  # Xj 12 + Xi 12 + Cj 4 + Ci 4 + Q 4 + idx 8 + valid 1
+# packed formulation (>= 3 iterations per call): record 8 + Xj 12 + matched point (calib: z 4; else Xi 12)
+PACKED_BYTES_PER_POINT_EDGE = {"calib": 24, "rays": 32, "points": 32}
 LOCAL = dict(sigma_ray=0.003, sigma_dist=10.0, sigma_pixel=1.0, sigma_depth=10.0, sigma_point=0.05,
              C_conf=0.0, Q_conf=1.5, pixel_border=-10, depth_eps=1e-6)  # base.yaml:35-50
 
@@ -121,13 +126,17 @@ def main():
     value = pair_iters / elapsed
     n_it = max(nprof.value, 1)
     acc_ms = prof[0] / n_it
-    bytes_launch = BYTES_PER_POINT_EDGE * g.HW * (hi - lo)
+    packed = iters >= 3 and os.environ.get("M3S_GN_PACK", "1") != "0"
+    bpe = PACKED_BYTES_PER_POINT_EDGE[mode] if packed else REF_BYTES_PER_POINT_EDGE
+    bytes_launch = bpe * g.HW * (hi - lo)
+    ref_bytes_launch = REF_BYTES_PER_POINT_EDGE * g.HW * (hi - lo)
     achieved = bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
     traffic = None
     if os.path.exists(args.traffic_file):
         try:
             tf = json.load(open(args.traffic_file))
-            if tf.get("config") == args.config and tf.get("n_gpus", 1) == world:
+            if (tf.get("config") == args.config and tf.get("n_gpus", 1) == world
+                    and tf.get("packed", False) == packed):
                 traffic = tf.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -164,7 +173,7 @@ def main():
             "retract": prof[3] / n_it,
         },
         "roofline": {
-            "kernel": f"gn_accum_kernel<{mode}>",
+            "kernel": f"gn_accum_packed_kernel<{mode}>" if packed else f"gn_accum_kernel<{mode}>",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
@@ -172,7 +181,10 @@ def main():
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_launch,
+            "algorithmic_bytes_per_point_edge": bpe,
             "avg_launch_ms": acc_ms,
+            "ref_formulation_bytes_per_launch": ref_bytes_launch,
+            "ref_formulation_equiv_GBps": ref_bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None,
         },
         "cpu_baseline": None,
     }

@@ -1,0 +1,587 @@
+// gn_accum.hip -- the per-iteration accumulate of the Sim3 Gauss-Newton backend (gfx950).
+//
+//   gn_pack_kernel           once per call: the iteration-invariant packed stream
+//                            {match index | invalid bit, sqrt q} per directed point-edge
+//   gn_depth_kernel          once per call (calib): the keyframes' depths as a dense array
+//   gn_accum_packed_kernel   per iteration: accumulate the unique entries of
+//                            M = sum w r r^T and g = sum w e r over RAW (pre-adjoint) Jacobian
+//                            rows from the packed stream (>= 3 iterations per call)
+//   gn_accum_kernel          per iteration, reading the reference's tensors directly
+// Replaces ray_align / calib_proj / point_align (reference gn_kernels.cu:813-1138, 1231-1543,
+// 455-723); the adjoint and the 4-block expansion happen per edge in gn_kernels.hip.
+// Built with -fno-slp-vectorize (Makefile): the SLP vectorizer re-packs the scalar path into
+// v_pk ops with register shuffles (204 instead of 92 VGPRs).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "gn_kernels.h"
+#include "sim3.h"
+
+namespace m3s {
+
+// ---------------------------------------------------------------------------
+// Point math, one point-edge per call, generic in the value type V (float here; a packed
+// float2 pair variant was measured: on gfx950 a v_pk_*_f32 op costs the SIMD twice the cycles
+// of a scalar one, so pairs only save issue slots while doubling the accumulator VGPRs
+// (144 vs 92, 3 vs 5 waves/SIMD) and ran 10 % slower -- the kernel is latency-bound).
+// ---------------------------------------------------------------------------
+template <typename V>
+struct VMask {
+    typedef bool type;
+};
+
+__device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ float vsplat(float s, float) { return s; }
+__device__ __forceinline__ float vrcp(float a) { return __builtin_amdgcn_rcpf(a); }    // v_rcp_f32
+__device__ __forceinline__ float vsqrt(float a) { return __builtin_amdgcn_sqrtf(a); }  // normal or 0 inputs
+__device__ __forceinline__ float vlog2(float a) { return __builtin_amdgcn_logf(a); }   // inputs > z_eps
+__device__ __forceinline__ float vabs(float a) { return fabsf(a); }
+__device__ __forceinline__ float vmin(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ float vsel(bool m, float a, float b) { return m ? a : b; }
+__device__ __forceinline__ bool vgt(float a, float b) { return a > b; }
+__device__ __forceinline__ bool vlt(float a, float b) { return a < b; }
+__device__ __forceinline__ bool vand(bool a, bool b) { return a && b; }
+
+// Huber weight (gn_kernels.cu:172-175): |r| < 1.345 ? 1 : 1.345/|r|, as min(1, 1.345/|r|)
+// (3 VALU, no compare/select; equal up to the 1-ulp reciprocal at |r| ~ 1.345).
+template <typename V>
+__device__ __forceinline__ V huber(V r) {
+    return vmin(vsplat(1.345f, r) * vrcp(vabs(r)), 1.0f);
+}
+
+// Accumulate one raw Jacobian row r (compile-time nonzero mask) with weight w, residual e.
+template <int MASK, typename V>
+__device__ __forceinline__ void acc_row(V* __restrict__ acc, const V* r, V w, V e) {
+    V wr[7];
+#pragma unroll
+    for (int a = 0; a < 7; a++) wr[a] = (MASK >> a & 1) ? w * r[a] : V(0.0f);
+#pragma unroll
+    for (int a = 0; a < 7; a++) {
+        if (!(MASK >> a & 1)) continue;
+#pragma unroll
+        for (int b = a; b < 7; b++) {
+            if (!(MASK >> b & 1)) continue;
+            acc[sym_idx(a, b)] = vfma(wr[a], r[b], acc[sym_idx(a, b)]);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 7; a++)
+        if (MASK >> a & 1) acc[28 + a] = vfma(wr[a], e, acc[28 + a]);
+}
+
+template <typename V>
+struct PointsIn {
+    V xi0, xi1, xi2, xj0, xj1, xj2;
+    V sq;                            // sqrt(q)
+    typename VMask<V>::type valid;   // match & q > Q_thresh & ci > C_thresh & cj > C_thresh
+    V ut, vt;  // calib: pixel of the match, (ind % W, ind / W) as float
+};
+
+// T_ij * Xj with the reference's quaternion formula (act_so3 + scale + translation,
+// gn_kernels.cu:195-205, 252-272), on one point or a packed pair.
+template <typename V>
+__device__ __forceinline__ void apply_rel(const Sim3f& T, V x0, V x1, V x2, V& X0, V& X1, V& X2) {
+    const V q0 = vsplat(T.q[0], x0), q1 = vsplat(T.q[1], x0), q2 = vsplat(T.q[2], x0),
+            q3 = vsplat(T.q[3], x0), two = vsplat(2.0f, x0);
+    const V uv0 = two * (q1 * x2 - q2 * x1);
+    const V uv1 = two * (q2 * x0 - q0 * x2);
+    const V uv2 = two * (q0 * x1 - q1 * x0);
+    const V y0 = (x0 + q3 * uv0) + (q1 * uv2 - q2 * uv1);
+    const V y1 = (x1 + q3 * uv1) + (q2 * uv0 - q0 * uv2);
+    const V y2 = (x2 + q3 * uv2) + (q0 * uv1 - q1 * uv0);
+    const V s = vsplat(T.s, x0);
+    X0 = y0 * s + vsplat(T.t[0], x0);
+    X1 = y1 * s + vsplat(T.t[1], x0);
+    X2 = y2 * s + vsplat(T.t[2], x0);
+}
+
+// One (pair of) point-edge(s): residuals, robust weights, raw rows -> acc.
+template <int MODE, typename V>
+__device__ __forceinline__ void point_body(const PointsIn<V>& p, const Sim3f& T, const AccParams& P,
+                                           V* __restrict__ acc) {
+    V X0, X1, X2;
+    apply_rel(T, p.xj0, p.xj1, p.xj2, X0, X1, X2);
+    auto valid = p.valid;
+    const V zero = vsplat(0.0f, X0);
+    const V sq = p.sq;
+
+    if constexpr (MODE == GN_RAYS) {
+        // gn_kernels.cu:924-1089
+        const V n2i = vfma(p.xi0, p.xi0, vfma(p.xi1, p.xi1, p.xi2 * p.xi2));
+        const V n1i = vsqrt(n2i);
+        const V n1i_inv = vrcp(n1i);
+        const V n2j = vfma(X0, X0, vfma(X1, X1, X2 * X2));
+        const V n1j = vsqrt(n2j);
+        const V n1j_inv = vrcp(n1j);
+        const V rx = n1j_inv * X0, ry = n1j_inv * X1, rz = n1j_inv * X2;
+        const V e0 = rx - n1i_inv * p.xi0;
+        const V e1 = ry - n1i_inv * p.xi1;
+        const V e2 = rz - n1i_inv * p.xi2;
+        const V e3 = n1j - n1i;
+        const V swr = vsel(valid, vsplat(P.s0_inv, sq) * sq, zero);
+        const V swd = vsel(valid, vsplat(P.s1_inv, sq) * sq, zero);
+        const V wcr = swr * swr, wcd = swd * swd;
+        const V w0 = huber(swr * e0) * wcr;
+        const V w1 = huber(swr * e1) * wcr;
+        const V w2 = huber(swr * e2) * wcr;
+        const V w3 = huber(swd * e3) * wcd;
+        const V n3 = n1j_inv * vrcp(n2j);
+        const V dxx = n1j_inv - X0 * X0 * n3;
+        const V dyy = n1j_inv - X1 * X1 * n3;
+        const V dzz = n1j_inv - X2 * X2 * n3;
+        const V dxy = -X0 * X1 * n3;
+        const V dxz = -X0 * X2 * n3;
+        const V dyz = -X1 * X2 * n3;
+        {
+            const V r[7] = {dxx, dxy, dxz, zero, rz, -ry, zero};
+            acc_row<0b0110111>(acc, r, w0, e0);
+        }
+        {
+            const V r[7] = {dxy, dyy, dyz, -rz, zero, rx, zero};
+            acc_row<0b0101111>(acc, r, w1, e1);
+        }
+        {
+            const V r[7] = {dxz, dyz, dzz, ry, -rx, zero, zero};
+            acc_row<0b0011111>(acc, r, w2, e2);
+        }
+        {
+            const V r[7] = {rx, ry, rz, zero, zero, zero, n1j};
+            acc_row<0b1000111>(acc, r, w3, e3);
+        }
+    } else if constexpr (MODE == GN_CALIB) {
+        // gn_kernels.cu:1360-1495
+        const auto valid_z = vand(vgt(X2, P.z_eps), vgt(p.xi2, P.z_eps));
+        const V zj_inv = vsel(valid_z, vrcp(X2), zero);
+        // log(zj) - log(zi) (gn_kernels.cu:1385-1390) as ln2 * log2(zj / zi): the residual is a
+        // small difference of two ~unit logs, so one log of the ratio keeps it to ~1e-7
+        // relative where two float logs lose ~1e-4 of it to cancellation (inf/NaN still
+        // propagate: 1/inf = 0 -> -inf).
+        const V e2 = vsel(valid_z, vsplat(0.69314718055994531f, X2) * vlog2(X2 * vrcp(p.xi2)), zero);
+        const V x = X0 * zj_inv, y = X1 * zj_inv;
+        const V u = vfma(vsplat(P.fx, x), x, vsplat(P.cx, x));
+        const V v = vfma(vsplat(P.fy, y), y, vsplat(P.cy, y));
+        valid = vand(vand(valid, valid_z),
+                     vand(vand(vgt(u, P.pb_lo), vlt(u, P.pb_hi_u)), vand(vgt(v, P.pb_lo), vlt(v, P.pb_hi_v))));
+        const V e0 = u - p.ut;
+        const V e1 = v - p.vt;
+        const V swp = vsel(valid, vsplat(P.s0_inv, sq) * sq, zero);
+        const V swd = vsel(valid, vsplat(P.s1_inv, sq) * sq, zero);
+        const V wcp = swp * swp, wcd = swd * swd;
+        const V w0 = huber(swp * e0) * wcp;
+        const V w1 = huber(swp * e1) * wcp;
+        const V w2 = huber(swd * e2) * wcd;
+        const V fx = vsplat(P.fx, x), fy = vsplat(P.fy, x), one = vsplat(1.0f, x);
+        const V xz = x * zj_inv, yz = y * zj_inv, xy = x * y;
+        {
+            const V r[7] = {fx * zj_inv, zero, -fx * xz, -fx * xy, fx * vfma(x, x, one), -fx * y, zero};
+            acc_row<0b0111101>(acc, r, w0, e0);
+        }
+        {
+            const V r[7] = {zero, fy * zj_inv, -fy * yz, -fy * vfma(y, y, one), fy * xy, fy * x, zero};
+            acc_row<0b0111110>(acc, r, w1, e1);
+        }
+        {
+            const V r[7] = {zero, zero, zj_inv, y, -x, zero, one};
+            acc_row<0b1011100>(acc, r, w2, e2);
+        }
+    } else {
+        // point_align_kernel, gn_kernels.cu:564-674
+        const V e0 = X0 - p.xi0, e1 = X1 - p.xi1, e2 = X2 - p.xi2;
+        const V swp = vsel(valid, vsplat(P.s0_inv, sq) * sq, zero);
+        const V wc = swp * swp;
+        const V w0 = huber(swp * e0) * wc;
+        const V w1 = huber(swp * e1) * wc;
+        const V w2 = huber(swp * e2) * wc;
+        const V one = vsplat(1.0f, X0);
+        {
+            const V r[7] = {one, zero, zero, zero, X2, -X1, X0};
+            acc_row<0b1110001>(acc, r, w0, e0);
+        }
+        {
+            const V r[7] = {zero, one, zero, -X2, zero, X0, X1};
+            acc_row<0b1101010>(acc, r, w1, e1);
+        }
+        {
+            const V r[7] = {zero, zero, one, X1, -X0, zero, X2};
+            acc_row<0b1011100>(acc, r, w2, e2);
+        }
+    }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Match index of a point: invalid -> 0 (the reference's `valid ? idx : 0`); an index outside
+// [0, HW) is clamped to HW-1 (the reference would read out of bounds).
+__device__ __forceinline__ int match_index(int64_t id, bool vm, int HW) {
+    const uint64_t u = (uint64_t)id;
+    const int c = u < (uint64_t)HW ? (int)u : HW - 1;
+    return vm ? c : 0;
+}
+
+// ind / W and ind % W exactly by multiply-shift (Granlund-Montgomery, ind < 2^31).
+__device__ __forceinline__ void pixel_of(int ind, const AccParams& P, float& ut, float& vt) {
+    const unsigned q = (unsigned)(((uint64_t)(unsigned)ind * P.div_m) >> P.div_sh);
+    vt = (float)(int)q;
+    ut = (float)(ind - (int)q * P.width);
+}
+
+// Deterministic workgroup reduction of the 35 sums: wave butterfly, then the 4 waves in fixed
+// order; one 36-float partial per (edge, chunk).
+__device__ __forceinline__ void block_partial(const float* accs, float* __restrict__ out) {
+    __shared__ float red[kAccThreads / 64][kNacc];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int q = 0; q < kNacc; q++) {
+        const float s = wave_sum(accs[q]);
+        if (lane == 0) red[wave][q] = s;
+    }
+    __syncthreads();
+    if (tid < kNacc) {
+        float s = red[0][tid];
+#pragma unroll
+        for (int w = 1; w < kAccThreads / 64; w++) s += red[w][tid];
+        out[tid] = s;
+    }
+}
+
+
+// One pipeline stage of the packed accumulate: the records, Xj and the gathered matched points
+// of 4 consecutive points of one lane.
+template <int MODE>
+struct AccStage {
+    int4 ka, kb;         // {code, sqrt q} x 2 points each
+    float4 xa, xb, xc;   // Xj of the 4 points
+    float g[4][3];       // gathered matched point (calib: depth only, in g[s][2])
+
+    // Zi_b: the dense depth array (packed path), or nullptr to read the depth from Xs
+    template <int M>
+    __device__ __forceinline__ void load(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
+                                         const float* __restrict__ Zi_b, int k) {
+        xa = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
+        xb = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
+        xc = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
+        const int ind[4] = {ka.x & 0x7fffffff, ka.z & 0x7fffffff, kb.x & 0x7fffffff, kb.z & 0x7fffffff};
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            if constexpr (M == GN_CALIB) {
+                g[s][2] = Zi_b ? Zi_b[ind[s]] : Xi_b[(int64_t)ind[s] * 3 + 2];
+            } else {
+                const float* xp = Xi_b + (int64_t)ind[s] * 3;
+                g[s][0] = xp[0];
+                g[s][1] = xp[1];
+                g[s][2] = xp[2];
+            }
+        }
+    }
+
+    // the 4 points one at a time on scalar accumulators
+    template <int M>
+    __device__ __forceinline__ void compute(const Sim3f& T, const AccParams& P, float* __restrict__ acc) const {
+        const int codes[4] = {ka.x, ka.z, kb.x, kb.z};
+        const int sqb[4] = {ka.y, ka.w, kb.y, kb.w};
+        const float xj[12] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w, xc.x, xc.y, xc.z, xc.w};
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            PointsIn<float> p;
+            if constexpr (M == GN_CALIB) {
+                p.xi0 = p.xi1 = 0.0f;
+                pixel_of(codes[s] & 0x7fffffff, P, p.ut, p.vt);
+            } else {
+                p.xi0 = g[s][0];
+                p.xi1 = g[s][1];
+            }
+            p.xi2 = g[s][2];
+            p.xj0 = xj[3 * s];
+            p.xj1 = xj[3 * s + 1];
+            p.xj2 = xj[3 * s + 2];
+            p.valid = codes[s] >= 0;
+            p.sq = __int_as_float(sqb[s]);
+            point_body<M, float>(p, T, P, acc);
+#if M3S_ACC_SCHED_BARRIER
+            __builtin_amdgcn_sched_barrier(0);  // one point's temporaries live at a time
+#endif
+        }
+    }
+};
+
+// Reads the reference's tensors directly every iteration (used when the call runs < 3
+// iterations, or the inputs are not 16-B aligned).  1-D grid over (edge, chunk) tasks in the
+// driver's XCD-aware order; 256 threads; VEC: 4 consecutive points per lane per step as two
+// packed pairs (16-B loads of idx/Q/Xj/Cj, 4-B valid).
+template <int MODE, bool VEC>
+__global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
+    const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
+    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int64_t* __restrict__ idx,
+    const uint8_t* __restrict__ valid, const float* __restrict__ Q, AccParams P,
+    const int* __restrict__ sched, float* __restrict__ partials, const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int task = sched[blockIdx.x];
+    const int e = task / P.nchunks;
+    const int c = task - e * P.nchunks;
+    const int ix = ii_loc[e], jx = jj_loc[e];
+    const Sim3f T = rel_sim3(load_sim3(Twc + (int64_t)ix * 8), load_sim3(Twc + (int64_t)jx * 8));
+
+    const int HW = P.HW;
+    const int64_t ebase = (int64_t)e * HW;
+    const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
+    const float* __restrict__ Ci_b = Cs + (int64_t)ix * HW;
+    const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
+    const float* __restrict__ Cj_b = Cs + (int64_t)jx * HW;
+    const int k0 = c * P.chunk;
+    const int k1 = min(k0 + P.chunk, HW);
+    const int tid = threadIdx.x;
+    float accs[kNacc];
+
+    if constexpr (VEC) {
+        // the same stage arithmetic as the packed kernel, from the reference's tensors: the
+        // two paths produce bitwise identical partials
+#pragma unroll
+        for (int q = 0; q < kNacc; q++) accs[q] = 0.0f;
+        for (int k = k0 + 4 * tid; k < k1; k += 4 * kAccThreads) {
+            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + ebase + k);
+            const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + ebase + k);
+            const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + ebase + k + 2);
+            const float4 q4 = *reinterpret_cast<const float4*>(Q + ebase + k);
+            const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
+            const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
+            const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
+            const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
+            const float cjs[4] = {cj4.x, cj4.y, cj4.z, cj4.w};
+            int code[4], sqb[4];
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int ind = match_index(ids[s], vm[s], HW);
+                const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) &&
+                                (cjs[s] > P.C_thresh);
+                code[s] = ok ? ind : (int)((unsigned)ind | 0x80000000u);
+                sqb[s] = __float_as_int(vsqrt(qs[s]));
+            }
+            AccStage<MODE> st;
+            st.ka = int4{code[0], sqb[0], code[1], sqb[1]};
+            st.kb = int4{code[2], sqb[2], code[3], sqb[3]};
+            st.template load<MODE>(Xj_b, Xi_b, nullptr, k);  // calib: the depth from Xs
+            st.template compute<MODE>(T, P, accs);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kNacc; q++) accs[q] = 0.0f;
+        for (int k = k0 + tid; k < k1; k += kAccThreads) {
+            PointsIn<float> p;
+            const bool vm = valid[ebase + k] != 0;
+            const int ind = match_index(idx[ebase + k], vm, HW);
+            const float q = Q[ebase + k];
+            p.xj0 = Xj_b[(int64_t)k * 3 + 0];
+            p.xj1 = Xj_b[(int64_t)k * 3 + 1];
+            p.xj2 = Xj_b[(int64_t)k * 3 + 2];
+            p.xi0 = Xi_b[(int64_t)ind * 3 + 0];
+            p.xi1 = Xi_b[(int64_t)ind * 3 + 1];
+            p.xi2 = Xi_b[(int64_t)ind * 3 + 2];
+            p.valid = vm && (q > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (Cj_b[k] > P.C_thresh);
+            p.sq = vsqrt(q);
+            if constexpr (MODE == GN_CALIB) pixel_of(ind, P, p.ut, p.vt);
+            point_body<MODE, float>(p, T, P, accs);
+        }
+    }
+    block_partial(accs, partials + ((int64_t)e * P.nchunks + c) * kNaccPad);
+}
+
+// ---------------------------------------------------------------------------
+// Iteration-invariant packing (once per GN call, >= 3 iterations): per directed point-edge
+// {code, sqrt(q)} with code = match index | (invalid << 31), where "valid" folds the
+// reference's pose-independent tests (match, q > Q_thresh, ci > C_thresh, cj > C_thresh;
+// gn_kernels.cu:953-957).  Every iteration then streams 8 B per point-edge instead of
+// idx 8 + valid 1 + Q 4 + Cj 4 + gathered Ci 4 = 21 B, and the point math is unchanged
+// (invalid points are still evaluated with weight 0, so NaN poisoning is kept).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
+    const float* __restrict__ Cs, const int* __restrict__ ii_loc, const int* __restrict__ jj_loc,
+    const int64_t* __restrict__ idx, const uint8_t* __restrict__ valid, const float* __restrict__ Q,
+    AccParams P, int4* __restrict__ pack, const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int e = blockIdx.y;
+    const int HW = P.HW;
+    const int64_t ebase = (int64_t)e * HW;
+    const float* __restrict__ Ci_b = Cs + (int64_t)ii_loc[e] * HW;
+    const float* __restrict__ Cj_b = Cs + (int64_t)jj_loc[e] * HW;
+    const int k = 4 * (blockIdx.x * kAccThreads + threadIdx.x);
+    if (k >= HW) return;
+    const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + ebase + k);
+    const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + ebase + k);
+    const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + ebase + k + 2);
+    const float4 q4 = *reinterpret_cast<const float4*>(Q + ebase + k);
+    const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
+    const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
+    const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
+    const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
+    const float cjs[4] = {cj4.x, cj4.y, cj4.z, cj4.w};
+    int code[4], sqb[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const int ind = match_index(ids[s], vm[s], HW);
+        const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (cjs[s] > P.C_thresh);
+        code[s] = ok ? ind : (int)((unsigned)ind | 0x80000000u);
+        sqb[s] = __float_as_int(vsqrt(qs[s]));
+    }
+    int4* dst = pack + (ebase + k) / 2;
+    dst[0] = int4{code[0], sqb[0], code[1], sqb[1]};
+    dst[1] = int4{code[2], sqb[2], code[3], sqb[3]};
+}
+
+// Zs[n, k] = Xs[n, k, 2]: the only coordinate of the matched point calib mode reads, as a
+// dense 4-B array so the per-iteration gather touches 4 B per point instead of a 12-B stride.
+__global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__ Xs, int64_t total,
+                                                       float* __restrict__ Zs) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256)
+        Zs[i] = Xs[i * 3 + 2];
+}
+
+// Per-iteration accumulate over the packed stream: 8 B {code, sqrt q} + Xj 12 B + the gather
+// of the matched point (calib: its depth from Zs; rays/points: Xi) per point-edge.
+#ifndef M3S_ACC_SCHED_BARRIER
+#define M3S_ACC_SCHED_BARRIER 1
+#endif
+
+#ifndef M3S_ACC_PIPE
+#define M3S_ACC_PIPE 1
+#endif
+#ifndef M3S_ACC_WAVES
+#define M3S_ACC_WAVES 1
+#endif
+template <int MODE>
+__global__ __launch_bounds__(kAccThreads) __attribute__((amdgpu_waves_per_eu(M3S_ACC_WAVES)))
+void gn_accum_packed_kernel(
+    const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Zs,
+    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int4* __restrict__ pack,
+    AccParams P, const int* __restrict__ sched, float* __restrict__ partials,
+    const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int task = sched[blockIdx.x];
+    const int e = task / P.nchunks;
+    const int c = task - e * P.nchunks;
+    const int ix = ii_loc[e], jx = jj_loc[e];
+    const Sim3f T = rel_sim3(load_sim3(Twc + (int64_t)ix * 8), load_sim3(Twc + (int64_t)jx * 8));
+
+    const int HW = P.HW;
+    const int64_t ebase = (int64_t)e * HW;
+    const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
+    const float* __restrict__ Zi_b = Zs + (int64_t)ix * HW;
+    const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
+    const int4* __restrict__ pk_b = pack + ebase / 2;
+    const int k0 = c * P.chunk;
+    const int k1 = min(k0 + P.chunk, HW);
+    const int tid = threadIdx.x;
+
+    float acc[kNacc];
+#pragma unroll
+    for (int q = 0; q < kNacc; q++) acc[q] = 0.0f;
+    // Steps of 4 points per lane; the packed records of the next step are loaded one step
+    // ahead, so a step waits for one memory round trip (its gathers + Xj) instead of two
+    // (records, then the gathers they index).  A deeper pipeline (gathers of the next step
+    // in flight too) needs ~180 VGPRs, drops to 2 waves/SIMD and measured 8 % slower.
+    constexpr int S = 4 * kAccThreads;
+#if M3S_ACC_PIPE == 2
+    // two-deep: the gathers + Xj of step s+1 and the records of step s+2 are in flight while
+    // step s is computed
+    AccStage<MODE> cur, nxt;
+    int4 pa2 = int4{0, 0, 0, 0}, pb2 = int4{0, 0, 0, 0};
+    int k = k0 + 4 * tid;
+    if (k < k1) {
+        cur.ka = pk_b[k / 2];
+        cur.kb = pk_b[k / 2 + 1];
+        cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
+    }
+    if (k + S < k1) {
+        nxt.ka = pk_b[(k + S) / 2];
+        nxt.kb = pk_b[(k + S) / 2 + 1];
+    }
+    for (; k < k1; k += S) {
+        if (k + S < k1) nxt.template load<MODE>(Xj_b, Xi_b, Zi_b, k + S);
+        if (k + 2 * S < k1) {
+            pa2 = pk_b[(k + 2 * S) / 2];
+            pb2 = pk_b[(k + 2 * S) / 2 + 1];
+        }
+        cur.template compute<MODE>(T, P, acc);
+        cur = nxt;
+        nxt.ka = pa2;
+        nxt.kb = pb2;
+    }
+#else
+    AccStage<MODE> cur;
+    int4 na = int4{0, 0, 0, 0}, nb = int4{0, 0, 0, 0};
+    int k = k0 + 4 * tid;
+    if (k < k1) {
+        na = pk_b[k / 2];
+        nb = pk_b[k / 2 + 1];
+    }
+    for (; k < k1; k += S) {
+        cur.ka = na;
+        cur.kb = nb;
+        if (k + S < k1) {
+            na = pk_b[(k + S) / 2];
+            nb = pk_b[(k + S) / 2 + 1];
+        }
+        cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
+        cur.template compute<MODE>(T, P, acc);
+    }
+#endif
+    block_partial(acc, partials + ((int64_t)e * P.nchunks + c) * kNaccPad);
+}
+
+hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
+                        const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
+                        const int64_t* idx, const uint8_t* valid, const float* Q,
+                        const AccParams& P, const int* sched, float* partials, const int* flags) {
+#define M3S_ACC(MODE, V)                                                                    \
+    hipLaunchKernelGGL((gn_accum_kernel<MODE, V>), grid, dim3(kAccThreads), 0, st, Twc, Xs, \
+                       Cs, ii_loc, jj_loc, idx, valid, Q, P, sched, partials, flags)
+    if (mode == GN_RAYS) {
+        if (vec) M3S_ACC(GN_RAYS, true); else M3S_ACC(GN_RAYS, false);
+    } else if (mode == GN_CALIB) {
+        if (vec) M3S_ACC(GN_CALIB, true); else M3S_ACC(GN_CALIB, false);
+    } else {
+        if (vec) M3S_ACC(GN_POINTS, true); else M3S_ACC(GN_POINTS, false);
+    }
+#undef M3S_ACC
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
+                       const int* ii_loc, const int* jj_loc, const int64_t* idx,
+                       const uint8_t* valid, const float* Q, const AccParams& P, int4* pack,
+                       float* Zs, const int* flags) {
+    if (E_local > 0) {
+        const dim3 grid((unsigned)((P.HW / 4 + kAccThreads - 1) / kAccThreads), (unsigned)E_local);
+        hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, idx,
+                           valid, Q, P, pack, flags);
+    }
+    if (Zs) {
+        const int64_t total = N * (int64_t)P.HW;
+        const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+        hipLaunchKernelGGL(gn_depth_kernel, dim3(blocks), dim3(256), 0, st, Xs, total, Zs);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
+                               const float* Xs, const float* Zs, const int* ii_loc,
+                               const int* jj_loc, const int4* pack, const AccParams& P,
+                               const int* sched, float* partials, const int* flags) {
+    if (mode == GN_RAYS)
+        hipLaunchKernelGGL(gn_accum_packed_kernel<GN_RAYS>, grid, dim3(kAccThreads), 0, st, Twc, Xs,
+                           Zs, ii_loc, jj_loc, pack, P, sched, partials, flags);
+    else if (mode == GN_CALIB)
+        hipLaunchKernelGGL(gn_accum_packed_kernel<GN_CALIB>, grid, dim3(kAccThreads), 0, st, Twc, Xs,
+                           Zs, ii_loc, jj_loc, pack, P, sched, partials, flags);
+    else
+        hipLaunchKernelGGL(gn_accum_packed_kernel<GN_POINTS>, grid, dim3(kAccThreads), 0, st, Twc, Xs,
+                           Zs, ii_loc, jj_loc, pack, P, sched, partials, flags);
+    return hipGetLastError();
+}
+
+}  // namespace m3s

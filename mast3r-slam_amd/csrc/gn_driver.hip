@@ -100,11 +100,11 @@ int chunk_points(int64_t HW, int nchunks) {
 
 struct Layout {
     size_t partials, edgeblk, compact, dense, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent,
-        grad_ptr, grad_ent, slotmap, linv, sched, total;
+        grad_ptr, grad_ent, slotmap, linv, sched, pack, zs, total;
     int nchunks, npad, nblk_max;
 };
 
-Layout make_layout(int64_t N, int64_t HW, int64_t E_total, int64_t E_local) {
+Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_local) {
     Layout L{};
     const int64_t npose = std::max<int64_t>(N - 1, 0);
     const int64_t n = 7 * npose;
@@ -132,6 +132,10 @@ Layout make_layout(int64_t N, int64_t HW, int64_t E_total, int64_t E_local) {
     L.slotmap = take(sizeof(int) * (size_t)npose * npose);
     L.linv = take(sizeof(double) * (size_t)L.npad * kCholTile);
     L.sched = take(sizeof(int) * (size_t)E_local * L.nchunks);
+    // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
+    // dense depth array of the keyframes (calib)
+    L.pack = take(8 * (size_t)E_local * (size_t)HW);
+    L.zs = take(mode == M3S_GN_CALIB ? sizeof(float) * (size_t)N * (size_t)HW : 0);
     L.total = off;
     return L;
 }
@@ -480,13 +484,14 @@ int validate(const m3s_gn_args& a) {
     M3S_REQUIRE(a.Twc && a.Xs && a.Cs && a.dx, "gauss_newton: null pointer");
     if (a.E_total > 0) M3S_REQUIRE(a.ii && a.jj, "gauss_newton: null ii/jj");
     if (a.E_local > 0) M3S_REQUIRE(a.idx && a.valid && a.Q, "gauss_newton: null edge data");
-    const size_t need = make_layout(a.N, a.HW, a.E_total, a.E_local).total;
+    const size_t need = make_layout(a.mode, a.N, a.HW, a.E_total, a.E_local).total;
     M3S_REQUIRE(a.ws != nullptr && a.ws_bytes >= need,
                 "gauss_newton: workspace too small (%zu < %zu bytes)", a.ws_bytes, need);
     return M3S_OK;
 }
 
 struct Ctx {
+    bool packed = false;  // per-call packed stream (gn_pack_kernel) feeds the accumulate
     Layout L;
     Plan plan;
     SparsePlan sp;
@@ -503,7 +508,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     if (rc) return rc;
     c.st = (hipStream_t)a.stream;
     c.ws = (char*)a.ws;
-    c.L = make_layout(a.N, a.HW, a.E_total, a.E_local);
+    c.L = make_layout(a.mode, a.N, a.HW, a.E_total, a.E_local);
     rc = build_plan(a, c.st, c.plan);
     if (rc) return rc;
     build_schedule(c.plan.ii_loc, c.plan.jj_loc, c.L.nchunks, c.plan.sched);
@@ -540,13 +545,33 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     P.z_eps = a.z_eps;
     P.width = a.width > 0 ? a.width : 1;
     P.height = a.height;
-    P.inv_width = 1.0f / (float)P.width;
+    {   // Granlund-Montgomery: l = ceil(log2 W), m = ceil(2^(31+l) / W) < 2^32
+        int l = 0;
+        while ((1LL << l) < P.width) l++;
+        const unsigned long long num = 1ULL << (31 + l);
+        P.div_m = (unsigned)((num + (unsigned long long)P.width - 1) / (unsigned long long)P.width);
+        P.div_sh = 31 + l;
+    }
     P.HW = (int)a.HW;
     P.chunk = chunk_points(a.HW, L.nchunks);
     P.nchunks = L.nchunks;
     auto al16 = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
     c.vec = (a.HW % 4 == 0) && al16(a.Xs) && al16(a.Cs) && al16(a.idx) && al16(a.valid) &&
             al16(a.Q);
+    // M3S_GN_PACK: 0 never, 1 (default) when the call runs >= 3 iterations, 2 always
+    const int pack_mode = env_int("M3S_GN_PACK", 1);
+    c.packed = c.vec && a.E_local > 0 && (pack_mode == 2 || (pack_mode == 1 && a.max_iter >= 3));
+    return M3S_OK;
+}
+
+// Once per call, before the iterations: the packed stream (and calib depth array).
+int prepare_iterations(const m3s_gn_args& a, Ctx& c) {
+    if (!c.packed) return M3S_OK;
+    const Layout& L = c.L;
+    M3S_HIP_CHECK(launch_pack(c.st, (int)a.E_local, a.Xs, a.N, a.Cs, c.at<int>(L.ii_loc),
+                              c.at<int>(L.jj_loc), a.idx, a.valid, a.Q, c.P, c.at<int4>(L.pack),
+                              a.mode == M3S_GN_CALIB ? c.at<float>(L.zs) : nullptr,
+                              c.at<int>(L.flags)));
     return M3S_OK;
 }
 
@@ -556,10 +581,17 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
     int* flags = c.at<int>(L.flags);
     if (a.E_local > 0) {
         g_prof.mark(c.st);
-        M3S_HIP_CHECK(launch_accum(a.mode, c.vec, dim3((unsigned)(L.nchunks * a.E_local)), c.st,
-                                   a.Twc, a.Xs, a.Cs, c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
-                                   a.idx, a.valid, a.Q, c.P, c.at<int>(L.sched),
-                                   c.at<float>(L.partials), flags));
+        const dim3 grid((unsigned)(L.nchunks * a.E_local));
+        if (c.packed)
+            M3S_HIP_CHECK(launch_accum_packed(a.mode, grid, c.st, a.Twc, a.Xs, c.at<float>(L.zs),
+                                              c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
+                                              c.at<int4>(L.pack), c.P, c.at<int>(L.sched),
+                                              c.at<float>(L.partials), flags));
+        else
+            M3S_HIP_CHECK(launch_accum(a.mode, c.vec, grid, c.st, a.Twc, a.Xs, a.Cs,
+                                       c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), a.idx, a.valid,
+                                       a.Q, c.P, c.at<int>(L.sched), c.at<float>(L.partials),
+                                       flags));
         g_prof.mark(c.st);
         M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
                                          a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
@@ -625,6 +657,8 @@ int run(const m3s_gn_args& a) {
         rc = upload_sparse_plan(c.sp, npose, c.st);
         if (rc) return rc;
     }
+    rc = prepare_iterations(a, c);
+    if (rc) return rc;
     for (int itr = 0; itr < a.max_iter; itr++) {
         g_prof.mark(c.st);
         rc = enqueue_system(a, c);
@@ -652,9 +686,8 @@ extern "C" const char* m3s_version(void) { return "m3s 0.1.0 gfx950"; }
 
 extern "C" size_t m3s_gn_workspace_bytes(int mode, int64_t N, int64_t HW, int64_t E_total,
                                          int64_t E_local) {
-    (void)mode;
     if (N < 1 || HW < 1 || E_total < 0 || E_local < 0) return 0;
-    return make_layout(N, HW, E_total, E_local).total;
+    return make_layout(mode, N, HW, E_total, E_local).total;
 }
 
 extern "C" int m3s_gauss_newton(const m3s_gn_args* args) {
@@ -677,6 +710,8 @@ extern "C" int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, doub
     const int npose = (int)(a.N - 1);
     const int n = 7 * npose;
     if (npose <= 0) return M3S_OK;
+    rc = prepare_iterations(a, c);
+    if (rc) return rc;
     rc = enqueue_system(a, c);
     if (rc) return rc;
     const Layout& L = c.L;

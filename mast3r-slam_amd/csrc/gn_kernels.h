@@ -19,13 +19,19 @@ constexpr int kFlagDone = 0;   // set once ||dx|| < delta_thresh (skips later it
 constexpr int kFlagFail = 1;   // set by the factorisation when a pivot <= 0
 constexpr int kNumFlags = 16;
 
+// Upper-triangle packing of a symmetric 7x7 block: index of (a,b), a <= b.
+__host__ __device__ constexpr int sym_idx(int a, int b) {
+    return a * 7 - a * (a - 1) / 2 + (b - a);
+}
+
 struct AccParams {
     float s0_inv, s1_inv;  // 1/sigma0, 1/sigma1
     float C_thresh, Q_thresh;
     float fx, fy, cx, cy;
     float pb_lo, pb_hi_u, pb_hi_v;  // calib border: (pb, W-1-pb, H-1-pb) as float
     float z_eps;
-    float inv_width;
+    unsigned div_m;  // ind / width == (ind * div_m) >> div_sh for 0 <= ind < 2^31
+    int div_sh;
     int width, height;
     int HW;
     int chunk;    // points per workgroup (multiple of 4)
@@ -36,6 +42,14 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
                         const int64_t* idx, const uint8_t* valid, const float* Q,
                         const AccParams& P, const int* sched, float* partials, const int* flags);
+hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
+                       const int* ii_loc, const int* jj_loc, const int64_t* idx,
+                       const uint8_t* valid, const float* Q, const AccParams& P, int4* pack,
+                       float* Zs, const int* flags);
+hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
+                               const float* Xs, const float* Zs, const int* ii_loc,
+                               const int* jj_loc, const int4* pack, const AccParams& P,
+                               const int* sched, float* partials, const int* flags);
 hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
                               const float* Twc, const int* ii_loc, double* edgeblk,
                               const int* flags);

@@ -1,10 +1,6 @@
 // gn_kernels.hip -- MI355X (gfx950) kernels of the Sim3 Gauss-Newton backend.
 //
-// Per GN iteration (driver in gn_driver.cpp):
-//   gn_accum_kernel<MODE>   stream idx/valid/Q + Xs/Cs, accumulate the 28 unique entries of
-//                           M = sum w r r^T and g = sum w e r over RAW (pre-adjoint) Jacobian
-//                           rows.  Replaces ray_align / calib_proj / point_align
-//                           (reference gn_kernels.cu:813-1138, 1231-1543, 455-723).
+// Per GN iteration (driver in gn_driver.hip), after the accumulate of gn_accum.hip:
 //   gn_edge_reduce_kernel   per directed edge: chunk partials summed in f64 (fixed order),
 //                           Hjj = A M A^T, vj = A g with A = the Sim3 adjoint map of
 //                           apply_Sim3_adj_inv (gn_kernels.cu:277-297).  Because
@@ -18,6 +14,7 @@
 //   gn_retract_kernel       dx = -x, left retraction (gn_kernels.cu:415-453), ||dx|| test.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "gn_kernels.h"
@@ -28,278 +25,6 @@ namespace m3s {
 // ---------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------
-
-// Upper-triangle packing of a symmetric 7x7 block: index of (a,b), a <= b.
-__host__ __device__ constexpr int sym_idx(int a, int b) {
-    return a * 7 - a * (a - 1) / 2 + (b - a);
-}
-
-__device__ __forceinline__ float huber_w(float r) {
-    // gn_kernels.cu:172-175 (the 1.345 compare is exact in float)
-    const float r_abs = fabsf(r);
-    return r_abs < 1.345f ? 1.0f : 1.345f * __builtin_amdgcn_rcpf(r_abs);
-}
-
-// Accumulate one raw Jacobian row r (compile-time nonzero mask) with weight w, residual e.
-template <int MASK>
-__device__ __forceinline__ void acc_row(float* __restrict__ acc, const float* r, float w, float e) {
-    float wr[7];
-#pragma unroll
-    for (int a = 0; a < 7; a++) wr[a] = (MASK >> a & 1) ? w * r[a] : 0.0f;
-#pragma unroll
-    for (int a = 0; a < 7; a++) {
-        if (!(MASK >> a & 1)) continue;
-#pragma unroll
-        for (int b = a; b < 7; b++) {
-            if (!(MASK >> b & 1)) continue;
-            acc[sym_idx(a, b)] = fmaf(wr[a], r[b], acc[sym_idx(a, b)]);
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < 7; a++)
-        if (MASK >> a & 1) acc[28 + a] = fmaf(wr[a], e, acc[28 + a]);
-}
-
-struct PointIn {
-    float xi0, xi1, xi2, xj0, xj1, xj2, ci, cj, q;
-    int vm;
-    int ind;
-};
-
-// One point-edge: residuals, robust weights, raw rows.  tij/qij/sij = T_i^{-1} T_j.
-template <int MODE>
-__device__ __forceinline__ void point_body(const PointIn& p, const Sim3f& Tij, const AccParams& P,
-                                           float* __restrict__ acc) {
-    const float Xj[3] = {p.xj0, p.xj1, p.xj2};
-    float Y[3];
-    act_so3(Tij.q, Xj, Y);
-    const float X0 = Y[0] * Tij.s + Tij.t[0];
-    const float X1 = Y[1] * Tij.s + Tij.t[1];
-    const float X2 = Y[2] * Tij.s + Tij.t[2];
-    bool valid = p.vm && (p.q > P.Q_thresh) && (p.ci > P.C_thresh) && (p.cj > P.C_thresh);
-
-    if constexpr (MODE == GN_RAYS) {
-        // gn_kernels.cu:924-1089
-        const float n2i = (p.xi0 * p.xi0 + p.xi1 * p.xi1) + p.xi2 * p.xi2;
-        const float n1i = sqrtf(n2i);
-        const float n1i_inv = __builtin_amdgcn_rcpf(n1i);
-        const float n2j = (X0 * X0 + X1 * X1) + X2 * X2;
-        const float n1j = sqrtf(n2j);
-        const float n1j_inv = __builtin_amdgcn_rcpf(n1j);
-        const float rx = n1j_inv * X0, ry = n1j_inv * X1, rz = n1j_inv * X2;
-        const float e0 = rx - n1i_inv * p.xi0;
-        const float e1 = ry - n1i_inv * p.xi1;
-        const float e2 = rz - n1i_inv * p.xi2;
-        const float e3 = n1j - n1i;
-        const float sq = sqrtf(p.q);
-        const float swr = valid ? P.s0_inv * sq : 0.0f;
-        const float swd = valid ? P.s1_inv * sq : 0.0f;
-        const float wcr = swr * swr, wcd = swd * swd;
-        const float w0 = huber_w(swr * e0) * wcr;
-        const float w1 = huber_w(swr * e1) * wcr;
-        const float w2 = huber_w(swr * e2) * wcr;
-        const float w3 = huber_w(swd * e3) * wcd;
-        const float n3 = n1j_inv * __builtin_amdgcn_rcpf(n2j);
-        const float dxx = n1j_inv - X0 * X0 * n3;
-        const float dyy = n1j_inv - X1 * X1 * n3;
-        const float dzz = n1j_inv - X2 * X2 * n3;
-        const float dxy = -X0 * X1 * n3;
-        const float dxz = -X0 * X2 * n3;
-        const float dyz = -X1 * X2 * n3;
-        {
-            const float r[7] = {dxx, dxy, dxz, 0.f, rz, -ry, 0.f};
-            acc_row<0b0110111>(acc, r, w0, e0);
-        }
-        {
-            const float r[7] = {dxy, dyy, dyz, -rz, 0.f, rx, 0.f};
-            acc_row<0b0101111>(acc, r, w1, e1);
-        }
-        {
-            const float r[7] = {dxz, dyz, dzz, ry, -rx, 0.f, 0.f};
-            acc_row<0b0011111>(acc, r, w2, e2);
-        }
-        {
-            const float r[7] = {rx, ry, rz, 0.f, 0.f, 0.f, n1j};
-            acc_row<0b1000111>(acc, r, w3, e3);
-        }
-    } else if constexpr (MODE == GN_CALIB) {
-        // gn_kernels.cu:1360-1495
-        int vt = (int)((float)p.ind * P.inv_width);
-        int ut = p.ind - vt * P.width;
-        while (ut < 0) { vt--; ut += P.width; }
-        while (ut >= P.width) { vt++; ut -= P.width; }
-        const bool valid_z = (X2 > P.z_eps) && (p.xi2 > P.z_eps);
-        const float zj_inv = valid_z ? __builtin_amdgcn_rcpf(X2) : 0.0f;
-        const float zj_log = valid_z ? __logf(X2) : 0.0f;
-        const float zi_log = valid_z ? __logf(p.xi2) : 0.0f;
-        const float x = X0 * zj_inv, y = X1 * zj_inv;
-        const float u = P.fx * x + P.cx;
-        const float v = P.fy * y + P.cy;
-        const bool valid_u = (u > P.pb_lo) && (u < P.pb_hi_u);
-        const bool valid_v = (v > P.pb_lo) && (v < P.pb_hi_v);
-        valid = valid && valid_u && valid_v && valid_z;
-        const float e0 = u - (float)ut;
-        const float e1 = v - (float)vt;
-        const float e2 = zj_log - zi_log;
-        const float sq = sqrtf(p.q);
-        const float swp = valid ? P.s0_inv * sq : 0.0f;
-        const float swd = valid ? P.s1_inv * sq : 0.0f;
-        const float wcp = swp * swp, wcd = swd * swd;
-        const float w0 = huber_w(swp * e0) * wcp;
-        const float w1 = huber_w(swp * e1) * wcp;
-        const float w2 = huber_w(swd * e2) * wcd;
-        {
-            const float r[7] = {P.fx * zj_inv, 0.f, -P.fx * x * zj_inv, -P.fx * x * y,
-                                P.fx * (1.0f + x * x), -P.fx * y, 0.f};
-            acc_row<0b0111101>(acc, r, w0, e0);
-        }
-        {
-            const float r[7] = {0.f, P.fy * zj_inv, -P.fy * y * zj_inv, -P.fy * (1.0f + y * y),
-                                P.fy * x * y, P.fy * x, 0.f};
-            acc_row<0b0111110>(acc, r, w1, e1);
-        }
-        {
-            const float r[7] = {0.f, 0.f, zj_inv, y, -x, 0.f, 1.0f};
-            acc_row<0b1011100>(acc, r, w2, e2);
-        }
-    } else {
-        // point_align_kernel, gn_kernels.cu:564-674
-        const float e0 = X0 - p.xi0, e1 = X1 - p.xi1, e2 = X2 - p.xi2;
-        const float swp = valid ? P.s0_inv * sqrtf(p.q) : 0.0f;
-        const float wc = swp * swp;
-        const float w0 = huber_w(swp * e0) * wc;
-        const float w1 = huber_w(swp * e1) * wc;
-        const float w2 = huber_w(swp * e2) * wc;
-        {
-            const float r[7] = {1.f, 0.f, 0.f, 0.f, X2, -X1, X0};
-            acc_row<0b1110001>(acc, r, w0, e0);
-        }
-        {
-            const float r[7] = {0.f, 1.f, 0.f, -X2, 0.f, X0, X1};
-            acc_row<0b1101010>(acc, r, w1, e1);
-        }
-        {
-            const float r[7] = {0.f, 0.f, 1.f, X1, -X0, 0.f, X2};
-            acc_row<0b1011100>(acc, r, w2, e2);
-        }
-    }
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-// Grid: x = point chunk, y = local directed edge.  256 threads, 4 points per lane per step
-// (VEC: 16-B loads of idx/Q/Xj/Cj/valid), fp32 register accumulators, wave + LDS tree,
-// one 36-float partial per workgroup.
-template <int MODE, bool VEC>
-__global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
-    const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
-    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int64_t* __restrict__ idx,
-    const uint8_t* __restrict__ valid, const float* __restrict__ Q, AccParams P,
-    const int* __restrict__ sched, float* __restrict__ partials, const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
-    // XCD-aware task order (built by the driver): block b -> (edge, chunk)
-    const int task = sched[blockIdx.x];
-    const int e = task / P.nchunks;
-    const int c = task - e * P.nchunks;
-    const int ix = ii_loc[e], jx = jj_loc[e];
-    const Sim3f Ti = load_sim3(Twc + (int64_t)ix * 8);
-    const Sim3f Tj = load_sim3(Twc + (int64_t)jx * 8);
-    const Sim3f Tij = rel_sim3(Ti, Tj);
-
-    float acc[kNacc];
-#pragma unroll
-    for (int q = 0; q < kNacc; q++) acc[q] = 0.0f;
-
-    const int HW = P.HW;
-    const int64_t ebase = (int64_t)e * HW;
-    const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
-    const float* __restrict__ Ci_b = Cs + (int64_t)ix * HW;
-    const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
-    const float* __restrict__ Cj_b = Cs + (int64_t)jx * HW;
-    const int k0 = c * P.chunk;
-    const int k1 = min(k0 + P.chunk, HW);
-    const int tid = threadIdx.x;
-
-    if constexpr (VEC) {
-        for (int k = k0 + 4 * tid; k < k1; k += 4 * kAccThreads) {
-            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + ebase + k);
-            const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + ebase + k);
-            const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + ebase + k + 2);
-            const float4 q4 = *reinterpret_cast<const float4*>(Q + ebase + k);
-            const float4 xa = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
-            const float4 xb = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
-            const float4 xc = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
-            const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
-            const int vms[4] = {vm4.x, vm4.y, vm4.z, vm4.w};
-            const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
-            const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
-            const float xj[12] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w,
-                                  xc.x, xc.y, xc.z, xc.w};
-            const float cjs[4] = {cj4.x, cj4.y, cj4.z, cj4.w};
-            PointIn pin[4];
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                int64_t ind = vms[s] ? ids[s] : 0;
-                ind = ind < 0 ? 0 : (ind >= HW ? HW - 1 : ind);  // OOB guard
-                pin[s].ind = (int)ind;
-                pin[s].vm = vms[s] != 0;
-                pin[s].q = qs[s];
-                pin[s].xj0 = xj[3 * s];
-                pin[s].xj1 = xj[3 * s + 1];
-                pin[s].xj2 = xj[3 * s + 2];
-                pin[s].cj = cjs[s];
-            }
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                const float* xi = Xi_b + (int64_t)pin[s].ind * 3;
-                pin[s].xi0 = xi[0];
-                pin[s].xi1 = xi[1];
-                pin[s].xi2 = xi[2];
-                pin[s].ci = Ci_b[pin[s].ind];
-            }
-#pragma unroll
-            for (int s = 0; s < 4; s++) point_body<MODE>(pin[s], Tij, P, acc);
-        }
-    } else {
-        for (int k = k0 + tid; k < k1; k += kAccThreads) {
-            PointIn p;
-            p.vm = valid[ebase + k] != 0;
-            int64_t ind = p.vm ? idx[ebase + k] : 0;
-            ind = ind < 0 ? 0 : (ind >= HW ? HW - 1 : ind);
-            p.ind = (int)ind;
-            p.q = Q[ebase + k];
-            p.xj0 = Xj_b[(int64_t)k * 3 + 0];
-            p.xj1 = Xj_b[(int64_t)k * 3 + 1];
-            p.xj2 = Xj_b[(int64_t)k * 3 + 2];
-            p.cj = Cj_b[k];
-            p.xi0 = Xi_b[ind * 3 + 0];
-            p.xi1 = Xi_b[ind * 3 + 1];
-            p.xi2 = Xi_b[ind * 3 + 2];
-            p.ci = Ci_b[ind];
-            point_body<MODE>(p, Tij, P, acc);
-        }
-    }
-
-    // deterministic block reduction: wave butterfly, then 4 waves in fixed order
-    __shared__ float red[kAccThreads / 64][kNacc];
-    const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int q = 0; q < kNacc; q++) {
-        const float s = wave_sum(acc[q]);
-        if (lane == 0) red[wave][q] = s;
-    }
-    __syncthreads();
-    if (tid < kNacc) {
-        float s = red[0][tid];
-#pragma unroll
-        for (int w = 1; w < kAccThreads / 64; w++) s += red[w][tid];
-        partials[((int64_t)e * P.nchunks + c) * kNaccPad + tid] = s;
-    }
-}
 
 // Per local edge: f64 chunk sum (fixed order), Hjj = A M A^T, vj = A g.
 __global__ __launch_bounds__(64) void gn_edge_reduce_kernel(const float* __restrict__ partials,
@@ -800,24 +525,6 @@ __global__ __launch_bounds__(256) void gn_retract_kernel(float* __restrict__ Twc
 // ---------------------------------------------------------------------------
 // launchers (host)
 // ---------------------------------------------------------------------------
-
-hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
-                        const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
-                        const int64_t* idx, const uint8_t* valid, const float* Q,
-                        const AccParams& P, const int* sched, float* partials, const int* flags) {
-#define M3S_ACC(MODE, V)                                                                    \
-    hipLaunchKernelGGL((gn_accum_kernel<MODE, V>), grid, dim3(kAccThreads), 0, st, Twc, Xs, \
-                       Cs, ii_loc, jj_loc, idx, valid, Q, P, sched, partials, flags)
-    if (mode == GN_RAYS) {
-        if (vec) M3S_ACC(GN_RAYS, true); else M3S_ACC(GN_RAYS, false);
-    } else if (mode == GN_CALIB) {
-        if (vec) M3S_ACC(GN_CALIB, true); else M3S_ACC(GN_CALIB, false);
-    } else {
-        if (vec) M3S_ACC(GN_POINTS, true); else M3S_ACC(GN_POINTS, false);
-    }
-#undef M3S_ACC
-    return hipGetLastError();
-}
 
 hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
                               const float* Twc, const int* ii_loc, double* edgeblk,

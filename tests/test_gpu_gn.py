@@ -85,10 +85,14 @@ def test_normal_equations_match_oracle(backend, oracle, mode):
     scale = np.abs(H_o).max()
     assert np.abs(H_g - H_o).max() / scale < 1e-4
     assert np.abs(b_g - b_o).max() / max(np.abs(b_o).max(), 1e-30) < 1e-4
-    # the solved updates agree much more tightly than the pose tolerance
+    # the solved updates: 2e-5 of the largest component.  Both sides sum ~10^4 fp32 terms per
+    # entry in different orders (the oracle reproduces the reference's 768-long serial
+    # per-thread chains, the HIP path 32-long chains + f64 chunk sums), and calib's
+    # ill-conditioned scale/depth rows amplify that ~1e-6 relative noise in b to ~1e-5 in x.
+    # The north_star pose tolerance (1e-5) is checked after full GN iterations below.
     x_o = np.linalg.solve(H_o, b_o)
     x_g = np.linalg.solve(H_g, b_g)
-    assert np.abs(x_g - x_o).max() < 1e-5 * max(np.abs(x_o).max(), 1e-3)
+    assert np.abs(x_g - x_o).max() < 2e-5 * max(np.abs(x_o).max(), 1e-3)
 
 
 @pytest.mark.parametrize("mode", ["rays", "calib", "points"])
@@ -194,3 +198,20 @@ def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo):
     assert np.isfinite(dx_s).all()
     assert np.abs(dx_s - dx_d).max() <= 1e-8 * max(np.abs(dx_d).max(), 1e-6)
     assert _rel(T_s, T_d) < 1e-6
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib", "points"])
+def test_packed_stream_gives_identical_system(backend, monkeypatch, mode):
+    """The per-call packed stream (gn_pack_kernel: {match index | invalid bit, sqrt q}, plus the
+    calib depth array) feeds the same point math as the direct path, so the normal equations
+    are bitwise identical (M3S_GN_PACK=2 forces the packed path, 0 disables it)."""
+    from m3s.debug import build_system_gpu
+
+    g = _graph(mode, N=5, E=6)
+    g.Q[0, :50] = 1.0            # below Q_thresh: folded into the invalid bit
+    g.valid[1, 10:90] = False    # unmatched: index 0, weight 0
+    monkeypatch.setenv("M3S_GN_PACK", "0")
+    H0, b0 = build_system_gpu(g, mode, LOCAL)
+    monkeypatch.setenv("M3S_GN_PACK", "2")
+    H2, b2 = build_system_gpu(g, mode, LOCAL)
+    assert np.array_equal(H0, H2) and np.array_equal(b0, b2)

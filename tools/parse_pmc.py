@@ -33,7 +33,8 @@ fill_kb = [v for k, v in cal_w.items() if "FillFunc" in k][0][0]
 k_write = (1 << 30) / (fill_kb * 1024.0)
 bf = load("bench", "FETCH_SIZE")
 bw = load("bench", "WRITE_SIZE")
-name = [k for k in bf if "gn_accum_kernel" in k][0]
+names = [k for k in bf if "gn_accum" in k]
+name = ([k for k in names if "packed" in k] or names)[0]
 fetch_kb = sum(bf[name]) / len(bf[name])
 write_kb = sum(bw[name]) / len(bw[name])
 read_b = fetch_kb * 1024 * k_fetch
@@ -42,6 +43,7 @@ res = {
     "config": cfg,
     "n_gpus": 1,
     "kernel": name,
+    "packed": "packed" in name,
     "launches": len(bf[name]),
     "FETCH_SIZE_KB_per_launch": fetch_kb,
     "WRITE_SIZE_KB_per_launch": write_kb,
