@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
@@ -72,6 +73,49 @@ namespace {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Pinned host staging for the per-call plan transfers (D2H of ii/jj/K, H2D of the plan
+// integers): one buffer per host thread, reused across calls.  The H2D copies of a call are
+// asynchronous; the next call waits for them (an event) before overwriting the buffer.
+struct Staging {
+    char* buf = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+    ~Staging() {
+        if (pending) (void)hipEventSynchronize(done);
+        if (done) (void)hipEventDestroy(done);
+        if (buf) (void)hipHostFree(buf);
+    }
+    // a buffer of >= bytes, free of in-flight copies
+    char* get(size_t bytes) {
+        if (pending) {
+            (void)hipEventSynchronize(done);
+            pending = false;
+        }
+        if (bytes > cap) {
+            if (buf) (void)hipHostFree(buf);
+            cap = align_up(std::max<size_t>(bytes, 1 << 16) * 2, 4096);
+            if (hipHostMalloc((void**)&buf, cap, hipHostMallocDefault) != hipSuccess) {
+                buf = nullptr;
+                cap = 0;
+            }
+        }
+        return buf;
+    }
+    hipError_t mark(hipStream_t st) {
+        if (!done) {
+            hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipEventRecord(done, st);
+        pending = e == hipSuccess;
+        return e;
+    }
+};
+thread_local Staging g_stage_in;   // D2H
+thread_local Staging g_stage_out;  // H2D: the sparse solver's plan
+thread_local Staging g_stage_ws;   // H2D: the workspace's plan (CSR lists, schedule)
+
 // Number of point chunks per directed edge: chunks of ~kChunkTarget points (the per-XCD
 // working set of a chunk-major schedule is ~16 keyframes x chunk x 16 B), and at least
 // ~4096 workgroups overall when the edge count is small.
@@ -129,9 +173,9 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.blk_ent = take(sizeof(int) * (size_t)E_local * 4);
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
-    L.slotmap = take(sizeof(int) * (size_t)npose * npose);
-    L.linv = take(sizeof(double) * (size_t)L.npad * kCholTile);
     L.sched = take(sizeof(int) * (size_t)E_local * L.nchunks);
+    L.slotmap = take(sizeof(int) * (size_t)npose * npose);  // dense solver / debug only
+    L.linv = take(sizeof(double) * (size_t)L.npad * kCholTile);
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
     L.pack = take(8 * (size_t)E_local * (size_t)HW);
@@ -197,29 +241,32 @@ void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_l
 
 int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     const int64_t E = a.E_total;
-    std::vector<int64_t> hii(E), hjj(E);
-    float Kh[9] = {0};
+    char* hb = g_stage_in.get(sizeof(int64_t) * 2 * (size_t)E + 64);
+    M3S_REQUIRE(hb != nullptr, "gauss_newton: pinned host allocation failed");
+    int64_t* hii = reinterpret_cast<int64_t*>(hb);
+    int64_t* hjj = hii + E;
+    float* Kh = reinterpret_cast<float*>(hjj + E);
     if (E > 0) {
-        M3S_HIP_CHECK(hipMemcpyAsync(hii.data(), a.ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
-        M3S_HIP_CHECK(hipMemcpyAsync(hjj.data(), a.jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
+        M3S_HIP_CHECK(hipMemcpyAsync(hii, a.ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
+        M3S_HIP_CHECK(hipMemcpyAsync(hjj, a.jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
     }
     if (a.mode == M3S_GN_CALIB)
         M3S_HIP_CHECK(hipMemcpyAsync(Kh, a.K, sizeof(float) * 9, hipMemcpyDeviceToHost, st));
     M3S_HIP_CHECK(hipStreamSynchronize(st));
-    plan.K[0] = Kh[0];  // fx = K[0][0]
-    plan.K[1] = Kh[4];  // fy = K[1][1]
-    plan.K[2] = Kh[2];  // cx = K[0][2]
-    plan.K[3] = Kh[5];  // cy = K[1][2]
+    if (a.mode == M3S_GN_CALIB) {
+        plan.K[0] = Kh[0];  // fx = K[0][0]
+        plan.K[1] = Kh[4];  // fy = K[1][1]
+        plan.K[2] = Kh[2];  // cx = K[0][2]
+        plan.K[3] = Kh[5];  // cy = K[1][2]
+    }
 
     // unique(cat(ii, jj)) sorted; searchsorted (gn_kernels.cu:161-170)
-    std::vector<int64_t> u;
-    u.reserve(2 * E);
-    u.insert(u.end(), hii.begin(), hii.end());
-    u.insert(u.end(), hjj.begin(), hjj.end());
+    std::vector<int64_t> u(hii, hii + E);
+    u.insert(u.end(), hjj, hjj + E);
     std::sort(u.begin(), u.end());
     u.erase(std::unique(u.begin(), u.end()), u.end());
     auto row_of = [&](int64_t id) {
-        return (int64_t)(std::lower_bound(u.begin(), u.end(), id) - u.begin());
+        return (int)(std::lower_bound(u.begin(), u.end(), id) - u.begin());
     };
     M3S_REQUIRE((int64_t)u.size() <= a.N,
                 "gauss_newton: %lld unique keyframe ids in ii/jj but only %lld poses in Twc/Xs",
@@ -228,61 +275,65 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     const int npose = (int)(a.N - 1);
     std::vector<int> iopt(E), jopt(E);
     for (int64_t e = 0; e < E; e++) {
-        iopt[e] = (int)row_of(hii[e]) - 1;  // pin = num_fix = 1
-        jopt[e] = (int)row_of(hjj[e]) - 1;
+        iopt[e] = row_of(hii[e]) - 1;  // pin = num_fix = 1
+        jopt[e] = row_of(hjj[e]) - 1;
     }
 
-    // block slots: diagonal blocks first (slot p <-> pose p+1), then unordered pairs in
-    // order of first appearance over ALL edges.
-    std::map<std::pair<int, int>, int> slot_of;
+    // block slots: diagonal blocks first (slot p <-> pose p), then unordered pairs in order of
+    // first appearance over ALL edges; slotmap is the dense (npose x npose) slot table
+    plan.slotmap.assign((size_t)std::max(npose, 0) * std::max(npose, 0), -1);
+    for (int q = 0; q < npose; q++) plan.slotmap[(size_t)q * npose + q] = q;
     plan.nblk = npose;
+    plan.pairs.clear();
     for (int64_t e = 0; e < E; e++) {
         const int i = iopt[e], j = jopt[e];
-        if (i >= 0 && j >= 0 && i != j) {
-            const auto key = std::make_pair(std::min(i, j), std::max(i, j));
-            if (!slot_of.count(key)) slot_of[key] = plan.nblk++;
+        if (i >= 0 && j >= 0 && i != j && plan.slotmap[(size_t)i * npose + j] < 0) {
+            plan.slotmap[(size_t)i * npose + j] = plan.slotmap[(size_t)j * npose + i] = plan.nblk++;
+            plan.pairs.push_back(std::make_pair(std::min(i, j), std::max(i, j)));
         }
     }
-    auto slot = [&](int r, int c) -> int {
-        if (r == c) return r;
-        return slot_of.at(std::make_pair(std::min(r, c), std::max(r, c)));
-    };
+    auto slot = [&](int r, int c) { return plan.slotmap[(size_t)r * npose + c]; };
 
-    // contributions of the LOCAL edges (update_lhs order: (ii,ii,+) (ii,jj,-) (jj,ii,-) (jj,jj,+))
-    std::vector<std::vector<int>> blk_lists(plan.nblk), grad_lists(std::max(npose, 0));
+    // contributions of the LOCAL edges as CSR lists (update_lhs order per edge:
+    // (ii,ii,+) (ii,jj,-) (jj,ii,-) (jj,jj,+)), built by counting sort
     plan.ii_loc.resize(a.E_local);
     plan.jj_loc.resize(a.E_local);
-    for (int64_t el = 0; el < a.E_local; el++) {
-        const int64_t e = a.edge_offset + el;
-        const int i = iopt[e], j = jopt[e];
-        plan.ii_loc[el] = i + 1;
-        plan.jj_loc[el] = j + 1;
-        const int rr[4] = {i, i, j, j}, cc[4] = {i, j, i, j}, neg[4] = {0, 1, 1, 0};
-        for (int b = 0; b < 4; b++) {
-            if (rr[b] >= 0 && cc[b] >= 0 && rr[b] <= cc[b])
-                blk_lists[slot(rr[b], cc[b])].push_back((int)(el << 1) | neg[b]);
+    plan.blk_ptr.assign(plan.nblk + 1, 0);
+    plan.grad_ptr.assign(std::max(npose, 0) + 1, 0);
+    for (int pass = 0; pass < 2; pass++) {
+        std::vector<int> bfill, gfill;
+        if (pass == 1) {
+            for (int k = 0; k < plan.nblk; k++) plan.blk_ptr[k + 1] += plan.blk_ptr[k];
+            for (int k = 0; k < npose; k++) plan.grad_ptr[k + 1] += plan.grad_ptr[k];
+            plan.blk_ent.assign(plan.blk_ptr[plan.nblk], 0);
+            plan.grad_ent.assign(plan.grad_ptr[npose], 0);
+            bfill.assign(plan.blk_ptr.begin(), plan.blk_ptr.end() - 1);
+            gfill.assign(plan.grad_ptr.begin(), plan.grad_ptr.end() - 1);
         }
-        if (i >= 0) grad_lists[i].push_back((int)(el << 1) | 1);  // vi = -vj
-        if (j >= 0) grad_lists[j].push_back((int)(el << 1));
-    }
-    plan.blk_ptr.assign(1, 0);
-    for (auto& l : blk_lists) {
-        plan.blk_ent.insert(plan.blk_ent.end(), l.begin(), l.end());
-        plan.blk_ptr.push_back((int)plan.blk_ent.size());
-    }
-    plan.grad_ptr.assign(1, 0);
-    for (auto& l : grad_lists) {
-        plan.grad_ent.insert(plan.grad_ent.end(), l.begin(), l.end());
-        plan.grad_ptr.push_back((int)plan.grad_ent.size());
-    }
-    plan.slotmap.assign((size_t)std::max(npose, 0) * std::max(npose, 0), -1);
-    for (int p = 0; p < npose; p++) plan.slotmap[(size_t)p * npose + p] = p;
-    plan.pairs.assign(plan.nblk - npose, std::make_pair(0, 0));
-    for (auto& kv : slot_of) {
-        const int r = kv.first.first, c = kv.first.second;
-        plan.slotmap[(size_t)r * npose + c] = kv.second;
-        plan.slotmap[(size_t)c * npose + r] = kv.second;
-        plan.pairs[kv.second - npose] = kv.first;
+        for (int64_t el = 0; el < a.E_local; el++) {
+            const int64_t e = a.edge_offset + el;
+            const int i = iopt[e], j = jopt[e];
+            if (pass == 0) {
+                plan.ii_loc[el] = i + 1;
+                plan.jj_loc[el] = j + 1;
+            }
+            const int rr[4] = {i, i, j, j}, cc[4] = {i, j, i, j}, neg[4] = {0, 1, 1, 0};
+            for (int b = 0; b < 4; b++) {
+                if (rr[b] >= 0 && cc[b] >= 0 && rr[b] <= cc[b]) {
+                    const int sl = slot(rr[b], cc[b]);
+                    if (pass == 0) plan.blk_ptr[sl + 1]++;
+                    else plan.blk_ent[bfill[sl]++] = (int)(el << 1) | neg[b];
+                }
+            }
+            if (i >= 0) {  // vi = -vj
+                if (pass == 0) plan.grad_ptr[i + 1]++;
+                else plan.grad_ent[gfill[i]++] = (int)(el << 1) | 1;
+            }
+            if (j >= 0) {
+                if (pass == 0) plan.grad_ptr[j + 1]++;
+                else plan.grad_ent[gfill[j]++] = (int)(el << 1);
+            }
+        }
     }
     return M3S_OK;
 }
@@ -293,19 +344,23 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
 // then a dense core.  Built once per GN call (the pose graph is fixed across iterations).
 // ---------------------------------------------------------------------------------
 struct SpRound {
-    int node_begin, nnodes, tbeg, nbt, rbeg, nrt;
+    int node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount;
 };
 
 struct SparsePlan {
     bool enabled = false;
-    int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0;
+    bool fused = false;       // the whole solve in one gn_solve launch (else multi-launch)
+    bool fused_tail = false;  // the dense tail fits the in-register factorisation of gn_solve
+    int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
     std::vector<SpRound> rounds;
     std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
     // device (one stream-ordered allocation per call)
     char* dbuf = nullptr;
-    size_t o_A = 0, o_b = 0, o_y = 0, o_L = 0, o_W = 0, o_xd = 0, o_int = 0;
+    // block-format system: b (npose x 7, padded to bpad doubles), then 49-f64 blocks
+    int bpad = 0;
+    size_t o_sys = 0, o_y = 0, o_L = 0, o_W = 0, o_xd = 0, o_Lg = 0, o_int = 0;
     size_t i_nodes = 0, i_fptr = 0, i_fronts = 0, i_tg = 0, i_tc = 0, i_rtg = 0, i_rc = 0,
-           i_tail = 0, i_tmap = 0;
+           i_tail = 0, i_tmap = 0, i_rounds = 0, nints = 0;
     template <typename T>
     T* dptr(size_t off) const { return reinterpret_cast<T*>(dbuf + off); }
     const int* iptr(size_t i) const { return reinterpret_cast<const int*>(dbuf + o_int) + i; }
@@ -316,103 +371,184 @@ int env_int(const char* name, int dflt) {
     return e ? atoi(e) : dflt;
 }
 
-void build_sparse_plan(const Plan& p, int npose, SparsePlan& sp) {
-    const int dcap = env_int("M3S_SPARSE_DCAP", 16);
-    const int rmin = env_int("M3S_SPARSE_RMIN", 2);
-    const int rmax = env_int("M3S_SPARSE_RMAX", 64);
-    std::vector<std::set<int>> adj(npose);
-    std::map<std::pair<int, int>, int> bid;
+// Elimination-round policy.  fused (gn_solve, one workgroup): rounds stop once the rest fits
+// the in-register tail unless a round still removes >= kmin poses; a round's W blocks / y are
+// staged in LDS (capped), RHS contributions name the pose's slot in the round.  multi
+// (gn_sparse.hip): low-degree independent sets until fewer than rmin poses qualify, the rest
+// goes to the tiled dense Cholesky; RHS contributions name the pose.
+struct RoundPolicy {
+    bool fused;
+    int dcap, rmin, rmax, tailcap, kmin;
+};
+RoundPolicy fused_policy() {
+    return {true, env_int("M3S_SPARSE_DCAP", 64), env_int("M3S_SPARSE_RMIN", 1),
+            env_int("M3S_SPARSE_RMAX", 64),
+            std::min(kTailPoseMax, env_int("M3S_SPARSE_TAILCAP", kTailPoseMax)),
+            env_int("M3S_SPARSE_KMIN", 4)};
+}
+RoundPolicy multi_policy() {
+    return {false, env_int("M3S_MULTI_DCAP", 16), env_int("M3S_MULTI_RMIN", 2),
+            env_int("M3S_MULTI_RMAX", 64), 0, 0};
+}
+
+void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparsePlan& sp) {
+    sp = SparsePlan();
+    const int dcap = pol.dcap, rmin = pol.rmin, rmax = pol.rmax, tailcap = pol.tailcap, kmin = pol.kmin;
+    // adjacency as bitsets (one row of nw 64-bit words per pose), degrees, dense block ids
+    const int nw = (npose + 63) / 64;
+    std::vector<uint64_t> adj((size_t)npose * nw, 0);
+    std::vector<int> deg(npose, 0);
+    auto has = [&](int x, int y) { return (adj[(size_t)x * nw + (y >> 6)] >> (y & 63)) & 1; };
+    auto link = [&](int x, int y) {
+        uint64_t& w = adj[(size_t)x * nw + (y >> 6)];
+        const uint64_t m = 1ull << (y & 63);
+        if (!(w & m)) {
+            w |= m;
+            deg[x]++;
+        }
+    };
+    auto unlink = [&](int x, int y) {
+        uint64_t& w = adj[(size_t)x * nw + (y >> 6)];
+        const uint64_t m = 1ull << (y & 63);
+        if (w & m) {
+            w &= ~m;
+            deg[x]--;
+        }
+    };
+    auto neighbours = [&](int x, std::vector<int>& out) {  // ascending
+        out.clear();
+        for (int k = 0; k < nw; k++)
+            for (uint64_t w = adj[(size_t)x * nw + k]; w; w &= w - 1) out.push_back(64 * k + __builtin_ctzll(w));
+    };
+    std::vector<int> bidm((size_t)npose * npose, -1);  // upper triangle (x < y) used
     for (size_t k = 0; k < p.pairs.size(); k++) {
         const int a = p.pairs[k].first, b = p.pairs[k].second;
-        adj[a].insert(b);
-        adj[b].insert(a);
-        bid[p.pairs[k]] = npose + (int)k;
+        link(a, b);
+        link(b, a);
+        bidm[(size_t)a * npose + b] = npose + (int)k;
     }
     sp.nblocks = p.nblk;
     auto block_of = [&](int x, int y) -> int {
         if (x == y) return x;
-        const auto key = std::make_pair(std::min(x, y), std::max(x, y));
-        auto it = bid.find(key);
-        if (it != bid.end()) return it->second;
-        bid[key] = sp.nblocks;
-        return sp.nblocks++;
+        int& id = bidm[(size_t)std::min(x, y) * npose + std::max(x, y)];
+        if (id < 0) id = sp.nblocks++;
+        return id;
     };
-    std::vector<char> alive(npose, 1);
+    std::vector<char> alive(npose, 1), blocked(npose, 0);
     int nalive = npose;
     sp.fptr.assign(1, 0);
+    std::vector<int> cand, chosen, nb;
+    std::vector<std::vector<int>> F;
+    struct TC { int r, s, q, wx, wy; };
+    struct RC { int r, q, w; };
+    std::vector<TC> tcs;
+    std::vector<RC> rcs;
     for (int round = 0; round < rmax && nalive > 0; round++) {
-        std::vector<int> cand;
+        // a remaining clique is the dense tail (eliminating it pose by pose gains nothing)
+        bool clique = true;
+        for (int v = 0; v < npose && clique; v++)
+            if (alive[v] && deg[v] != nalive - 1) clique = false;
+        if (clique && nalive > 1) break;
+        cand.clear();
         for (int v = 0; v < npose; v++)
-            if (alive[v] && (int)adj[v].size() <= dcap) cand.push_back(v);
-        std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) {
-            return adj[a].size() != adj[b].size() ? adj[a].size() < adj[b].size() : a < b;
-        });
-        std::vector<char> blocked(npose, 0);
-        std::vector<int> chosen;
+            if (alive[v] && deg[v] <= dcap) cand.push_back(v);
+        std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return deg[a] < deg[b]; });
+        std::fill(blocked.begin(), blocked.end(), 0);
+        chosen.clear();
         for (int v : cand) {
             if (blocked[v]) continue;
             chosen.push_back(v);
             blocked[v] = 1;
-            for (int r : adj[v]) blocked[r] = 1;
+            for (int k = 0; k < nw; k++)
+                for (uint64_t w = adj[(size_t)v * nw + k]; w; w &= w - 1) blocked[64 * k + __builtin_ctzll(w)] = 1;
+        }
+        // a round's W blocks and y vectors are staged in LDS: cap its poses (the rest stay
+        // for the next round; any subset of an independent set is independent)
+        if (pol.fused) {
+            size_t k = 0, wsum = 0;
+            while (k < chosen.size() && (int)k < kSolveRoundPoses &&
+                   (wsum + deg[chosen[k]]) * 49 <= (size_t)kSolveWStage) {
+                wsum += deg[chosen[k]];
+                k++;
+            }
+            chosen.resize(k);
         }
         if ((int)chosen.size() < rmin && (int)chosen.size() != nalive) break;
+        // once the rest fits the in-register dense tail, a round must eliminate enough poses
+        // to beat the per-pose cost of the tail steps
+        if (nalive <= tailcap && (int)chosen.size() < kmin) break;
         std::sort(chosen.begin(), chosen.end());
         SpRound R;
         R.node_begin = (int)sp.nodes.size();
         R.nnodes = (int)chosen.size();
-        std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> tgt;
-        std::map<int, std::vector<std::pair<int, int>>> rtgt;
-        std::vector<std::vector<int>> F(chosen.size());
+        R.wbeg = sp.nW;
+        F.resize(chosen.size());
+        tcs.clear();
+        rcs.clear();
         for (size_t q = 0; q < chosen.size(); q++) {
             const int v = chosen[q];
-            F[q].assign(adj[v].begin(), adj[v].end());
+            neighbours(v, F[q]);
             sp.nodes.push_back(v);
-            std::map<int, int> wof;
+            const int w0 = sp.nW;
             for (int r : F[q]) {
                 const int blk = block_of(r, v);
-                const int wid = sp.nW++;
-                sp.fronts.insert(sp.fronts.end(), {r, blk, r > v ? 1 : 0, wid});
-                wof[r] = wid;
+                sp.fronts.insert(sp.fronts.end(), {r, blk, r > v ? 1 : 0, sp.nW++});
             }
             sp.fptr.push_back((int)sp.fronts.size() / 4);
-            for (size_t i = 0; i < F[q].size(); i++)
-                for (size_t j = i; j < F[q].size(); j++) {
-                    const int r = F[q][i], s2 = F[q][j];  // r <= s2 (sorted)
-                    tgt[std::make_pair(r, s2)].push_back(std::make_pair(wof[r], wof[s2]));
-                }
-            for (int r : F[q]) rtgt[r].push_back(std::make_pair(wof[r], v));
+            for (size_t i = 0; i < F[q].size(); i++) {
+                for (size_t j = i; j < F[q].size(); j++)
+                    tcs.push_back({F[q][i], F[q][j], (int)q, w0 + (int)i, w0 + (int)j});
+                rcs.push_back({F[q][i], pol.fused ? (int)q : v, w0 + (int)i});
+            }
         }
+        // targets in (r, s) order, contributions in pose order (deterministic sums)
+        std::sort(tcs.begin(), tcs.end(), [](const TC& x, const TC& y) {
+            return x.r != y.r ? x.r < y.r : x.s != y.s ? x.s < y.s : x.q < y.q;
+        });
+        std::stable_sort(rcs.begin(), rcs.end(), [](const RC& x, const RC& y) { return x.r < y.r; });
         R.tbeg = (int)sp.tg.size() / 3;
-        for (auto& kv : tgt) {
-            const int blk = block_of(kv.first.first, kv.first.second);
+        for (size_t k = 0; k < tcs.size();) {
+            size_t e = k;
             const int c0 = (int)sp.tc.size() / 2;
-            for (auto& pr : kv.second) sp.tc.insert(sp.tc.end(), {pr.first, pr.second});
-            sp.tg.insert(sp.tg.end(), {blk, c0, (int)sp.tc.size() / 2});
+            while (e < tcs.size() && tcs[e].r == tcs[k].r && tcs[e].s == tcs[k].s) {
+                sp.tc.insert(sp.tc.end(), {tcs[e].wx, tcs[e].wy});
+                e++;
+            }
+            sp.tg.insert(sp.tg.end(), {block_of(tcs[k].r, tcs[k].s), c0, (int)sp.tc.size() / 2});
+            k = e;
         }
-        R.nbt = (int)tgt.size();
+        R.nbt = (int)sp.tg.size() / 3 - R.tbeg;
         R.rbeg = (int)sp.rtg.size() / 3;
-        for (auto& kv : rtgt) {
+        for (size_t k = 0; k < rcs.size();) {
+            size_t e = k;
             const int c0 = (int)sp.rc.size() / 2;
-            for (auto& pr : kv.second) sp.rc.insert(sp.rc.end(), {pr.first, pr.second});
-            sp.rtg.insert(sp.rtg.end(), {kv.first, c0, (int)sp.rc.size() / 2});
+            while (e < rcs.size() && rcs[e].r == rcs[k].r) {
+                sp.rc.insert(sp.rc.end(), {rcs[e].w, rcs[e].q});  // (W id, node slot | pose)
+                e++;
+            }
+            sp.rtg.insert(sp.rtg.end(), {rcs[k].r, c0, (int)sp.rc.size() / 2});
+            k = e;
         }
-        R.nrt = (int)rtgt.size();
+        R.nrt = (int)sp.rtg.size() / 3 - R.rbeg;
+        R.wcount = sp.nW - R.wbeg;
         sp.rounds.push_back(R);
         // eliminate: drop the poses, connect each front into a clique (fill)
         for (size_t q = 0; q < chosen.size(); q++) {
             const int v = chosen[q];
-            for (int r : F[q]) adj[r].erase(v);
+            for (int r : F[q]) unlink(r, v);
             for (int r : F[q])
                 for (int s2 : F[q])
-                    if (r != s2) adj[r].insert(s2);
-            adj[v].clear();
+                    if (r != s2) link(r, s2);
+            for (int r : F[q]) unlink(v, r);
             alive[v] = 0;
             nalive--;
         }
     }
+    (void)has;
     for (int v = 0; v < npose; v++)
         if (alive[v]) sp.tail.push_back(v);
     sp.ntail = (int)sp.tail.size();
+    sp.zero_blk = sp.nblocks++;  // an all-zero block (zeroed with the fill blocks)
     sp.npad_tail = sp.ntail > 0 ? (int)align_up((size_t)sp.ntail * 7, kCholTile) : 0;
     sp.tmap.assign((size_t)sp.ntail * sp.ntail, -1);
     for (int i = 0; i < sp.ntail; i++)
@@ -422,11 +558,13 @@ void build_sparse_plan(const Plan& p, int npose, SparsePlan& sp) {
             if (x == y) {
                 code = 2 * x;
             } else {
-                auto it = bid.find(std::make_pair(std::min(x, y), std::max(x, y)));
-                if (it != bid.end()) code = 2 * it->second + (x > y ? 1 : 0);
+                const int id = bidm[(size_t)std::min(x, y) * npose + std::max(x, y)];
+                if (id >= 0) code = 2 * id + (x > y ? 1 : 0);
             }
             sp.tmap[(size_t)i * sp.ntail + j] = code;
         }
+    sp.fused_tail = sp.ntail * 7 <= kTailMax;
+    sp.fused = pol.fused && sp.fused_tail;
     sp.enabled = true;
 }
 
@@ -437,33 +575,42 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         off = align_up(off + std::max<size_t>(bytes, 8), 256);
         return o;
     };
-    sp.o_A = take(sizeof(double) * 49 * (size_t)sp.nblocks);
-    sp.o_b = take(sizeof(double) * 7 * (size_t)npose);
+    sp.bpad = (int)align_up((size_t)npose * 7, 49);
+    sp.o_sys = take(sizeof(double) * ((size_t)sp.bpad + 49 * (size_t)sp.nblocks));
     sp.o_y = take(sizeof(double) * 7 * (size_t)npose);
-    sp.o_L = take(sizeof(double) * 49 * sp.nodes.size());
+    sp.o_L = take(sizeof(double) * std::max(kLStoreRec, 49) * sp.nodes.size());
     sp.o_W = take(sizeof(double) * 49 * (size_t)sp.nW);
     sp.o_xd = take(sizeof(double) * (size_t)std::max(sp.npad_tail, 1));
-    std::vector<int> ints;
-    auto put = [&](const std::vector<int>& v) {
-        size_t i = ints.size();
-        ints.insert(ints.end(), v.begin(), v.end());
-        return i;
-    };
-    sp.i_nodes = put(sp.nodes);
-    sp.i_fptr = put(sp.fptr);
-    sp.i_fronts = put(sp.fronts);
-    sp.i_tg = put(sp.tg);
-    sp.i_tc = put(sp.tc);
-    sp.i_rtg = put(sp.rtg);
-    sp.i_rc = put(sp.rc);
-    sp.i_tail = put(sp.tail);
-    sp.i_tmap = put(sp.tmap);
-    sp.o_int = take(sizeof(int) * std::max<size_t>(ints.size(), 1));
+    sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
+    // the plan integers in one array: [nodes fptr fronts tg tc rtg rc tail tmap rounds]
+    std::vector<const std::vector<int>*> parts = {&sp.nodes, &sp.fptr, &sp.fronts, &sp.tg, &sp.tc,
+                                                  &sp.rtg, &sp.rc, &sp.tail, &sp.tmap};
+    size_t* offs[] = {&sp.i_nodes, &sp.i_fptr, &sp.i_fronts, &sp.i_tg, &sp.i_tc,
+                      &sp.i_rtg, &sp.i_rc, &sp.i_tail, &sp.i_tmap};
+    size_t n = 0;
+    for (size_t k = 0; k < parts.size(); k++) {
+        *offs[k] = n;
+        n += parts[k]->size();
+    }
+    sp.i_rounds = n;
+    n += 8 * sp.rounds.size();
+    sp.nints = n;
+    sp.o_int = take(sizeof(int) * std::max<size_t>(n, 1));
     M3S_HIP_CHECK(hipMallocAsync((void**)&sp.dbuf, off, st));
-    if (!ints.empty())
-        M3S_HIP_CHECK(hipMemcpyAsync(sp.dbuf + sp.o_int, ints.data(), sizeof(int) * ints.size(),
-                                     hipMemcpyHostToDevice, st));
-    M3S_HIP_CHECK(hipStreamSynchronize(st));  // the host vector dies with this call
+    if (n > 0) {
+        int* h = reinterpret_cast<int*>(g_stage_out.get(sizeof(int) * n));
+        M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
+        for (size_t k = 0; k < parts.size(); k++)
+            if (!parts[k]->empty()) std::memcpy(h + *offs[k], parts[k]->data(), sizeof(int) * parts[k]->size());
+        int* hr = h + sp.i_rounds;
+        for (const SpRound& R : sp.rounds) {
+            const int v[8] = {R.node_begin, R.nnodes, R.tbeg, R.nbt, R.rbeg, R.nrt, R.wbeg, R.wcount};
+            std::memcpy(hr, v, sizeof(v));
+            hr += 8;
+        }
+        M3S_HIP_CHECK(hipMemcpyAsync(sp.dbuf + sp.o_int, h, sizeof(int) * n, hipMemcpyHostToDevice, st));
+        M3S_HIP_CHECK(g_stage_out.mark(st));  // no host sync: the staging buffer outlives the copy
+    }
     return M3S_OK;
 }
 
@@ -491,6 +638,7 @@ int validate(const m3s_gn_args& a) {
 }
 
 struct Ctx {
+    bool need_slotmap = false;  // dense solver / debug system: upload the slot table
     bool packed = false;  // per-call packed stream (gn_pack_kernel) feeds the accumulate
     Layout L;
     Plan plan;
@@ -509,26 +657,44 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     c.st = (hipStream_t)a.stream;
     c.ws = (char*)a.ws;
     c.L = make_layout(a.mode, a.N, a.HW, a.E_total, a.E_local);
+    static const bool prof_host = env_int("M3S_PROF_HOST", 0) != 0;
+    const auto s0 = std::chrono::steady_clock::now();
     rc = build_plan(a, c.st, c.plan);
     if (rc) return rc;
+    const auto s1 = std::chrono::steady_clock::now();
     build_schedule(c.plan.ii_loc, c.plan.jj_loc, c.L.nchunks, c.plan.sched);
+    if (prof_host)
+        fprintf(stderr, "gn host: build_plan %.0f us, schedule %.0f us\n",
+                std::chrono::duration<double, std::micro>(s1 - s0).count(),
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - s1).count());
     const Layout& L = c.L;
     const Plan& p = c.plan;
-    auto up = [&](size_t off, const std::vector<int>& v) -> hipError_t {
-        if (v.empty()) return hipSuccess;
-        return hipMemcpyAsync(c.ws + off, v.data(), sizeof(int) * v.size(), hipMemcpyHostToDevice, c.st);
-    };
-    M3S_HIP_CHECK(up(L.ii_loc, p.ii_loc));
-    M3S_HIP_CHECK(up(L.jj_loc, p.jj_loc));
-    M3S_HIP_CHECK(up(L.blk_ptr, p.blk_ptr));
-    M3S_HIP_CHECK(up(L.blk_ent, p.blk_ent));
-    M3S_HIP_CHECK(up(L.grad_ptr, p.grad_ptr));
-    M3S_HIP_CHECK(up(L.grad_ent, p.grad_ent));
-    M3S_HIP_CHECK(up(L.slotmap, p.slotmap));
-    M3S_HIP_CHECK(up(L.sched, p.sched));
-    M3S_HIP_CHECK(hipMemsetAsync(c.ws + L.flags, 0, sizeof(int) * kNumFlags, c.st));
-    // the host vectors die with this call: wait for the (pageable) uploads
-    M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+    // the workspace's plan integers (flags .. sched, one contiguous span of the layout) as an
+    // image in pinned memory, one asynchronous copy
+    {
+        const size_t lo = L.flags, hi = L.sched + sizeof(int) * p.sched.size();
+        const size_t nslot = c.need_slotmap ? p.slotmap.size() : 0;
+        char* h = g_stage_ws.get(hi - lo + sizeof(int) * nslot);
+        M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
+        std::memset(h, 0, L.ii_loc - lo);  // flags
+        auto put = [&](size_t off, const std::vector<int>& v) {
+            if (!v.empty()) std::memcpy(h + (off - lo), v.data(), sizeof(int) * v.size());
+        };
+        put(L.ii_loc, p.ii_loc);
+        put(L.jj_loc, p.jj_loc);
+        put(L.blk_ptr, p.blk_ptr);
+        put(L.blk_ent, p.blk_ent);
+        put(L.grad_ptr, p.grad_ptr);
+        put(L.grad_ent, p.grad_ent);
+        put(L.sched, p.sched);
+        M3S_HIP_CHECK(hipMemcpyAsync(c.ws + lo, h, hi - lo, hipMemcpyHostToDevice, c.st));
+        if (nslot) {  // the dense (npose x npose) slot table
+            std::memcpy(h + (hi - lo), p.slotmap.data(), sizeof(int) * nslot);
+            M3S_HIP_CHECK(hipMemcpyAsync(c.ws + L.slotmap, h + (hi - lo), sizeof(int) * nslot,
+                                         hipMemcpyHostToDevice, c.st));
+        }
+        M3S_HIP_CHECK(g_stage_ws.mark(c.st));
+    }
 
     AccParams& P = c.P;
     P.s0_inv = 1.0f / a.sigma0;
@@ -597,6 +763,21 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
                                          a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
     }
     const int npose = (int)(a.N - 1);
+    if (c.sp.enabled && c.sp.fused) {
+        // block format for the single-workgroup solve, in the solver's buffer
+        SparsePlan& sp = c.sp;
+        double* sys = sp.dptr<double>(sp.o_sys);
+        M3S_HIP_CHECK(launch_assemble(c.st, c.at<double>(L.edgeblk), c.at<int>(L.blk_ptr),
+                                      c.at<int>(L.blk_ent), c.at<int>(L.grad_ptr),
+                                      c.at<int>(L.grad_ent), c.plan.nblk, sp.nblocks, npose, sp.bpad,
+                                      sys, flags));
+        if (a.comm) {
+            const size_t count = (size_t)sp.bpad + (size_t)c.plan.nblk * 49;
+            int rc = comm_allreduce_sum_f64(a.comm, sys, count, c.st);
+            if (rc) return rc;
+        }
+        return M3S_OK;
+    }
     M3S_HIP_CHECK(launch_compact(c.st, c.at<double>(L.edgeblk), c.at<int>(L.blk_ptr),
                                  c.at<int>(L.blk_ent), c.at<int>(L.grad_ptr),
                                  c.at<int>(L.grad_ent), c.plan.nblk, npose,
@@ -620,12 +801,69 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         return M3S_OK;
     }
     SparsePlan& sp = c.sp;
-    double* A = sp.dptr<double>(sp.o_A);
-    double* b = sp.dptr<double>(sp.o_b);
-    double* y = sp.dptr<double>(sp.o_y);
-    double* Ls = sp.dptr<double>(sp.o_L);
-    double* W = sp.dptr<double>(sp.o_W);
-    double* x = c.at<double>(L.x);
+    SolveArgs S;
+    S.npose = npose;
+    S.b = sp.dptr<double>(sp.o_sys);
+    S.A = S.b + sp.bpad;
+    S.y = sp.dptr<double>(sp.o_y);
+    S.Lstore = sp.dptr<double>(sp.o_L);
+    S.W = sp.dptr<double>(sp.o_W);
+    S.Lg = sp.dptr<double>(sp.o_Lg);
+    S.x = c.at<double>(L.x);
+    S.meta = sp.iptr(0);
+    S.nmeta = (int)sp.nints;
+    S.meta_lds = solve_lds_bytes(S.nmeta) <= (size_t)kSolveMaxLds && env_int("M3S_SOLVE_META_LDS", 1);
+    S.o_rounds = (int)sp.i_rounds;
+    S.o_nodes = (int)sp.i_nodes;
+    S.o_fptr = (int)sp.i_fptr;
+    S.o_fronts = (int)sp.i_fronts;
+    S.o_tg = (int)sp.i_tg;
+    S.o_tc = (int)sp.i_tc;
+    S.o_rtg = (int)sp.i_rtg;
+    S.o_rc = (int)sp.i_rc;
+    S.o_tail = (int)sp.i_tail;
+    S.o_tmap = (int)sp.i_tmap;
+    S.nrounds = (int)sp.rounds.size();
+    S.zero_blk = sp.zero_blk;
+    S.ntail = sp.ntail;
+    S.Twc = a.Twc;
+    S.dx = a.dx;
+    S.N = (int)a.N;
+    S.delta_thresh = a.delta_thresh;
+    S.flags = flags;
+    S.debug = env_int("M3S_SOLVE_DEBUG", 0);
+    if (S.debug) {
+        static int printed = 0;
+        if (printed++ == 0) {
+            fprintf(stderr, "solve plan: npose %d nblocks %d (real %d) nW %d ntail %d nints %zu meta_lds %d fused %d\n",
+                    npose, sp.nblocks, c.plan.nblk, sp.nW, sp.ntail, sp.nints, S.meta_lds, (int)sp.fused_tail);
+            for (const SpRound& R : sp.rounds) {
+                int ncontrib = 0, maxc = 0;
+                for (int t = 0; t < R.nbt; t++) {
+                    const int k = sp.tg[3 * (R.tbeg + t) + 2] - sp.tg[3 * (R.tbeg + t) + 1];
+                    ncontrib += k;
+                    maxc = std::max(maxc, k);
+                }
+                int nf = 0;
+                for (int q = R.node_begin; q < R.node_begin + R.nnodes; q++) nf += sp.fptr[q + 1] - sp.fptr[q];
+                fprintf(stderr, "  round: nodes %d fronts %d block targets %d (contrib %d, max %d) rhs targets %d\n",
+                        R.nnodes, nf, R.nbt, ncontrib, maxc, R.nrt);
+            }
+        }
+    }
+    if (sp.fused) {
+        // one launch: rounds, in-register dense tail, back-substitution, retraction
+        S.do_fwd = S.do_tail = S.do_back = 1;
+        M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+        return M3S_OK;
+    }
+    // multi-launch: one launch per round phase, the tail by the tiled dense Cholesky
+    double* A = S.A;
+    double* b = S.b;
+    double* y = S.y;
+    double* Ls = S.Lstore;
+    double* W = S.W;
+    double* x = S.x;
     M3S_HIP_CHECK(launch_sp_init(c.st, c.at<double>(L.compact), c.plan.nblk, sp.nblocks, npose, A, b,
                                  flags));
     for (const SpRound& R : sp.rounds) {
@@ -645,20 +883,42 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
 }
 
 int run(const m3s_gn_args& a) {
+    // M3S_PROF_HOST: host-side phase times of the call (stderr)
+    static const bool prof_host = env_int("M3S_PROF_HOST", 0) != 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto us = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+        return std::chrono::duration<double, std::micro>(y - x).count();
+    };
+    const auto t0 = now();
     Ctx c;
+    c.need_slotmap = env_int("M3S_SOLVER_DENSE", 0) != 0;
     int rc = setup(a, c);
     if (rc) return rc;
+    const auto t1 = now();
     const int npose = (int)(a.N - 1);
     if (npose <= 0) return M3S_OK;  // nothing to optimise (all poses pinned)
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
+    std::chrono::steady_clock::time_point t2 = t1, t3 = t1;
     if (env_int("M3S_SOLVER_DENSE", 0) == 0) {
-        build_sparse_plan(c.plan, npose, c.sp);
+        // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
+        // single-workgroup solve when its plan needs few rounds, else multi-launch
+        const int choice = env_int("M3S_SOLVER", 0);
+        build_sparse_plan(c.plan, npose, fused_policy(), c.sp);
+        const bool fused_ok = c.sp.fused && (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <=
+                                                                                 env_int("M3S_FUSED_MAX_ROUNDS", 3)));
+        if (!fused_ok) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
+        t2 = now();
         rc = upload_sparse_plan(c.sp, npose, c.st);
         if (rc) return rc;
+        t3 = now();
     }
     rc = prepare_iterations(a, c);
     if (rc) return rc;
+    const auto t4 = now();
+    if (prof_host)
+        fprintf(stderr, "gn host: setup %.0f us, sparse plan %.0f us, upload %.0f us, pack launch %.0f us\n",
+                us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4));
     for (int itr = 0; itr < a.max_iter; itr++) {
         g_prof.mark(c.st);
         rc = enqueue_system(a, c);
@@ -667,8 +927,9 @@ int run(const m3s_gn_args& a) {
         rc = enqueue_solve(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
-        M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
-                                     a.delta_thresh, flags));
+        if (!c.sp.fused)  // the single-workgroup solve retracts inside its launch
+            M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
+                                         a.delta_thresh, flags));
         g_prof.mark(c.st);
     }
     if (c.sp.dbuf) M3S_HIP_CHECK(hipFreeAsync(c.sp.dbuf, c.st));
@@ -705,6 +966,7 @@ extern "C" int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, doub
     }
     const m3s_gn_args& a = *args;
     Ctx c;
+    c.need_slotmap = true;
     int rc = setup(a, c);
     if (rc) return rc;
     const int npose = (int)(a.N - 1);

@@ -56,13 +56,16 @@ hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials
 hipError_t launch_compact(hipStream_t st, const double* edgeblk, const int* blk_ptr,
                           const int* blk_ent, const int* grad_ptr, const int* grad_ent, int nblk,
                           int npose, double* compact, const int* flags);
+hipError_t launch_assemble(hipStream_t st, const double* edgeblk, const int* blk_ptr,
+                           const int* blk_ent, const int* grad_ptr, const int* grad_ent, int nblk,
+                           int nblocks, int npose, int bpad, double* out, const int* flags);
 hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                         int npose, int n, int npad, double* Hd, double* Linv, double* x,
                         int* flags);
 constexpr int kMaxNpad = 8192;  // dense solve limit: N <= 1171 keyframes
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
                                      double* x, int* flags);
-// block-sparse elimination (gn_sparse.hip)
+// multi-launch block-sparse elimination (gn_sparse.hip)
 hipError_t launch_sp_init(hipStream_t st, const double* compact, int nblk, int nblocks, int npose,
                           double* A, double* b, const int* flags);
 hipError_t launch_sp_factor(hipStream_t st, int nnodes, const int* nodes, const int* fptr,
@@ -79,6 +82,33 @@ hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, cons
                           double* xd, double* x, int* flags);
 hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                             int npose, int n, int npad, double* Hd, const int* flags);
+// Fused single-workgroup solve (gn_solve.hip)
+constexpr int kSolveThreads = 256;
+constexpr int kTailMax = 192;      // in-register dense tail: <= 192 unknowns (12 x 16-wide tiles)
+constexpr int kTailPoseMax = 27;   // = kTailMax / 7
+constexpr int kLStoreRec = 40;     // per eliminated pose: packed lower L (28) + 1/diag (7) + pad
+constexpr int kSolveMaxLds = 160 * 1024 - 2048;  // dynamic LDS cap (static LDS besides)
+constexpr int kSolveWStage = 8192;    // doubles: a round's W blocks staged in LDS
+constexpr int kSolveRoundPoses = 256; // poses per round (their y vectors staged in LDS)
+struct SolveArgs {
+    double *A, *b;          // block-format system (gn_assemble_kernel), updated in place
+    double *y, *Lstore, *W, *Lg, *x;
+    // the host plan: one int array; offsets of its parts.  rounds: 8 ints each (node_begin,
+    // nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount); rc: (W id, node slot)
+    const int* meta;
+    int nmeta, meta_lds;  // meta_lds: stage it in LDS
+    int o_rounds, o_nodes, o_fptr, o_fronts, o_tg, o_tc, o_rtg, o_rc, o_tail, o_tmap;
+    int nrounds, ntail, npose, zero_blk;
+    float* Twc;
+    float* dx;
+    int N;
+    float delta_thresh;
+    int* flags;
+    int do_fwd, do_tail, do_back;  // rounds | in-kernel dense tail | back rounds + retract
+    int debug;                     // M3S_SOLVE_DEBUG: printf phase times (wall clock, thread 0)
+};
+size_t solve_lds_bytes(int nmeta_lds);
+hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
                           float delta_thresh, int* flags);
 

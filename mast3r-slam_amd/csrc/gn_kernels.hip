@@ -144,6 +144,52 @@ __global__ __launch_bounds__(64) void gn_compact_kernel(
     }
 }
 
+// Block-format system of the sparse solve (gn_solve.hip), written in place of the compact
+// one: out = [b (npose x 7, zero-padded to bpad)] [nblk real blocks, 49 f64 row-major (the
+// symmetric 7x7 expanded)] [nblocks - nblk fill blocks, zeroed].  The RCCL all-reduce covers
+// the first bpad + 49 nblk doubles.  One 64-lane workgroup per block / gradient row.
+__global__ __launch_bounds__(64) void gn_assemble_kernel(
+    const double* __restrict__ edgeblk, const int* __restrict__ blk_ptr,
+    const int* __restrict__ blk_ent, const int* __restrict__ grad_ptr,
+    const int* __restrict__ grad_ent, int nblk, int nblocks, int npose, int bpad,
+    double* __restrict__ out, const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (s < nblk) {
+        if (tid < 28) {
+            double acc = 0.0;
+            for (int k = blk_ptr[s]; k < blk_ptr[s + 1]; k++) {
+                const int code = blk_ent[k];
+                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + tid];
+                acc += (code & 1) ? -v : v;
+            }
+            int a = 0, r = tid;
+            while (r >= 7 - a) {
+                r -= 7 - a;
+                a++;
+            }
+            const int b = a + r;
+            double* blk = out + bpad + (int64_t)s * 49;
+            blk[a * 7 + b] = acc;
+            blk[b * 7 + a] = acc;
+        }
+    } else if (s < nblocks) {
+        if (tid < 49) out[bpad + (int64_t)s * 49 + tid] = 0.0;
+    } else {
+        const int p = s - nblocks;
+        if (p < npose && tid < 7) {
+            double acc = 0.0;
+            for (int k = grad_ptr[p]; k < grad_ptr[p + 1]; k++) {
+                const int code = grad_ent[k];
+                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + 28 + tid];
+                acc += (code & 1) ? -v : v;
+            }
+            out[p * 7 + tid] = acc;
+        }
+    }
+}
+
 // Dense f64 matrix [npad + T rows][npad cols]: system in rows < npad (identity on the
 // padding), RHS b in row npad (the bordered row: the forward solve rides along with the
 // factorisation).
@@ -539,6 +585,14 @@ hipError_t launch_compact(hipStream_t st, const double* edgeblk, const int* blk_
                           int npose, double* compact, const int* flags) {
     hipLaunchKernelGGL(gn_compact_kernel, dim3(nblk + npose), dim3(64), 0, st, edgeblk, blk_ptr,
                        blk_ent, grad_ptr, grad_ent, nblk, npose, compact, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble(hipStream_t st, const double* edgeblk, const int* blk_ptr,
+                           const int* blk_ent, const int* grad_ptr, const int* grad_ent, int nblk,
+                           int nblocks, int npose, int bpad, double* out, const int* flags) {
+    hipLaunchKernelGGL(gn_assemble_kernel, dim3(nblocks + npose), dim3(64), 0, st, edgeblk, blk_ptr,
+                       blk_ent, grad_ptr, grad_ent, nblk, nblocks, npose, bpad, out, flags);
     return hipGetLastError();
 }
 

@@ -1,0 +1,775 @@
+// gn_solve.hip -- the whole per-iteration solve + retraction in ONE workgroup (gfx950).
+//
+// Replaces SparseBlock::solve (Eigen SimplicialLLT, reference gn_kernels.cu:132-153), the
+// dx = -solve / pose_retr_kernel / ||dx|| test of the GN drivers (gn_kernels.cu:1209-1222,
+// 415-453).  A multi-launch design (one launch per elimination round / 64-tile step) is bound
+// by launch latency (~5 us per dependent launch); here ONE 256-thread workgroup (4 waves, one
+// per SIMD, 512 registers each) runs the block elimination end to end with __syncthreads()
+// between dependent steps (~0.1 us each).  Since one CU issues everything, the design keeps
+// dependent chains short: the host plan (integers) is staged into LDS once; every 7x7 factor
+// is computed serially in registers by each lane that needs it (no cross-lane traffic on the
+// pivot chain); global loads are issued unconditionally (invalid entries read an all-zero
+// block) so that independent loads overlap instead of waiting one by one.
+//
+// The system arrives in block format (gn_assemble_kernel): b, then 49-f64 row-major blocks
+// (block (x,y) holds the rows of pose x < y; fill blocks zeroed), and is updated in place.
+//
+//   rounds    per independent set of poses (host plan, gn_driver.hip): 7 lanes per pose (9
+//             poses per wave); every lane factors A_vv = L L^T (packed lower, rsq + one Newton
+//             step per pivot) and computes row `ra` of W_rv = A_rv L^-T for each front pose r
+//             (forward substitution) into LDS (and global, for the back-substitution); lane 0 of
+//             the group y_v = L^-1 b_v.  barrier.  Schur updates, one thread per target BLOCK:
+//             A_rs -= sum_v W_rv W_sv^T (49 accumulators, host-ordered contribution list:
+//             deterministic), b_r -= sum_v W_rv y_v.  barrier.
+//   tail      the remaining dense core (<= 27 poses, 189 unknowns) lives in REGISTERS as 16x16
+//             f64 tiles of the lower triangle.  The tile map is a compile-time function of the
+//             tail's tile count T: slot s holds tile (I0_s + wave, J_s), i.e. each tile column
+//             is cut into groups of 4 consecutive tiles, one per wave.  Factored right-looking
+//             one pose (7 columns) at a time, two barriers per pose:
+//               A: every wave with panel rows factors the 7x7 diagonal block in registers (from
+//                  LDS broadcasts) and solves y_K = L^-1 z_K; each thread turns one panel row
+//                  into a row of L (forward substitution) and updates its RHS entry; wave 0
+//                  stores L_KK^-1 for the back-substitution | barrier |
+//               B: rank-7 update of the live tiles, two v_mfma_f64_16x16x4_f64 each (operand
+//                  loads of 4 slots ahead of their MFMAs); the owners of the next 7 columns
+//                  extract them to LDS | barrier.
+//             Back-substitution right-looking (x_K = L_KK^-T z_K as a matvec), one barrier
+//             per pose, the L entries of the next pose prefetched.
+//   back      the rounds in reverse: x_v = L^-T (y_v - sum_r W_rv^T x_r), 7 lanes per pose.
+//   retract   dx = -x (0 if a pivot failed), Twc <- exp(dx) * Twc, ||dx|| < delta_thresh.
+// Failure semantics follow SimplicialLLT: a pivot <= 0 fails (NaN passes) => dx = 0.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gn_kernels.h"
+#include "sim3.h"
+
+namespace m3s {
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = kSolveThreads;
+constexpr int kWaves = kThreads / 64;
+constexpr int kGroups = 9;   // 7-lane groups (one pose each) per wave
+constexpr int kPS = 9;       // LDS row stride (doubles) of the panel buffers: conflict-free MFMA reads
+constexpr int kLRec = 28;    // tail per-pose record in LDS: packed lower L_KK^-1
+constexpr int kMaxTicks = 96;
+
+// dynamic LDS (doubles): a union of the tail buffers and the round staging, then the plan ints
+constexpr int kOffPn = 0;
+constexpr int kOffPop = kOffPn + kTailMax * kPS;
+constexpr int kOffZ = kOffPop + kTailMax * kPS;
+constexpr int kOffL = kOffZ + kTailMax;
+constexpr int kTailDoubles = kOffL + kTailPoseMax * kLRec;
+constexpr int kOffWst = 0;                                   // round: W blocks of the round
+constexpr int kOffYst = kOffWst + kSolveWStage;              // round: y of the round's poses
+constexpr int kRoundDoubles = kOffYst + 7 * kSolveRoundPoses;
+constexpr int kRegionDoubles = kTailDoubles > kRoundDoubles ? kTailDoubles : kRoundDoubles;
+
+__host__ __device__ constexpr int pk(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower
+
+// Compile-time tile map of a T x T tile lower triangle: tile column J is cut into groups of
+// 4 consecutive tile rows (I0, I0+1, I0+2, I0+3), one per wave; slot s = one group.
+__host__ __device__ constexpr int tail_slots(int T) {
+    int n = 0;
+    for (int J = 0; J < T; J++) n += (T - J + 3) / 4;
+    return n;
+}
+__host__ __device__ constexpr int slot_J(int T, int s) {
+    for (int J = 0; J < T; J++) {
+        const int g = (T - J + 3) / 4;
+        if (s < g) return J;
+        s -= g;
+    }
+    return T;
+}
+__host__ __device__ constexpr int slot_I0(int T, int s) {
+    for (int J = 0; J < T; J++) {
+        const int g = (T - J + 3) / 4;
+        if (s < g) return J + 4 * s;
+        s -= g;
+    }
+    return T;
+}
+
+// Workgroup barrier that orders LDS only: it waits for this wave's LDS operations but not for
+// its global stores (a __syncthreads() release fence waits for every outstanding global store
+// to be acknowledged, ~1 us).  Global data handed between waves of the solve always crosses a
+// full __syncthreads() before it is read.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// 1/sqrt(d) to f64 accuracy: v_rsq_f64 + one Newton step (d <= 0 / NaN propagate)
+__device__ __forceinline__ double rsqrt_f64(double d) {
+    const double y = __builtin_amdgcn_rsq(d);
+    return y * fma(-0.5 * d * y, y, 1.5);
+}
+
+// Serial 7x7 LL^T in registers: a (packed lower) -> L, inv[i] = 1 / L_ii.
+__device__ __forceinline__ void chol7(double (&a)[28], double (&inv)[7], bool& bad) {
+#pragma unroll
+    for (int p = 0; p < 7; p++) {
+        const double d = a[pk(p, p)];
+        bad |= (d <= 0.0);  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
+        const double y = rsqrt_f64(d);
+        inv[p] = y;
+        a[pk(p, p)] = d * y;
+#pragma unroll
+        for (int i = p + 1; i < 7; i++) a[pk(i, p)] *= y;
+#pragma unroll
+        for (int i = p + 1; i < 7; i++)
+#pragma unroll
+            for (int j = p + 1; j <= i; j++) a[pk(i, j)] = fma(-a[pk(i, p)], a[pk(j, p)], a[pk(i, j)]);
+    }
+}
+
+// out = L^-1 in (forward substitution)
+__device__ __forceinline__ void fwd7(const double (&L)[28], const double (&inv)[7],
+                                     const double (&in)[7], double (&out)[7]) {
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+        double s = in[c];
+#pragma unroll
+        for (int m = 0; m < c; m++) s = fma(-L[pk(c, m)], out[m], s);
+        out[c] = s * inv[c];
+    }
+}
+
+// z <- L^-T z (backward substitution)
+__device__ __forceinline__ void bwd7(const double (&L)[28], const double (&inv)[7], double (&z)[7]) {
+#pragma unroll
+    for (int c = 6; c >= 0; c--) {
+        double s = z[c];
+#pragma unroll
+        for (int m = c + 1; m < 7; m++) s = fma(-L[pk(m, c)], z[m], s);
+        z[c] = s * inv[c];
+    }
+}
+
+// Li = L^-1 (packed lower) from L and inv = 1/diag
+__device__ __forceinline__ void inv7(const double (&L)[28], const double (&inv)[7], double (&Li)[28]) {
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        Li[pk(j, j)] = inv[j];
+#pragma unroll
+        for (int i = j + 1; i < 7; i++) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = j; k < i; k++) s = fma(L[pk(i, k)], Li[pk(k, j)], s);
+            Li[pk(i, j)] = -s * inv[i];
+        }
+    }
+}
+
+// v[k] for a runtime k in [0, 7) without dynamic register indexing
+__device__ __forceinline__ double pick7(const double (&v)[7], int k) {
+    double r = v[0];
+#pragma unroll
+    for (int m = 1; m < 7; m++) r = (m == k) ? v[m] : r;
+    return r;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------
+// The in-register dense tail, as seen by wave W (compile time): its slots, their tiles
+// (I, J) and the operand registers are all compile-time, so the per-step work is the panel
+// operand loads, the MFMAs of the live slots and the extraction of the next panel.
+// The accumulators hold -A (so both MFMA operands are the plain panel P: -A += P_I P_J^T).
+// ---------------------------------------------------------------------------------
+struct SlotMap {
+    int n;
+    int I[64], J[64];
+};
+__host__ __device__ constexpr SlotMap make_slot_map(int T, int W) {
+    SlotMap m{};
+    m.n = 0;
+    for (int s = 0; s < tail_slots(T); s++) {
+        const int I = slot_I0(T, s) + W, J = slot_J(T, s);
+        if (I < T) {
+            m.I[m.n] = I;
+            m.J[m.n] = J;
+            m.n++;
+        }
+    }
+    return m;
+}
+
+template <int T, int W, typename Tick>
+__device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __restrict__ M, double* smem,
+                                           bool& bad, Tick& tick) {
+    constexpr SlotMap SM = make_slot_map(T, W);
+    constexpr int NS = SM.n;
+    double* __restrict__ sPn = smem + kOffPn;    // extracted panel (7 columns used)
+    double* __restrict__ sPop = smem + kOffPop;  // MFMA operand: L panel rows (0 outside live rows)
+    double* __restrict__ sZ = smem + kOffZ;      // tail RHS -> y -> (back) partial sums
+    double* __restrict__ sL = smem + kOffL;      // per tail pose: packed L_KK^-1
+    double* __restrict__ A = a.A;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int zb = a.zero_blk;
+    const int nt = a.ntail, n = 7 * nt;
+    const int* __restrict__ Mtail = M + a.o_tail;
+    const int* __restrict__ Mtmap = M + a.o_tmap;
+    d4 acc[NS > 0 ? NS : 1];
+    // -A from the blocks: every load issued unconditionally (entries outside the tail or of
+    // absent blocks read the zero block)
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+        const int col = 16 * SM.J[k] + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int row = 16 * SM.I[k] + (lane >> 4) + 4 * e;
+            const bool in = row < n && col < n;
+            const int code = in ? Mtmap[(row / 7) * nt + col / 7] : -1;
+            const int r7 = row % 7, c7 = col % 7;
+            const int64_t off = code < 0 ? (int64_t)zb * 49
+                                         : (int64_t)(code >> 1) * 49 + ((code & 1) ? c7 * 7 + r7 : r7 * 7 + c7);
+            acc[k][e] = -A[off];
+        }
+    }
+    for (int i = tid; i < kTailMax * kPS; i += kThreads) sPop[i] = 0.0;
+    for (int i = tid; i < n; i += kThreads) sZ[i] = a.b[(int64_t)Mtail[i / 7] * 7 + i % 7];
+    // the panel of pose 0 (tile column 0)
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+        if (SM.J[k] == 0) {
+            const int col = lane & 15;
+            if (col < 7) {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int row = 16 * SM.I[k] + (lane >> 4) + 4 * e;
+                    if (row >= col && row < n) sPn[row * kPS + col] = -acc[k][e];
+                }
+            }
+        }
+    }
+    lds_barrier();
+    tick(6);
+
+    for (int K = 0; K < nt; K++) {
+        const int c0 = 7 * K;
+        const int nrows = n - c0 - 7;  // panel rows below the diagonal block
+        // A1. wave 0: L_KK (in-lane serial, every lane), L_KK^-1 and y_K = L_KK^-1 z_K
+        if (W == 0) {
+            double L[28], inv[7], z[7], y[7], Li[28];
+#pragma unroll
+            for (int i = 0; i < 7; i++) {
+#pragma unroll
+                for (int j = 0; j <= i; j++) L[pk(i, j)] = sPn[(c0 + i) * kPS + j];
+                z[i] = sZ[c0 + i];
+            }
+            chol7(L, inv, bad);
+            inv7(L, inv, Li);
+#pragma unroll
+            for (int c = 0; c < 7; c++) {
+                double s2 = 0.0;
+#pragma unroll
+                for (int m = 0; m <= c; m++) s2 = fma(Li[pk(c, m)], z[m], s2);
+                y[c] = s2;
+            }
+            if (lane < 28) {
+                double v = Li[0];
+#pragma unroll
+                for (int k = 1; k < 28; k++) v = (k == lane) ? Li[k] : v;
+                sL[K * kLRec + lane] = v;
+            }
+            if (lane < 7) sZ[c0 + lane] = pick7(y, lane);
+        }
+        if (K >= 3 && K < 5) tick(7);
+        lds_barrier();
+        // A2. panel rows of L: P_i = L_KK^-1 a_i (matvec), RHS update
+        {
+            const double* Li = sL + K * kLRec;
+            const int i = c0 + 7 + tid;
+            if (tid < nrows) {
+                double in[7], out[7], y[7];
+#pragma unroll
+                for (int c = 0; c < 7; c++) {
+                    in[c] = sPn[i * kPS + c];
+                    y[c] = sZ[c0 + c];
+                }
+                double zr = sZ[i];
+                double* Lg = a.Lg + (int64_t)i * n + c0;
+#pragma unroll
+                for (int c = 0; c < 7; c++) {
+                    double s2 = 0.0;
+#pragma unroll
+                    for (int m = 0; m <= c; m++) s2 = fma(Li[pk(c, m)], in[m], s2);
+                    out[c] = s2;
+                    sPop[i * kPS + c] = s2;
+                    Lg[c] = s2;
+                    zr = fma(-s2, y[c], zr);
+                }
+                sZ[i] = zr;
+            }
+            if (tid >= kThreads - 7) {  // the pose's own rows leave the MFMA operand
+                const int rr = c0 + (tid - (kThreads - 7));
+#pragma unroll
+                for (int c = 0; c < 8; c++) sPop[rr * kPS + c] = 0.0;
+            }
+        }
+        if (K >= 3 && K < 5) tick(8);
+        lds_barrier();
+        // B. -C_IJ += P_I P_J^T for the live tiles (J >= Jmin), operands from registers.  The
+        //    slots are sorted by J, so the live ones are a suffix [kf, NS): a fall-through
+        //    switch enters the unrolled MFMA sequence at kf with no per-slot tests.  Then the
+        //    slots of the next pose's columns (J in [J0, J1], a contiguous range) are extracted.
+        {
+            const int Jmin = (c0 + 7) >> 4;
+            double P0[T], P1[T];
+            const int kq = lane >> 4;
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                const int r = (16 * t + (lane & 15)) * kPS + kq;
+                P0[t] = sPop[r];
+                P1[t] = sPop[r + 4];
+            }
+            int kf = 0;
+#pragma unroll
+            for (int k = 0; k < NS; k++) kf += SM.J[k] < Jmin;
+            // two passes (k = 0..3 of the panel, then 4..7) so the two MFMAs of one tile are
+            // never back to back
+#define M3S_MF(k, PP)                                                                              \
+    case k:                                                                                        \
+        if constexpr (k < NS)                                                                      \
+            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(PP[SM.I[k]], PP[SM.J[k]], acc[k], 0, 0, 0); \
+        [[fallthrough]];
+#define M3S_MFS(PP)                                                                                \
+    switch (kf) {                                                                                  \
+        M3S_MF(0, PP) M3S_MF(1, PP) M3S_MF(2, PP) M3S_MF(3, PP) M3S_MF(4, PP) M3S_MF(5, PP)        \
+        M3S_MF(6, PP) M3S_MF(7, PP) M3S_MF(8, PP) M3S_MF(9, PP) M3S_MF(10, PP) M3S_MF(11, PP)      \
+        M3S_MF(12, PP) M3S_MF(13, PP) M3S_MF(14, PP) M3S_MF(15, PP) M3S_MF(16, PP) M3S_MF(17, PP)  \
+        M3S_MF(18, PP) M3S_MF(19, PP) M3S_MF(20, PP) M3S_MF(21, PP) M3S_MF(22, PP) M3S_MF(23, PP)  \
+        M3S_MF(24, PP) M3S_MF(25, PP) M3S_MF(26, PP) M3S_MF(27, PP) M3S_MF(28, PP) M3S_MF(29, PP)  \
+        M3S_MF(30, PP) M3S_MF(31, PP)                                                              \
+        default: break;                                                                            \
+    }
+            M3S_MFS(P0)
+            M3S_MFS(P1)
+#undef M3S_MFS
+#undef M3S_MF
+            static_assert(NS <= 32, "tail slot map exceeds the unrolled MFMA switch");
+            if (K + 1 < nt) {
+                const int c1 = c0 + 7;
+                const int J0 = c1 >> 4, J1 = (c1 + 6) >> 4;
+                int klo = 0, khi = 0;
+#pragma unroll
+                for (int k = 0; k < NS; k++) {
+                    klo += SM.J[k] < J0;
+                    khi += SM.J[k] <= J1;
+                }
+                const int col_l = (lane & 15);
+                const int rbase = (lane >> 4);
+#define M3S_EX(k)                                                                                 \
+    case k:                                                                                       \
+        if constexpr (k < NS) {                                                                   \
+            if (k >= khi) break;                                                                  \
+            const int col = 16 * SM.J[k] + col_l;                                                 \
+            if (col >= c1 && col < c1 + 7) {                                                      \
+                _Pragma("unroll") for (int e = 0; e < 4; e++) {                                    \
+                    const int row = 16 * SM.I[k] + rbase + 4 * e;                                 \
+                    if (row >= col && row < n) sPn[row * kPS + (col - c1)] = -acc[k][e];          \
+                }                                                                                 \
+            }                                                                                     \
+        }                                                                                         \
+        [[fallthrough]];
+                switch (klo) {
+                    M3S_EX(0) M3S_EX(1) M3S_EX(2) M3S_EX(3) M3S_EX(4) M3S_EX(5) M3S_EX(6) M3S_EX(7)
+                    M3S_EX(8) M3S_EX(9) M3S_EX(10) M3S_EX(11) M3S_EX(12) M3S_EX(13) M3S_EX(14)
+                    M3S_EX(15) M3S_EX(16) M3S_EX(17) M3S_EX(18) M3S_EX(19) M3S_EX(20) M3S_EX(21)
+                    M3S_EX(22) M3S_EX(23) M3S_EX(24) M3S_EX(25) M3S_EX(26) M3S_EX(27) M3S_EX(28)
+                    M3S_EX(29) M3S_EX(30) M3S_EX(31)
+                    default: break;
+                }
+#undef M3S_EX
+            }
+            if (K >= 3 && K < 5) {
+                if (NS > 0) asm volatile("s_nop 0" :: "v"(acc[NS - 1][0]));
+                tick(9);
+            }
+        }
+        lds_barrier();
+        if (K >= 3 && K < 5) tick(11);
+    }
+    tick(2);
+
+    // back-substitution L^T x = y over the tail, right-looking: x_K = L_KK^-T z_K, then every
+    // z_j (j < 7K) drops its L[7K + c][j] x_K[c] terms.  The L entries a thread needs for the
+    // next pose are prefetched before the barrier.
+    double lp[7];
+    {
+        const int c0 = 7 * (nt - 1);
+#pragma unroll
+        for (int c = 0; c < 7; c++) lp[c] = tid < c0 ? a.Lg[(int64_t)(c0 + c) * n + tid] : 0.0;
+    }
+    for (int K = nt - 1; K >= 0; K--) {
+        const int c0 = 7 * K;
+        double Li[28], z[7], xk[7];
+#pragma unroll
+        for (int k = 0; k < 28; k++) Li[k] = sL[K * kLRec + k];
+#pragma unroll
+        for (int k = 0; k < 7; k++) z[k] = sZ[c0 + k];
+#pragma unroll
+        for (int c = 0; c < 7; c++) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int i = c; i < 7; i++) s2 = fma(Li[pk(i, c)], z[i], s2);
+            xk[c] = s2;
+        }
+        if (W == 0 && lane < 7) a.x[(int64_t)Mtail[K] * 7 + lane] = pick7(xk, lane);
+        if (tid < c0) {
+            double s2 = sZ[tid];
+#pragma unroll
+            for (int c = 0; c < 7; c++) s2 = fma(-lp[c], xk[c], s2);
+            sZ[tid] = s2;
+        }
+        if (K > 0) {
+            const int c1 = c0 - 7;
+#pragma unroll
+            for (int c = 0; c < 7; c++) lp[c] = tid < c1 ? a.Lg[(int64_t)(c1 + c) * n + tid] : 0.0;
+        }
+        lds_barrier();
+    }
+    __syncthreads();  // x of the tail (global) is read by the back rounds
+    tick(3);
+}
+
+// T = tile rows of the in-register tail (0: no in-kernel tail)
+template <int T>
+__global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
+    if (a.flags[kFlagDone]) return;
+    extern __shared__ double smem[];
+    __shared__ double sRed[kWaves];
+    __shared__ int sFail;
+    __shared__ uint64_t sT[kMaxTicks];
+    __shared__ int sTk[kMaxTicks];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+    bool bad = false;  // per thread; OR-ed into sFail before the retraction
+    if (tid == 0) sFail = 0;
+    // M3S_SOLVE_DEBUG: thread 0 records the wall clock (100 MHz) after each phase and prints
+    // the phase times once at the end (printf inside the timed phases would dominate them)
+    int nticks = 0;
+    if (a.debug && tid == 0) sT[nticks++] = wall_clock64();
+    auto tick = [&](int code) {
+        if (a.debug && tid == 0 && nticks < kMaxTicks) {
+            sTk[nticks] = code;
+            sT[nticks++] = wall_clock64();
+        }
+    };
+
+    // the plan integers: staged in LDS (one coalesced pass) when they fit
+    const int* __restrict__ M = a.meta;
+    if (a.meta_lds) {
+        int* sM = reinterpret_cast<int*>(smem + kRegionDoubles);
+        for (int i = tid; i < a.nmeta; i += kThreads) sM[i] = a.meta[i];
+        M = sM;
+        lds_barrier();
+    }
+    const int* __restrict__ Mrounds = M + a.o_rounds;
+    const int* __restrict__ Mnodes = M + a.o_nodes;
+    const int* __restrict__ Mfptr = M + a.o_fptr;
+    const int* __restrict__ Mfronts = M + a.o_fronts;
+    double* __restrict__ A = a.A;
+    double* __restrict__ b = a.b;
+    double* __restrict__ W = a.W;
+    const int zb = a.zero_blk;
+
+    // 7-lane groups: lane = 7 g + ra (lane 63 idle)
+    const int g = lane / 7, ra = lane - 7 * (lane / 7);
+
+    // ------------------------------------------------------------------ rounds
+    if (a.do_fwd) {
+        double* __restrict__ sW = smem + kOffWst;
+        double* __restrict__ sY = smem + kOffYst;
+        for (int rd = 0; rd < a.nrounds; rd++) {
+            const int* R = Mrounds + 8 * rd;  // node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount
+            const int nb = R[0], nn = R[1], wbeg = R[6];
+            for (int base = wave * kGroups; base < nn; base += kWaves * kGroups) {
+                const int qi = base + g;
+                if (lane < 7 * kGroups && qi < nn) {
+                    const int q = nb + qi, v = Mnodes[q];
+                    const int f0 = Mfptr[q], f1 = Mfptr[q + 1];
+                    // A_vv, b_v and the rows `ra` of the first 4 front blocks, all in flight
+                    double L[28], inv[7], bv[7];
+                    const double* Av = A + (int64_t)v * 49;
+#pragma unroll
+                    for (int i = 0; i < 7; i++)
+#pragma unroll
+                        for (int j = 0; j <= i; j++) L[pk(i, j)] = Av[i * 7 + j];
+#pragma unroll
+                    for (int m = 0; m < 7; m++) bv[m] = b[(int64_t)v * 7 + m];
+                    double rows[4][7];
+                    auto load_rows = [&](int fb) {
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const int f = fb + u;
+                            const int* F = Mfronts + 4 * (f < f1 ? f : 0);
+                            const int blk = f < f1 ? F[1] : zb;
+                            const int tr = f < f1 ? F[2] : 0;
+                            const double* Ab = A + (int64_t)blk * 49;
+#pragma unroll
+                            for (int m = 0; m < 7; m++) rows[u][m] = tr ? Ab[m * 7 + ra] : Ab[ra * 7 + m];
+                        }
+                    };
+                    load_rows(f0);
+                    chol7(L, inv, bad);
+                    double* Ls = a.Lstore + (int64_t)q * kLStoreRec;
+#pragma unroll
+                    for (int k = 0; k < 35; k++)
+                        if (k % 7 == ra) Ls[k] = k < 28 ? L[k] : inv[k - 28];
+                    {
+                        double yv[7];
+                        fwd7(L, inv, bv, yv);
+                        if (ra == 0) {
+#pragma unroll
+                            for (int m = 0; m < 7; m++) {
+                                a.y[(int64_t)v * 7 + m] = yv[m];
+                                sY[qi * 7 + m] = yv[m];
+                            }
+                        }
+                    }
+                    for (int fb = f0; fb < f1; fb += 4) {
+                        double cur[4][7];
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+#pragma unroll
+                            for (int m = 0; m < 7; m++) cur[u][m] = rows[u][m];
+                        if (fb + 4 < f1) load_rows(fb + 4);
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            if (fb + u < f1) {
+                                const int wid = Mfronts[4 * (fb + u) + 3];
+                                double out[7];
+                                fwd7(L, inv, cur[u], out);
+                                double* Wd = W + (int64_t)wid * 49 + ra * 7;
+                                double* Ws = sW + (wid - wbeg) * 49 + ra * 7;
+#pragma unroll
+                                for (int m = 0; m < 7; m++) {
+                                    Wd[m] = out[m];
+                                    Ws[m] = out[m];
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            if (rd < 2) tick(12);
+            lds_barrier();
+            // Schur updates, one thread per target block (49 accumulators) / RHS target (7);
+            // W and y come from LDS, the target from global (loaded up front)
+            const int tbeg = R[2], nbt = R[3], rbeg = R[4], nrt = R[5];
+            for (int t = tid; t < nbt + nrt; t += kThreads) {
+                if (t < nbt) {
+                    const int* T_ = M + a.o_tg + 3 * (tbeg + t);
+                    double* dst = A + (int64_t)T_[0] * 49;
+                    double acc[49];
+#pragma unroll
+                    for (int k = 0; k < 49; k++) acc[k] = dst[k];
+                    for (int c = T_[1]; c < T_[2]; c++) {
+                        const int* C = M + a.o_tc + 2 * c;
+                        const double* Wx = sW + (C[0] - wbeg) * 49;
+                        const double* Wy = sW + (C[1] - wbeg) * 49;
+#pragma unroll
+                        for (int m = 0; m < 7; m++) {
+                            double wx[7], wy[7];
+#pragma unroll
+                            for (int i = 0; i < 7; i++) {
+                                wx[i] = Wx[i * 7 + m];
+                                wy[i] = Wy[i * 7 + m];
+                            }
+#pragma unroll
+                            for (int i = 0; i < 7; i++)
+#pragma unroll
+                                for (int j = 0; j < 7; j++) acc[i * 7 + j] = fma(-wx[i], wy[j], acc[i * 7 + j]);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 49; k++) dst[k] = acc[k];
+                } else {
+                    const int* Rr = M + a.o_rtg + 3 * (rbeg + t - nbt);
+                    double* dst = b + (int64_t)Rr[0] * 7;
+                    double acc[7];
+#pragma unroll
+                    for (int k = 0; k < 7; k++) acc[k] = dst[k];
+                    for (int c = Rr[1]; c < Rr[2]; c++) {
+                        const int* C = M + a.o_rc + 2 * c;
+                        const double* Wr = sW + (C[0] - wbeg) * 49;
+                        const double* yv = sY + C[1] * 7;  // C[1]: the pose's slot in the round
+#pragma unroll
+                        for (int i = 0; i < 7; i++)
+#pragma unroll
+                            for (int m = 0; m < 7; m++) acc[i] = fma(-Wr[i * 7 + m], yv[m], acc[i]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 7; k++) dst[k] = acc[k];
+                }
+            }
+            __syncthreads();
+            tick(1);
+        }
+    }
+
+    // ------------------------------------------------------------------ dense tail
+    if constexpr (T > 0) {
+        if (a.do_tail && a.ntail > 0) {
+            switch (wave) {  // compile-time tile maps per wave
+                case 0: tail_solve<T, 0>(a, M, smem, bad, tick); break;
+                case 1: tail_solve<T, 1>(a, M, smem, bad, tick); break;
+                case 2: tail_solve<T, 2>(a, M, smem, bad, tick); break;
+                default: tail_solve<T, 3>(a, M, smem, bad, tick); break;
+            }
+        }
+    }
+
+    // ------------------------------------------------------------------ back rounds
+    if (a.do_back) {
+        for (int rd = a.nrounds - 1; rd >= 0; rd--) {
+            const int* R = Mrounds + 8 * rd;
+            const int nb = R[0], nn = R[1];
+            for (int base = wave * kGroups; base < nn; base += kWaves * kGroups) {
+                const int qi = base + g;
+                const bool on = lane < 7 * kGroups && qi < nn;
+                const int q = nb + (on ? qi : 0);
+                // lane ra: z_ra = y_v[ra] - sum_r (W_rv^T x_r)[ra]
+                double z = 0.0;
+                double L[28], inv[7];
+                if (on) {
+                    const double* Ls = a.Lstore + (int64_t)q * kLStoreRec;
+#pragma unroll
+                    for (int k = 0; k < 28; k++) L[k] = Ls[k];
+#pragma unroll
+                    for (int k = 0; k < 7; k++) inv[k] = Ls[28 + k];
+                    const int v = Mnodes[q];
+                    z = a.y[(int64_t)v * 7 + ra];
+                    const int f0 = Mfptr[q], f1 = Mfptr[q + 1];
+                    for (int fb = f0; fb < f1; fb += 4) {
+                        double wv[4][7], xv[4][7];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const int f = fb + u < f1 ? fb + u : fb;
+                            const int* F = Mfronts + 4 * f;
+                            const double* Wr = W + (int64_t)F[3] * 49 + ra;
+                            const double* xr = a.x + (int64_t)F[0] * 7;
+#pragma unroll
+                            for (int i = 0; i < 7; i++) {
+                                wv[u][i] = Wr[i * 7];
+                                xv[u][i] = xr[i];
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+                            if (fb + u < f1)
+#pragma unroll
+                                for (int i = 0; i < 7; i++) z = fma(-wv[u][i], xv[u][i], z);
+                    }
+                }
+                double zz[7];
+#pragma unroll
+                for (int m = 0; m < 7; m++) zz[m] = __shfl(z, (lane < 63 ? 7 * g : 0) + m, 64);
+                if (on) {
+                    bwd7(L, inv, zz);
+                    a.x[(int64_t)Mnodes[q] * 7 + ra] = pick7(zz, ra);
+                }
+            }
+            __syncthreads();
+        }
+        tick(4);
+
+        // -------------------------------------------------------------- retract
+        if (bad) sFail = 1;  // benign race: every writer stores 1
+        __syncthreads();
+        const bool fail = sFail != 0 || a.flags[kFlagFail] != 0;
+        double nrm = 0.0;
+        for (int p = 1 + tid; p < a.N; p += kThreads) {
+            float xi[7];
+#pragma unroll
+            for (int q = 0; q < 7; q++) {
+                const float v = fail ? 0.0f : -(float)a.x[(int64_t)(p - 1) * 7 + q];
+                xi[q] = v;
+                a.dx[(int64_t)(p - 1) * 7 + q] = v;
+                nrm += (double)v * (double)v;
+            }
+            retr_sim3(xi, a.Twc + (int64_t)p * 8);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
+        if (lane == 0) sRed[wave] = nrm;
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0;
+            for (int w = 0; w < kWaves; w++) s += sRed[w];
+            a.flags[kFlagFail] = 0;
+            if ((float)sqrt(s) < a.delta_thresh) a.flags[kFlagDone] = 1;
+        }
+        tick(5);
+    } else if (a.do_fwd) {
+        // forward-only launch (the tail is factored by the multi-launch dense path): publish
+        // a failed pivot for the retraction launch
+        if (bad) sFail = 1;
+        __syncthreads();
+        if (tid == 0 && sFail) a.flags[kFlagFail] = 1;
+    }
+    if (a.debug && tid == 0) {
+        for (int k = 1; k < nticks; k++) {
+            const double us = (double)(sT[k] - sT[k - 1]) * 0.01;
+            switch (sTk[k]) {
+                case 1: printf("gn_solve  R: schur+barrier %8.2f us\n", us); break;
+                case 2: printf("gn_solve tail factor %8.2f us\n", us); break;
+                case 3: printf("gn_solve tail back   %8.2f us\n", us); break;
+                case 4: printf("gn_solve back rounds %8.2f us\n", us); break;
+                case 6: printf("gn_solve tail load   %8.2f us\n", us); break;
+                case 7: printf("gn_solve  K: A1 chol (w0)  %8.2f us\n", us); break;
+                case 8: printf("gn_solve  K: A2 rows       %8.2f us\n", us); break;
+                case 9: printf("gn_solve  K: B mfma+extract %8.2f us\n", us); break;
+                case 11: printf("gn_solve  K: barrier B     %8.2f us\n", us); break;
+                case 12: printf("gn_solve  R: factor (w0)  %8.2f us\n", us); break;
+                default: printf("gn_solve retract     %8.2f us\n", us); break;
+            }
+        }
+    }
+}
+
+size_t solve_lds_bytes(int nmeta_lds) {
+    return sizeof(double) * kRegionDoubles + sizeof(int) * (size_t)nmeta_lds;
+}
+
+hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args) {
+    int T = 0;
+    if (args.do_tail && args.ntail > 0) {
+        T = (7 * args.ntail + 15) / 16;
+        T += T & 1;  // instantiated for even T (a padding tile row is harmless)
+    }
+    const size_t lds = solve_lds_bytes(args.meta_lds ? args.nmeta : 0);
+#define M3S_SOLVE(TT)                                                                         \
+    do {                                                                                      \
+        static bool attr = false;                                                             \
+        if (!attr) {                                                                          \
+            hipError_t e = hipFuncSetAttribute((const void*)gn_solve_kernel<TT>,              \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                                               (int)kSolveMaxLds);                            \
+            if (e != hipSuccess) return e;                                                    \
+            attr = true;                                                                      \
+        }                                                                                     \
+        hipLaunchKernelGGL(gn_solve_kernel<TT>, dim3(1), dim3(kThreads), lds, st, args);      \
+    } while (0)
+    switch (T) {
+        case 0: M3S_SOLVE(0); break;
+        case 2: M3S_SOLVE(2); break;
+        case 4: M3S_SOLVE(4); break;
+        case 6: M3S_SOLVE(6); break;
+        case 8: M3S_SOLVE(8); break;
+        case 10: M3S_SOLVE(10); break;
+        case 12: M3S_SOLVE(12); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef M3S_SOLVE
+    return hipGetLastError();
+}
+
+}  // namespace m3s

@@ -1,4 +1,4 @@
-// gn_sparse.hip -- block-sparse elimination of the pose-graph normal equations.
+// gn_sparse.hip -- the multi-launch block-sparse solve of the pose-graph normal equations.
 //
 // The GN system is a graph Laplacian with 7x7 blocks: one block row per non-pinned pose,
 // a block per co-observing pose pair.  The driver (gn_driver.hip, build_sparse_plan) picks,
@@ -8,9 +8,11 @@
 //               pose r (the L blocks), y_v = Li_v b_v                    (the forward solve)
 //   sp_schur  : A_rs -= sum_v W_rv W_sv^T, b_r -= sum_v W_rv y_v over the round, each target
 //               summed by one workgroup over a host-ordered contribution list (deterministic)
-// The poses left after the rounds (a small, dense-ish core) are factored by the dense
-// blocked Cholesky of gn_kernels.hip; then sp_back runs the rounds in reverse:
+// The poses left after the rounds (a dense-ish core) are moved into the dense f64 matrix of
+// the tiled Cholesky (gn_kernels.hip, sp_tail_*); then sp_back runs the rounds in reverse:
 //   x_v = Li_v^T (y_v - sum_r W_rv^T x_r).
+// This path serves graphs whose elimination needs many rounds (many workgroups per round hide
+// the memory latency); small graphs run the single-workgroup solve of gn_solve.hip instead.
 // Failure semantics follow SimplicialLLT (gn_kernels.cu:142-150): a pivot <= 0 sets the
 // failure flag and the update becomes zero.
 #include <hip/hip_runtime.h>
