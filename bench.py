@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--config", default="cfg3", choices=["cfg1", "cfg2", "cfg3", "cfg4"])
     ap.add_argument("--iters", type=int, default=None, help="GN iterations per op call")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-matching", action="store_true", help="skip the matching-kernel section")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "accum_traffic.json"))
     return ap.parse_args()
 
@@ -191,12 +192,68 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(g, mode, E_und)
+    if rank == 0 and world == 1 and not args.no_matching:
+        out["matching"] = matching_bench(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def matching_bench(dev, reps=10):
+    """Matching ops (SURVEY.md §8(d) 'matching pairs/s, B=1 and B=8'): iter_proj + refine_matches
+    at 512x384 (inputs resident, base.yaml matching parameters), kernel time from events on the
+    current stream; plus the whole match_iterative_proj glue call.  Bytes per pixel as SURVEY
+    §8(d): iter_proj 65 B, refine 128 B (+ the candidate gathers, served from L2/MALL)."""
+    import mast3r_slam_backends as mb
+    from m3s import synth
+    from m3s.config import config as cfg0
+    from m3s.matching import match_iterative_proj, prep_for_iter_proj
+
+    mc = cfg0["matching"]
+    res = {}
+    for B in (1, 8):
+        mp = synth.make_match_pair(B=B, H=384, W=512, seed=11, device=dev)
+        rays, pts, p_init = prep_for_iter_proj(mp.X11, mp.X21, mp.idx_init)
+        b, h, w = mp.X21.shape[:3]
+        D11 = mp.D11.half()
+        D21 = mp.D21.view(b, h * w, -1).half()
+        p1, _ = mb.iter_proj(rays, pts, p_init, mc["max_iter"], mc["lambda_init"], mc["convergence_thresh"])
+        p1 = p1.long()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        t_ip = t_rf = 0.0
+        for r in range(reps + 2):
+            ev[0].record()
+            mb.iter_proj(rays, pts, p_init, mc["max_iter"], mc["lambda_init"], mc["convergence_thresh"])
+            ev[1].record()
+            mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r >= 2:
+                t_ip += ev[0].elapsed_time(ev[1]) / reps
+                t_rf += ev[1].elapsed_time(ev[2]) / reps
+        for _ in range(2):
+            match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init)
+        torch.cuda.synchronize()
+        t_glue = (time.perf_counter() - t0) / reps * 1e3
+        npx = B * h * w
+        res[f"B{B}"] = {
+            "pairs_per_s_kernels": B / ((t_ip + t_rf) * 1e-3),
+            "pairs_per_s_glue": B / (t_glue * 1e-3),
+            "iter_proj_ms": t_ip,
+            "refine_ms": t_rf,
+            "match_iterative_proj_ms": t_glue,
+            "iter_proj_GBps": 65 * npx / (t_ip * 1e-3) / 1e9,
+            "refine_GBps": 128 * npx / (t_rf * 1e-3) / 1e9,
+            "refine_candidate_GBps": 245 * 48 * npx / (t_rf * 1e-3) / 1e9,
+        }
+    return res
 
 
 def cpu_baseline(g, mode, E_und):

@@ -151,25 +151,76 @@ typedef _Float16 half_t;
 // F = 24 fp16 fast path: the query descriptor lives in registers (3 x 16 B loads),
 // each candidate row is 48 B = 3 x dwordx4.  Sequential fp16 accumulation exactly as
 // c10::Half: round after every * and after every +=.
+// Pixel order (locality of the candidate gathers): a workgroup takes a 16x16 pixel tile (a
+// wave 4 rows x 16), and tiles are handed out so that the 8 XCDs (workgroups b, b+8, ... share
+// an XCD) each sweep a contiguous band of tile rows: an XCD's candidate windows then cover
+// ~1/8 of D11 (+ the search radius), which stays in its L2.  Pure performance mapping: every
+// pixel is computed exactly once whatever the placement.
+constexpr int kTile = 16;
+struct TileMap {
+    int tiles_x, tiles_y, ntiles;  // per image
+};
+__device__ __forceinline__ bool tile_pixel(const TileMap& tm, int64_t B, int W, int H, int64_t& g) {
+    const int64_t nblk = (int64_t)gridDim.x;
+    const int64_t blk = blockIdx.x;
+    // XCD-aware: logical block = (blk % 8) * ceil(nblk / 8) + blk / 8
+    const int64_t per = (nblk + 7) / 8;
+    const int64_t lb = (blk % 8) * per + blk / 8;
+    if (lb >= (int64_t)tm.ntiles * B) return false;
+    const int64_t b = lb / tm.ntiles;
+    const int t = (int)(lb - b * tm.ntiles);
+    const int ty = t / tm.tiles_x, tx = t - ty * tm.tiles_x;
+    const int lx = threadIdx.x & (kTile - 1), ly = threadIdx.x / kTile;
+    const int u = tx * kTile + lx, v = ty * kTile + ly;
+    if (u >= W || v >= H) return false;
+    g = b * (int64_t)H * W + (int64_t)v * W + u;
+    return true;
+}
+
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+// One candidate's score with c10::Half semantics: p_k = fl16(q_k * h_k), s = fl16(s + p_k) in
+// k order.  The products are formed two at a time (v_pk_mul_f16 rounds each half exactly like
+// the scalar multiply); the sum stays a sequential chain.
 template <int F>
+__device__ __forceinline__ half_t score_f16(const half2_t (&q2)[F / 2], const uint4 (&row)[F / 8]) {
+    half_t score = (half_t)0.0f;
+#pragma unroll
+    for (int c = 0; c < F / 8; c++) {
+        const half2_t* hp = reinterpret_cast<const half2_t*>(&row[c]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const half2_t p = q2[c * 4 + k] * hp[k];
+            score = score + p.x;
+            score = score + p.y;
+        }
+    }
+    return score;
+}
+
+// F = 24 fp16 fast path: the query descriptor lives in registers (3 x 16 B loads), each
+// candidate row is 48 B = 3 x dwordx4.  R = radius when it is a compile-time constant (the
+// window column of 2R+1 candidates is unrolled: its loads are issued together and the
+// independent score chains interleave), R < 0 for any radius.
+template <int F, int R>
 __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
     const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21,
     const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int H, int W, int64_t N,
-    int64_t total, int radius, int dilation_max) {
+    int64_t B, TileMap tm, int radius_rt, int dilation_max) {
     static_assert(F % 8 == 0, "vector path needs F % 8 == 0");
-    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (g >= total) return;
+    int64_t g;
+    if (!tile_pixel(tm, B, W, H, g)) return;
     const int64_t b = g / N;
 
-    half_t q[F];
+    half2_t q2[F / 2];
     {
         const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
 #pragma unroll
         for (int c = 0; c < F / 8; c++) {
             uint4 w = src[c];
-            const half_t* hp = reinterpret_cast<const half_t*>(&w);
+            const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
 #pragma unroll
-            for (int k = 0; k < 8; k++) q[c * 8 + k] = hp[k];
+            for (int k = 0; k < 4; k++) q2[c * 4 + k] = hp[k];
         }
     }
     const uint16_t* __restrict__ img = D11 + b * (int64_t)H * W * F;
@@ -178,30 +229,47 @@ __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
     int64_t v0 = p1[g * 2 + 1];
     half_t max_score = (half_t)kRefineHalfMaxInit;
     int64_t u_new = u0, v_new = v0;
+    const int radius = R >= 0 ? R : radius_rt;
     const int S = 2 * radius + 1;
     for (int d = dilation_max; d > 0; d--) {
         const int rd = radius * d;
         for (int i = 0; i < S; i++) {          // u offset outer (matching_kernels.cu:54)
             const int64_t u = u0 - rd + (int64_t)i * d;
-            for (int j = 0; j < S; j++) {      // v offset inner (:55)
-                const int64_t v = v0 - rd + (int64_t)j * d;
-                if (inside_image(u, v, W, H)) {
-                    const uint4* src = reinterpret_cast<const uint4*>(img + (v * W + u) * F);
-                    half_t score = (half_t)0.0f;
+            if constexpr (R >= 0) {
+                constexpr int SC = 2 * R + 1;
+                uint4 rows[SC][F / 8];
+                bool ok[SC];
 #pragma unroll
-                    for (int c = 0; c < F / 8; c++) {
-                        uint4 w = src[c];
-                        const half_t* hp = reinterpret_cast<const half_t*>(&w);
+                for (int j = 0; j < SC; j++) {  // v offset inner (:55)
+                    const int64_t v = v0 - rd + (int64_t)j * d;
+                    ok[j] = inside_image(u, v, W, H);
+                    const uint4* src = reinterpret_cast<const uint4*>(img + (ok[j] ? (v * W + u) * F : 0));
 #pragma unroll
-                        for (int k = 0; k < 8; k++) {
-                            const half_t p = q[c * 8 + k] * hp[k];
-                            score = score + p;
-                        }
-                    }
-                    if (score > max_score) {
+                    for (int c = 0; c < F / 8; c++) rows[j][c] = src[c];
+                }
+#pragma unroll
+                for (int j = 0; j < SC; j++) {
+                    const half_t score = score_f16<F>(q2, rows[j]);
+                    if (ok[j] && score > max_score) {
                         max_score = score;
                         u_new = u;
-                        v_new = v;
+                        v_new = v0 - rd + (int64_t)j * d;
+                    }
+                }
+            } else {
+                for (int j = 0; j < S; j++) {
+                    const int64_t v = v0 - rd + (int64_t)j * d;
+                    if (inside_image(u, v, W, H)) {
+                        uint4 row[F / 8];
+                        const uint4* src = reinterpret_cast<const uint4*>(img + (v * W + u) * F);
+#pragma unroll
+                        for (int c = 0; c < F / 8; c++) row[c] = src[c];
+                        const half_t score = score_f16<F>(q2, row);
+                        if (score > max_score) {
+                            max_score = score;
+                            u_new = u;
+                            v_new = v;
+                        }
                     }
                 }
             }
@@ -304,10 +372,21 @@ extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, 
     const int64_t total = B * N;
     if (total == 0) return M3S_OK;
     const bool aligned = ((uintptr_t)D11 % 16 == 0) && ((uintptr_t)D21 % 16 == 0);
-    if (F == 24 && aligned) {
-        hipLaunchKernelGGL(refine_f16_kernel<24>, dim3(grid_for(total)), dim3(kBlock), 0,
-                           (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, total,
-                           radius, dilation_max);
+    if (F == 24 && aligned && N == H * W) {
+        TileMap tm;
+        tm.tiles_x = (int)((W + kTile - 1) / kTile);
+        tm.tiles_y = (int)((H + kTile - 1) / kTile);
+        tm.ntiles = tm.tiles_x * tm.tiles_y;
+        const int64_t nblk = (int64_t)tm.ntiles * B;
+        const int64_t grid = (nblk + 7) / 8 * 8;  // whole rounds of the 8 XCDs
+        if (radius == 3)  // base.yaml:13
+            hipLaunchKernelGGL((refine_f16_kernel<24, 3>), dim3((unsigned)grid), dim3(kBlock), 0,
+                               (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, B, tm,
+                               radius, dilation_max);
+        else
+            hipLaunchKernelGGL((refine_f16_kernel<24, -1>), dim3((unsigned)grid), dim3(kBlock), 0,
+                               (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, B, tm,
+                               radius, dilation_max);
     } else {
         hipLaunchKernelGGL(refine_generic_kernel<half_t>, dim3(grid_for(total)), dim3(kBlock), 0,
                            (hipStream_t)stream, reinterpret_cast<const half_t*>(D11),
