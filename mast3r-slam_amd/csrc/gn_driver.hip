@@ -565,6 +565,8 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
         }
     sp.fused_tail = sp.ntail * 7 <= kTailMax;
     sp.fused = pol.fused && sp.fused_tail;
+    sp.nints = sp.nodes.size() + sp.fptr.size() + sp.fronts.size() + sp.tg.size() + sp.tc.size() +
+               sp.rtg.size() + sp.rc.size() + sp.tail.size() + sp.tmap.size() + 8 * sp.rounds.size();
     sp.enabled = true;
 }
 
@@ -905,8 +907,10 @@ int run(const m3s_gn_args& a) {
         // single-workgroup solve when its plan needs few rounds, else multi-launch
         const int choice = env_int("M3S_SOLVER", 0);
         build_sparse_plan(c.plan, npose, fused_policy(), c.sp);
-        const bool fused_ok = c.sp.fused && (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <=
-                                                                                 env_int("M3S_FUSED_MAX_ROUNDS", 3)));
+        const bool meta_fits = solve_lds_bytes((int)c.sp.nints) <= (size_t)kSolveMaxLds;
+        const bool fused_ok = c.sp.fused && meta_fits &&
+                              (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <=
+                                                                   env_int("M3S_FUSED_MAX_ROUNDS", 3)));
         if (!fused_ok) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
         t2 = now();
         rc = upload_sparse_plan(c.sp, npose, c.st);

@@ -200,7 +200,7 @@ __host__ __device__ constexpr SlotMap make_slot_map(int T, int W) {
 }
 
 template <int T, int W, typename Tick>
-__device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __restrict__ M, double* smem,
+__device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __restrict__ M, double* __restrict__ smem,
                                            bool& bad, Tick& tick) {
     constexpr SlotMap SM = make_slot_map(T, W);
     constexpr int NS = SM.n;
@@ -331,26 +331,21 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
             int kf = 0;
 #pragma unroll
             for (int k = 0; k < NS; k++) kf += SM.J[k] < Jmin;
-            // two passes (k = 0..3 of the panel, then 4..7) so the two MFMAs of one tile are
-            // never back to back
-#define M3S_MF(k, PP)                                                                              \
-    case k:                                                                                        \
-        if constexpr (k < NS)                                                                      \
-            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(PP[SM.I[k]], PP[SM.J[k]], acc[k], 0, 0, 0); \
+#define M3S_MF(k)                                                                                 \
+    case k:                                                                                       \
+        if constexpr (k < NS) {                                                                   \
+            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(P0[SM.I[k]], P0[SM.J[k]], acc[k], 0, 0, 0); \
+            acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(P1[SM.I[k]], P1[SM.J[k]], acc[k], 0, 0, 0); \
+        }                                                                                         \
         [[fallthrough]];
-#define M3S_MFS(PP)                                                                                \
-    switch (kf) {                                                                                  \
-        M3S_MF(0, PP) M3S_MF(1, PP) M3S_MF(2, PP) M3S_MF(3, PP) M3S_MF(4, PP) M3S_MF(5, PP)        \
-        M3S_MF(6, PP) M3S_MF(7, PP) M3S_MF(8, PP) M3S_MF(9, PP) M3S_MF(10, PP) M3S_MF(11, PP)      \
-        M3S_MF(12, PP) M3S_MF(13, PP) M3S_MF(14, PP) M3S_MF(15, PP) M3S_MF(16, PP) M3S_MF(17, PP)  \
-        M3S_MF(18, PP) M3S_MF(19, PP) M3S_MF(20, PP) M3S_MF(21, PP) M3S_MF(22, PP) M3S_MF(23, PP)  \
-        M3S_MF(24, PP) M3S_MF(25, PP) M3S_MF(26, PP) M3S_MF(27, PP) M3S_MF(28, PP) M3S_MF(29, PP)  \
-        M3S_MF(30, PP) M3S_MF(31, PP)                                                              \
-        default: break;                                                                            \
-    }
-            M3S_MFS(P0)
-            M3S_MFS(P1)
-#undef M3S_MFS
+            switch (kf) {
+                M3S_MF(0) M3S_MF(1) M3S_MF(2) M3S_MF(3) M3S_MF(4) M3S_MF(5) M3S_MF(6) M3S_MF(7)
+                M3S_MF(8) M3S_MF(9) M3S_MF(10) M3S_MF(11) M3S_MF(12) M3S_MF(13) M3S_MF(14)
+                M3S_MF(15) M3S_MF(16) M3S_MF(17) M3S_MF(18) M3S_MF(19) M3S_MF(20) M3S_MF(21)
+                M3S_MF(22) M3S_MF(23) M3S_MF(24) M3S_MF(25) M3S_MF(26) M3S_MF(27) M3S_MF(28)
+                M3S_MF(29) M3S_MF(30) M3S_MF(31)
+                default: break;
+            }
 #undef M3S_MF
             static_assert(NS <= 32, "tail slot map exceeds the unrolled MFMA switch");
             if (K + 1 < nt) {
@@ -463,14 +458,12 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
         }
     };
 
-    // the plan integers: staged in LDS (one coalesced pass) when they fit
-    const int* __restrict__ M = a.meta;
-    if (a.meta_lds) {
-        int* sM = reinterpret_cast<int*>(smem + kRegionDoubles);
-        for (int i = tid; i < a.nmeta; i += kThreads) sM[i] = a.meta[i];
-        M = sM;
-        lds_barrier();
-    }
+    // the plan integers, staged in LDS in one coalesced pass (the host only selects this solver
+    // when they fit).  M must be a known-LDS pointer: a generic pointer compiles to FLAT loads,
+    // and waiting on a FLAT load also waits for every outstanding global store (~1 us each).
+    int* __restrict__ M = reinterpret_cast<int*>(smem + kRegionDoubles);
+    for (int i = tid; i < a.nmeta; i += kThreads) M[i] = a.meta[i];
+    lds_barrier();
     const int* __restrict__ Mrounds = M + a.o_rounds;
     const int* __restrict__ Mnodes = M + a.o_nodes;
     const int* __restrict__ Mfptr = M + a.o_fptr;

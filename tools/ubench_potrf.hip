@@ -7,6 +7,13 @@
 #include <vector>
 
 using namespace m3s;
+namespace m3s {
+#include "potrf_v2.inc"
+}
+__global__ __launch_bounds__(512) void potrf_v2_kernel(double* Hd, int npad, double* Linv, int* flags,
+                                                        unsigned long long* tt) {
+    m3s::pv2::potrf64(Hd, npad, Linv, flags, tt);
+}
 
 // instrumented copy of the potrf phases: t[0..] = s_memtime after each phase (thread 0)
 __global__ __launch_bounds__(kPotrfThreads) void potrf_timed(double* __restrict__ Hd, int npad, int k,
@@ -167,5 +174,35 @@ int main() {
                "inverse %llu, store %llu, total %llu (%.1f us)\n",
                ms * 1000, t[0], t[1], t[2], t[3], t[4], t[5], t[5] / 2400.0);
     }
+    // v2: timing and agreement with the current kernel
+    std::vector<double> H1(H.size()), H2(H.size()), L1((size_t)npad * 64), L2((size_t)npad * 64);
+    (void)hipMemcpy(dH, H.data(), H.size() * 8, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(chol_potrf_kernel, dim3(1), dim3(kPotrfThreads), 0, 0, dH, npad, 0, dL, dF);
+    (void)hipMemcpy(H1.data(), dH, H.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(L1.data(), dL, 64 * 64 * 8, hipMemcpyDeviceToHost);
+    for (int rep = 0; rep < 3; rep++) {
+        (void)hipMemcpy(dH, H.data(), H.size() * 8, hipMemcpyHostToDevice);
+        (void)hipEventRecord(e0, 0);
+        hipLaunchKernelGGL(potrf_v2_kernel, dim3(1), dim3(512), 0, 0, dH, npad, dL, dF, dT);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        unsigned long long t[9];
+        (void)hipMemcpy(t, dT, sizeof(t), hipMemcpyDeviceToHost);
+        printf("potrf v2 launch %.1f us | cycles: load %llu, factor(w0) %llu, barrier %llu, update %llu, inverse %llu, store %llu | sub-panel 0: lds %llu chol %llu inv %llu\n",
+               ms * 1000, t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], t[8]);
+    }
+    (void)hipMemcpy(H2.data(), dH, H.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(L2.data(), dL, 64 * 64 * 8, hipMemcpyDeviceToHost);
+    double eL = 0, eI = 0, sL = 0, sI = 0;
+    for (int r = 0; r < 64; r++)
+        for (int c = 0; c <= r; c++) {
+            eL = fmax(eL, fabs(H1[(size_t)r * npad + c] - H2[(size_t)r * npad + c]));
+            sL = fmax(sL, fabs(H1[(size_t)r * npad + c]));
+            eI = fmax(eI, fabs(L1[r * 64 + c] - L2[r * 64 + c]));
+            sI = fmax(sI, fabs(L1[r * 64 + c]));
+        }
+    printf("v2 vs current: max|dL|/max|L| = %.2e, max|dLi|/max|Li| = %.2e\n", eL / sL, eI / sI);
     return 0;
 }
