@@ -376,19 +376,24 @@ int env_int(const char* name, int dflt) {
 // staged in LDS (capped), RHS contributions name the pose's slot in the round.  multi
 // (gn_sparse.hip): low-degree independent sets until fewer than rmin poses qualify, the rest
 // goes to the tiled dense Cholesky; RHS contributions name the pose.
+// mmd: multiple-minimum-degree candidates -- a round takes only poses of degree
+// <= max(2 d_min, d_min + 1) (d_min: the current minimum degree), which keeps the fill close to
+// a sequential minimum-degree ordering (cfg3: a 26-pose dense tail after 8 rounds, where taking
+// every independent pose of degree <= dcap leaves a 31-35-pose clique).
 struct RoundPolicy {
     bool fused;
     int dcap, rmin, rmax, tailcap, kmin;
+    bool mmd;
 };
 RoundPolicy fused_policy() {
     return {true, env_int("M3S_SPARSE_DCAP", 64), env_int("M3S_SPARSE_RMIN", 1),
             env_int("M3S_SPARSE_RMAX", 64),
             std::min(kTailPoseMax, env_int("M3S_SPARSE_TAILCAP", kTailPoseMax)),
-            env_int("M3S_SPARSE_KMIN", 4)};
+            env_int("M3S_SPARSE_KMIN", 4), env_int("M3S_SPARSE_MMD", 1) != 0};
 }
 RoundPolicy multi_policy() {
     return {false, env_int("M3S_MULTI_DCAP", 16), env_int("M3S_MULTI_RMIN", 2),
-            env_int("M3S_MULTI_RMAX", 64), 0, 0};
+            env_int("M3S_MULTI_RMAX", 64), 0, 0, env_int("M3S_MULTI_MMD", 0) != 0};
 }
 
 void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparsePlan& sp) {
@@ -450,8 +455,15 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
             if (alive[v] && deg[v] != nalive - 1) clique = false;
         if (clique && nalive > 1) break;
         cand.clear();
+        int dlim = dcap;
+        if (pol.mmd) {
+            int dmin = npose;
+            for (int v = 0; v < npose; v++)
+                if (alive[v]) dmin = std::min(dmin, deg[v]);
+            dlim = std::min(dcap, std::max(2 * dmin, dmin + 1));
+        }
         for (int v = 0; v < npose; v++)
-            if (alive[v] && deg[v] <= dcap) cand.push_back(v);
+            if (alive[v] && deg[v] <= dlim) cand.push_back(v);
         std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return deg[a] < deg[b]; });
         std::fill(blocked.begin(), blocked.end(), 0);
         chosen.clear();
@@ -901,14 +913,17 @@ int run(const m3s_gn_args& a) {
     if (npose <= 0) return M3S_OK;  // nothing to optimise (all poses pinned)
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
-    std::chrono::steady_clock::time_point t2 = t1, t3 = t1;
+    // the packed stream first: the GPU builds it while the host plans the elimination
+    rc = prepare_iterations(a, c);
+    if (rc) return rc;
+    std::chrono::steady_clock::time_point t2 = now(), t3 = t2;
     if (env_int("M3S_SOLVER_DENSE", 0) == 0) {
         // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
         // single-workgroup solve when its plan needs few rounds, else multi-launch
         const int choice = env_int("M3S_SOLVER", 0);
         build_sparse_plan(c.plan, npose, fused_policy(), c.sp);
         const bool meta_fits = solve_lds_bytes((int)c.sp.nints) <= (size_t)kSolveMaxLds;
-        const bool fused_ok = c.sp.fused && meta_fits &&
+        const bool fused_ok = c.sp.fused && meta_fits && npose <= solve_max_poses() &&
                               (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <=
                                                                    env_int("M3S_FUSED_MAX_ROUNDS", 3)));
         if (!fused_ok) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
@@ -917,11 +932,9 @@ int run(const m3s_gn_args& a) {
         if (rc) return rc;
         t3 = now();
     }
-    rc = prepare_iterations(a, c);
-    if (rc) return rc;
     const auto t4 = now();
     if (prof_host)
-        fprintf(stderr, "gn host: setup %.0f us, sparse plan %.0f us, upload %.0f us, pack launch %.0f us\n",
+        fprintf(stderr, "gn host: setup %.0f us, pack launch %.0f us, sparse plan %.0f us, upload %.0f us\n",
                 us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4));
     for (int itr = 0; itr < a.max_iter; itr++) {
         g_prof.mark(c.st);

@@ -108,6 +108,7 @@ struct SolveArgs {
     int debug;                     // M3S_SOLVE_DEBUG: printf phase times (wall clock, thread 0)
 };
 size_t solve_lds_bytes(int nmeta_lds);
+int solve_max_poses();  // x stays in LDS: the single-workgroup solve takes at most this many poses
 hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
                           float delta_thresh, int* flags);

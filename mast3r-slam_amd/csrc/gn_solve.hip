@@ -64,6 +64,7 @@ constexpr int kOffPop = kOffPn + kTailMax * kPS;
 constexpr int kOffZ = kOffPop + kTailMax * kPS;
 constexpr int kOffL = kOffZ + kTailMax;
 constexpr int kTailDoubles = kOffL + kTailPoseMax * kLRec;
+constexpr int kOffX = kTailDoubles;  // x (7 per pose) after the tail buffers: live from the tail on
 constexpr int kOffWst = 0;                                   // round: W blocks of the round
 constexpr int kOffYst = kOffWst + kSolveWStage;              // round: y of the round's poses
 constexpr int kRoundDoubles = kOffYst + 7 * kSolveRoundPoses;
@@ -208,6 +209,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
     double* __restrict__ sPop = smem + kOffPop;  // MFMA operand: L panel rows (0 outside live rows)
     double* __restrict__ sZ = smem + kOffZ;      // tail RHS -> y -> (back) partial sums
     double* __restrict__ sL = smem + kOffL;      // per tail pose: packed L_KK^-1
+    double* __restrict__ sX = smem + kOffX;      // the solution x (7 per pose), LDS-resident
     double* __restrict__ A = a.A;
     const int tid = threadIdx.x, lane = tid & 63;
     const int zb = a.zero_blk;
@@ -392,6 +394,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
     }
     tick(2);
 
+    __syncthreads();  // the L rows (global, written by every wave) are read below
     // back-substitution L^T x = y over the tail, right-looking: x_K = L_KK^-T z_K, then every
     // z_j (j < 7K) drops its L[7K + c][j] x_K[c] terms.  The L entries a thread needs for the
     // next pose are prefetched before the barrier.
@@ -415,7 +418,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
             for (int i = c; i < 7; i++) s2 = fma(Li[pk(i, c)], z[i], s2);
             xk[c] = s2;
         }
-        if (W == 0 && lane < 7) a.x[(int64_t)Mtail[K] * 7 + lane] = pick7(xk, lane);
+        if (W == 0 && lane < 7) sX[Mtail[K] * 7 + lane] = pick7(xk, lane);
         if (tid < c0) {
             double s2 = sZ[tid];
 #pragma unroll
@@ -429,7 +432,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
         }
         lds_barrier();
     }
-    __syncthreads();  // x of the tail (global) is read by the back rounds
+    lds_barrier();  // x of the tail (LDS) is read by the back rounds
     tick(3);
 }
 
@@ -473,6 +476,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
     double* __restrict__ W = a.W;
     const int zb = a.zero_blk;
 
+    double* __restrict__ sX = smem + kOffX;  // x: written by the tail and the back rounds
     // 7-lane groups: lane = 7 g + ra (lane 63 idle)
     const int g = lane / 7, ra = lane - 7 * (lane / 7);
 
@@ -512,21 +516,16 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
                     };
                     load_rows(f0);
                     chol7(L, inv, bad);
-                    double* Ls = a.Lstore + (int64_t)q * kLStoreRec;
-#pragma unroll
-                    for (int k = 0; k < 35; k++)
-                        if (k % 7 == ra) Ls[k] = k < 28 ? L[k] : inv[k - 28];
                     {
                         double yv[7];
                         fwd7(L, inv, bv, yv);
                         if (ra == 0) {
 #pragma unroll
-                            for (int m = 0; m < 7; m++) {
-                                a.y[(int64_t)v * 7 + m] = yv[m];
-                                sY[qi * 7 + m] = yv[m];
-                            }
+                            for (int m = 0; m < 7; m++) sY[qi * 7 + m] = yv[m];
                         }
                     }
+                    // W rows go to LDS only: a global store here would make every later load
+                    // wait for it (vmcnt counts loads and stores in order)
                     for (int fb = f0; fb < f1; fb += 4) {
                         double cur[4][7];
 #pragma unroll
@@ -540,69 +539,77 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
                                 const int wid = Mfronts[4 * (fb + u) + 3];
                                 double out[7];
                                 fwd7(L, inv, cur[u], out);
-                                double* Wd = W + (int64_t)wid * 49 + ra * 7;
                                 double* Ws = sW + (wid - wbeg) * 49 + ra * 7;
 #pragma unroll
-                                for (int m = 0; m < 7; m++) {
-                                    Wd[m] = out[m];
-                                    Ws[m] = out[m];
-                                }
+                                for (int m = 0; m < 7; m++) Ws[m] = out[m];
                             }
                         }
                     }
+                    double* Ls = a.Lstore + (int64_t)q * kLStoreRec;
+#pragma unroll
+                    for (int k = 0; k < 35; k++)
+                        if (k % 7 == ra) Ls[k] = k < 28 ? L[k] : inv[k - 28];
                 }
             }
             if (rd < 2) tick(12);
             lds_barrier();
             // Schur updates, one thread per target block (49 accumulators) / RHS target (7);
             // W and y come from LDS, the target from global (loaded up front)
-            const int tbeg = R[2], nbt = R[3], rbeg = R[4], nrt = R[5];
-            for (int t = tid; t < nbt + nrt; t += kThreads) {
-                if (t < nbt) {
-                    const int* T_ = M + a.o_tg + 3 * (tbeg + t);
-                    double* dst = A + (int64_t)T_[0] * 49;
-                    double acc[49];
+            {
+                const int tbeg = R[2], nbt = R[3], rbeg = R[4], nrt = R[5];
+                for (int t = tid; t < nbt + nrt; t += kThreads) {
+                    if (t < nbt) {
+                        const int* T_ = M + a.o_tg + 3 * (tbeg + t);
+                        double* dst = A + (int64_t)T_[0] * 49;
+                        double acc[49];
 #pragma unroll
-                    for (int k = 0; k < 49; k++) acc[k] = dst[k];
-                    for (int c = T_[1]; c < T_[2]; c++) {
-                        const int* C = M + a.o_tc + 2 * c;
-                        const double* Wx = sW + (C[0] - wbeg) * 49;
-                        const double* Wy = sW + (C[1] - wbeg) * 49;
+                        for (int k = 0; k < 49; k++) acc[k] = dst[k];
+                        for (int c = T_[1]; c < T_[2]; c++) {
+                            const int* C = M + a.o_tc + 2 * c;
+                            const double* Wx = sW + (C[0] - wbeg) * 49;
+                            const double* Wy = sW + (C[1] - wbeg) * 49;
 #pragma unroll
-                        for (int m = 0; m < 7; m++) {
-                            double wx[7], wy[7];
+                            for (int m = 0; m < 7; m++) {
+                                double wx[7], wy[7];
 #pragma unroll
-                            for (int i = 0; i < 7; i++) {
-                                wx[i] = Wx[i * 7 + m];
-                                wy[i] = Wy[i * 7 + m];
+                                for (int i = 0; i < 7; i++) {
+                                    wx[i] = Wx[i * 7 + m];
+                                    wy[i] = Wy[i * 7 + m];
+                                }
+#pragma unroll
+                                for (int i = 0; i < 7; i++)
+#pragma unroll
+                                    for (int j = 0; j < 7; j++) acc[i * 7 + j] = fma(-wx[i], wy[j], acc[i * 7 + j]);
                             }
+                        }
+#pragma unroll
+                        for (int k = 0; k < 49; k++) dst[k] = acc[k];
+                    } else {
+                        const int* Rr = M + a.o_rtg + 3 * (rbeg + t - nbt);
+                        double* dst = b + (int64_t)Rr[0] * 7;
+                        double acc[7];
+#pragma unroll
+                        for (int k = 0; k < 7; k++) acc[k] = dst[k];
+                        for (int c = Rr[1]; c < Rr[2]; c++) {
+                            const int* C = M + a.o_rc + 2 * c;
+                            const double* Wr = sW + (C[0] - wbeg) * 49;
+                            const double* yv = sY + C[1] * 7;  // C[1]: the pose's slot in the round
 #pragma unroll
                             for (int i = 0; i < 7; i++)
 #pragma unroll
-                                for (int j = 0; j < 7; j++) acc[i * 7 + j] = fma(-wx[i], wy[j], acc[i * 7 + j]);
+                                for (int m = 0; m < 7; m++) acc[i] = fma(-Wr[i * 7 + m], yv[m], acc[i]);
                         }
+#pragma unroll
+                        for (int k = 0; k < 7; k++) dst[k] = acc[k];
                     }
-#pragma unroll
-                    for (int k = 0; k < 49; k++) dst[k] = acc[k];
-                } else {
-                    const int* Rr = M + a.o_rtg + 3 * (rbeg + t - nbt);
-                    double* dst = b + (int64_t)Rr[0] * 7;
-                    double acc[7];
-#pragma unroll
-                    for (int k = 0; k < 7; k++) acc[k] = dst[k];
-                    for (int c = Rr[1]; c < Rr[2]; c++) {
-                        const int* C = M + a.o_rc + 2 * c;
-                        const double* Wr = sW + (C[0] - wbeg) * 49;
-                        const double* yv = sY + C[1] * 7;  // C[1]: the pose's slot in the round
-#pragma unroll
-                        for (int i = 0; i < 7; i++)
-#pragma unroll
-                            for (int m = 0; m < 7; m++) acc[i] = fma(-Wr[i * 7 + m], yv[m], acc[i]);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 7; k++) dst[k] = acc[k];
                 }
+                // the round's W blocks and y vectors (LDS) to global for the back-substitution
+                const int wcount = R[7];
+                for (int i = tid; i < wcount * 49; i += kThreads) W[(int64_t)wbeg * 49 + i] = sW[i];
+                for (int i = tid; i < nn * 7; i += kThreads)
+                    a.y[(int64_t)Mnodes[nb + i / 7] * 7 + i % 7] = sY[i];
             }
+            if (rd < 2) tick(13);
             __syncthreads();
             tick(1);
         }
@@ -648,7 +655,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
                             const int f = fb + u < f1 ? fb + u : fb;
                             const int* F = Mfronts + 4 * f;
                             const double* Wr = W + (int64_t)F[3] * 49 + ra;
-                            const double* xr = a.x + (int64_t)F[0] * 7;
+                            const double* xr = sX + F[0] * 7;
 #pragma unroll
                             for (int i = 0; i < 7; i++) {
                                 wv[u][i] = Wr[i * 7];
@@ -667,10 +674,10 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
                 for (int m = 0; m < 7; m++) zz[m] = __shfl(z, (lane < 63 ? 7 * g : 0) + m, 64);
                 if (on) {
                     bwd7(L, inv, zz);
-                    a.x[(int64_t)Mnodes[q] * 7 + ra] = pick7(zz, ra);
+                    sX[Mnodes[q] * 7 + ra] = pick7(zz, ra);
                 }
             }
-            __syncthreads();
+            lds_barrier();
         }
         tick(4);
 
@@ -683,7 +690,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
             float xi[7];
 #pragma unroll
             for (int q = 0; q < 7; q++) {
-                const float v = fail ? 0.0f : -(float)a.x[(int64_t)(p - 1) * 7 + q];
+                const float v = fail ? 0.0f : -(float)sX[(p - 1) * 7 + q];
                 xi[q] = v;
                 a.dx[(int64_t)(p - 1) * 7 + q] = v;
                 nrm += (double)v * (double)v;
@@ -700,6 +707,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
             a.flags[kFlagFail] = 0;
             if ((float)sqrt(s) < a.delta_thresh) a.flags[kFlagDone] = 1;
         }
+        for (int i = tid; i < 7 * a.npose; i += kThreads) a.x[i] = sX[i];
         tick(5);
     } else if (a.do_fwd) {
         // forward-only launch (the tail is factored by the multi-launch dense path): publish
@@ -722,11 +730,14 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
                 case 9: printf("gn_solve  K: B mfma+extract %8.2f us\n", us); break;
                 case 11: printf("gn_solve  K: barrier B     %8.2f us\n", us); break;
                 case 12: printf("gn_solve  R: factor (w0)  %8.2f us\n", us); break;
+                case 13: printf("gn_solve  R: schur (w0)   %8.2f us\n", us); break;
                 default: printf("gn_solve retract     %8.2f us\n", us); break;
             }
         }
     }
 }
+
+int solve_max_poses() { return (kRegionDoubles - kOffX) / 7; }
 
 size_t solve_lds_bytes(int nmeta_lds) {
     return sizeof(double) * kRegionDoubles + sizeof(int) * (size_t)nmeta_lds;
