@@ -157,6 +157,66 @@ int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, double* b_host)
 int m3s_prof_begin(void);
 int m3s_prof_end(double* out /* [4] */, int* n_iter);
 
+/* ---------------- frame tracking (single-pair Sim3 GN) ---------------- */
+
+/*
+ * track_sim3 -- replaces the torch loop of FrameTracker.opt_pose_ray_dist_sim3 /
+ * opt_pose_calib_sim3 (/root/reference/mast3r_slam/tracker.py:173-266) with its solve
+ * (:156-171), huber (nonlinear_optimizer.py:28-33), check_convergence (:5-25) and the
+ * residual models point_to_ray_dist / act_Sim3 / project_calib (geometry.py:17-104).
+ * The reference has no native op for this (it is torch + lietorch); this entry is an
+ * extension of the drop-in module (mast3r_slam_backends.track_sim3).
+ *   mode      M3S_GN_RAYS (ray + distance residual, 4 rows) or M3S_GN_CALIB (pixel +
+ *             log-depth, 3 rows)
+ *   Xf        [HW,3] f32  frame points already gathered by the match (Xf[idx_f2k])
+ *   Xk        [HW,3] f32  keyframe points (rays mode; unused by calib)
+ *   Qk        [HW]   f32  match confidence sqrt(Qff[idx] * Qkf)
+ *   valid     [HW]   u8   valid_opt
+ *   meas_k    [HW,3] f32  calib: (u, v, log z) of the keyframe pixel (0 where invalid)
+ *   valid_meas[HW]   u8   calib: z_k > depth_eps
+ *   K         [3,3]  f32  calib intrinsics (device)
+ *   T_WCf, T_WCk [8] f32  lietorch Sim3 data (t, q xyzw, s) (device)
+ *   T_WCf_out, T_CkCf_out [8] f32 (device, out)
+ *   info      [4] i32 (device, out): iterations run, converged, cholesky failed, 0
+ *   cost      [1] f64 (device, out): cost of the last linearisation
+ * The python-float parameters (sigmas, huber k, thresholds) are passed as double and
+ * rounded where torch rounds them.  One host synchronisation per `check_every`
+ * iterations (the reference syncs on every iteration's `.item()`).  A non-positive (or
+ * NaN) Cholesky pivot stops the loop and sets info[2] -- the caller raises, as
+ * torch.linalg.cholesky does (tracker.py:91).
+ */
+typedef struct m3s_track_args {
+    int mode;
+    const float* Xf;
+    const float* Xk;
+    const float* Qk;
+    const uint8_t* valid;
+    const float* meas_k;
+    const uint8_t* valid_meas;
+    const float* K;
+    const float* T_WCf;
+    const float* T_WCk;
+    int64_t HW;
+    int height, width, pixel_border;
+    double z_eps;
+    double sigma0;          /* sigma_ray   | sigma_pixel */
+    double sigma1;          /* sigma_dist  | sigma_depth */
+    double huber_k;
+    int max_iters;
+    double rel_error, delta_norm;
+    int check_every;        /* iterations between host checks of the convergence flag */
+    float* T_WCf_out;
+    float* T_CkCf_out;
+    int* info;
+    double* cost;
+    void* ws;
+    size_t ws_bytes;
+    void* stream;
+} m3s_track_args;
+
+size_t m3s_track_workspace_bytes(int64_t HW);
+int m3s_track_sim3(const m3s_track_args* args);
+
 /* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
 
 #define M3S_COMM_ID_BYTES 128

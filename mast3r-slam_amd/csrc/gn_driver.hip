@@ -867,6 +867,17 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     }
     if (sp.fused) {
         // one launch: rounds, in-register dense tail, back-substitution, retraction
+        if (env_int("M3S_SOLVE_SPLIT", 1) && S.nrounds > 0) {
+            // the rounds by a wider workgroup (memory latency overlapped across 8 waves), then
+            // the in-register tail + back-substitution + retraction
+            S.do_fwd = 1;
+            S.do_tail = S.do_back = 0;
+            M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+            S.do_fwd = 0;
+            S.do_tail = S.do_back = 1;
+            M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+            return M3S_OK;
+        }
         S.do_fwd = S.do_tail = S.do_back = 1;
         M3S_HIP_CHECK(launch_gn_solve(c.st, S));
         return M3S_OK;

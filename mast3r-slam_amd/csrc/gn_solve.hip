@@ -57,6 +57,7 @@ constexpr int kGroups = 9;   // 7-lane groups (one pose each) per wave
 constexpr int kPS = 9;       // LDS row stride (doubles) of the panel buffers: conflict-free MFMA reads
 constexpr int kLRec = 28;    // tail per-pose record in LDS: packed lower L_KK^-1
 constexpr int kMaxTicks = 96;
+constexpr int kSchurBatch = 4;  // Schur targets per 7-lane group with their loads in flight together
 
 // dynamic LDS (doubles): a union of the tail buffers and the round staging, then the plan ints
 constexpr int kOffPn = 0;
@@ -436,16 +437,19 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
     tick(3);
 }
 
-// T = tile rows of the in-register tail (0: no in-kernel tail)
-template <int T>
-__global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
+// T = tile rows of the in-register tail (0: no in-kernel tail); NT = threads (the tail needs
+// exactly kThreads; a rounds-only launch (T = 0) uses more waves to overlap memory latency)
+template <int T, int NT>
+__global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
+    constexpr int NW = NT / 64;
     if (a.flags[kFlagDone]) return;
     extern __shared__ double smem[];
-    __shared__ double sRed[kWaves];
+    __shared__ double sRed[NW];
     __shared__ int sFail;
     __shared__ uint64_t sT[kMaxTicks];
     __shared__ int sTk[kMaxTicks];
 
+    static_assert(T == 0 || NT == kThreads, "the in-register tail is laid out for kThreads");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
     bool bad = false;  // per thread; OR-ed into sFail before the retraction
@@ -465,7 +469,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
     // when they fit).  M must be a known-LDS pointer: a generic pointer compiles to FLAT loads,
     // and waiting on a FLAT load also waits for every outstanding global store (~1 us each).
     int* __restrict__ M = reinterpret_cast<int*>(smem + kRegionDoubles);
-    for (int i = tid; i < a.nmeta; i += kThreads) M[i] = a.meta[i];
+    for (int i = tid; i < a.nmeta; i += NT) M[i] = a.meta[i];
     lds_barrier();
     const int* __restrict__ Mrounds = M + a.o_rounds;
     const int* __restrict__ Mnodes = M + a.o_nodes;
@@ -487,7 +491,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
         for (int rd = 0; rd < a.nrounds; rd++) {
             const int* R = Mrounds + 8 * rd;  // node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount
             const int nb = R[0], nn = R[1], wbeg = R[6];
-            for (int base = wave * kGroups; base < nn; base += kWaves * kGroups) {
+            for (int base = wave * kGroups; base < nn; base += NW * kGroups) {
                 const int qi = base + g;
                 if (lane < 7 * kGroups && qi < nn) {
                     const int q = nb + qi, v = Mnodes[q];
@@ -553,60 +557,79 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
             }
             if (rd < 2) tick(12);
             lds_barrier();
-            // Schur updates, one thread per target block (49 accumulators) / RHS target (7);
-            // W and y come from LDS, the target from global (loaded up front)
+            // Schur updates, one 7-lane group per target; lane ra owns COLUMN ra of the block
+            // (7 accumulators), so each of the group's 7 loads / stores touches 7 consecutive
+            // doubles (a lane per block, or per block row, made every load instruction touch
+            // ~64 separate cache lines).  A_rs -= sum W_r W_s^T, b_r -= sum W_r y; W, y from
+            // LDS.  kSchurBatch targets per group in flight together.  Per entry the
+            // contributions are summed in host order, m inner (deterministic).
             {
                 const int tbeg = R[2], nbt = R[3], rbeg = R[4], nrt = R[5];
-                for (int t = tid; t < nbt + nrt; t += kThreads) {
-                    if (t < nbt) {
-                        const int* T_ = M + a.o_tg + 3 * (tbeg + t);
-                        double* dst = A + (int64_t)T_[0] * 49;
-                        double acc[49];
+                const int ntask = nbt + nrt;
+                constexpr int NG = NW * kGroups;
+                const int gid = wave * kGroups + g;
+                if (lane < 7 * kGroups) {
+                    for (int t0 = gid; t0 < ntask; t0 += NG * kSchurBatch) {
+                        double acc[kSchurBatch][7];
+                        int64_t off[kSchurBatch];
 #pragma unroll
-                        for (int k = 0; k < 49; k++) acc[k] = dst[k];
-                        for (int c = T_[1]; c < T_[2]; c++) {
-                            const int* C = M + a.o_tc + 2 * c;
-                            const double* Wx = sW + (C[0] - wbeg) * 49;
-                            const double* Wy = sW + (C[1] - wbeg) * 49;
+                        for (int u = 0; u < kSchurBatch; u++) {
+                            const int t = t0 + u * NG;
+                            if (t < nbt) {
+                                off[u] = (int64_t)M[a.o_tg + 3 * (tbeg + t)] * 49 + ra;
 #pragma unroll
-                            for (int m = 0; m < 7; m++) {
-                                double wx[7], wy[7];
-#pragma unroll
-                                for (int i = 0; i < 7; i++) {
-                                    wx[i] = Wx[i * 7 + m];
-                                    wy[i] = Wy[i * 7 + m];
-                                }
-#pragma unroll
-                                for (int i = 0; i < 7; i++)
-#pragma unroll
-                                    for (int j = 0; j < 7; j++) acc[i * 7 + j] = fma(-wx[i], wy[j], acc[i * 7 + j]);
+                                for (int i = 0; i < 7; i++) acc[u][i] = A[off[u] + 7 * i];
+                            } else if (t < ntask) {
+                                off[u] = (int64_t)M[a.o_rtg + 3 * (rbeg + t - nbt)] * 7 + ra;
+                                acc[u][0] = b[off[u]];
                             }
                         }
 #pragma unroll
-                        for (int k = 0; k < 49; k++) dst[k] = acc[k];
-                    } else {
-                        const int* Rr = M + a.o_rtg + 3 * (rbeg + t - nbt);
-                        double* dst = b + (int64_t)Rr[0] * 7;
-                        double acc[7];
+                        for (int u = 0; u < kSchurBatch; u++) {
+                            const int t = t0 + u * NG;
+                            if (t < nbt) {
+                                const int* T_ = M + a.o_tg + 3 * (tbeg + t);
+                                for (int c = T_[1]; c < T_[2]; c++) {
+                                    const int* C = M + a.o_tc + 2 * c;
+                                    const double* Wx = sW + (C[0] - wbeg) * 49;
+                                    const double* Wy = sW + (C[1] - wbeg) * 49 + ra * 7;
+                                    double wy[7];
 #pragma unroll
-                        for (int k = 0; k < 7; k++) acc[k] = dst[k];
-                        for (int c = Rr[1]; c < Rr[2]; c++) {
-                            const int* C = M + a.o_rc + 2 * c;
-                            const double* Wr = sW + (C[0] - wbeg) * 49;
-                            const double* yv = sY + C[1] * 7;  // C[1]: the pose's slot in the round
+                                    for (int m = 0; m < 7; m++) wy[m] = Wy[m];
 #pragma unroll
-                            for (int i = 0; i < 7; i++)
+                                    for (int m = 0; m < 7; m++)
 #pragma unroll
-                                for (int m = 0; m < 7; m++) acc[i] = fma(-Wr[i * 7 + m], yv[m], acc[i]);
+                                        for (int i = 0; i < 7; i++) acc[u][i] = fma(-Wx[i * 7 + m], wy[m], acc[u][i]);
+                                }
+                            } else if (t < ntask) {
+                                const int* Rr = M + a.o_rtg + 3 * (rbeg + t - nbt);
+                                double s1 = acc[u][0];
+                                for (int c = Rr[1]; c < Rr[2]; c++) {
+                                    const int* C = M + a.o_rc + 2 * c;
+                                    const double* Wr = sW + (C[0] - wbeg) * 49 + ra * 7;
+                                    const double* yv = sY + C[1] * 7;  // C[1]: the pose's slot in the round
+#pragma unroll
+                                    for (int m = 0; m < 7; m++) s1 = fma(-Wr[m], yv[m], s1);
+                                }
+                                acc[u][0] = s1;
+                            }
                         }
 #pragma unroll
-                        for (int k = 0; k < 7; k++) dst[k] = acc[k];
+                        for (int u = 0; u < kSchurBatch; u++) {
+                            const int t = t0 + u * NG;
+                            if (t < nbt) {
+#pragma unroll
+                                for (int i = 0; i < 7; i++) A[off[u] + 7 * i] = acc[u][i];
+                            } else if (t < ntask) {
+                                b[off[u]] = acc[u][0];
+                            }
+                        }
                     }
                 }
                 // the round's W blocks and y vectors (LDS) to global for the back-substitution
                 const int wcount = R[7];
-                for (int i = tid; i < wcount * 49; i += kThreads) W[(int64_t)wbeg * 49 + i] = sW[i];
-                for (int i = tid; i < nn * 7; i += kThreads)
+                for (int i = tid; i < wcount * 49; i += NT) W[(int64_t)wbeg * 49 + i] = sW[i];
+                for (int i = tid; i < nn * 7; i += NT)
                     a.y[(int64_t)Mnodes[nb + i / 7] * 7 + i % 7] = sY[i];
             }
             if (rd < 2) tick(13);
@@ -632,7 +655,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
         for (int rd = a.nrounds - 1; rd >= 0; rd--) {
             const int* R = Mrounds + 8 * rd;
             const int nb = R[0], nn = R[1];
-            for (int base = wave * kGroups; base < nn; base += kWaves * kGroups) {
+            for (int base = wave * kGroups; base < nn; base += NW * kGroups) {
                 const int qi = base + g;
                 const bool on = lane < 7 * kGroups && qi < nn;
                 const int q = nb + (on ? qi : 0);
@@ -686,7 +709,7 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
         __syncthreads();
         const bool fail = sFail != 0 || a.flags[kFlagFail] != 0;
         double nrm = 0.0;
-        for (int p = 1 + tid; p < a.N; p += kThreads) {
+        for (int p = 1 + tid; p < a.N; p += NT) {
             float xi[7];
 #pragma unroll
             for (int q = 0; q < 7; q++) {
@@ -703,11 +726,11 @@ __global__ __launch_bounds__(kThreads) void gn_solve_kernel(SolveArgs a) {
         __syncthreads();
         if (tid == 0) {
             double s = 0.0;
-            for (int w = 0; w < kWaves; w++) s += sRed[w];
+            for (int w = 0; w < NW; w++) s += sRed[w];
             a.flags[kFlagFail] = 0;
             if ((float)sqrt(s) < a.delta_thresh) a.flags[kFlagDone] = 1;
         }
-        for (int i = tid; i < 7 * a.npose; i += kThreads) a.x[i] = sX[i];
+        for (int i = tid; i < 7 * a.npose; i += NT) a.x[i] = sX[i];
         tick(5);
     } else if (a.do_fwd) {
         // forward-only launch (the tail is factored by the multi-launch dense path): publish
@@ -750,26 +773,30 @@ hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args) {
         T += T & 1;  // instantiated for even T (a padding tile row is harmless)
     }
     const size_t lds = solve_lds_bytes(args.meta_lds ? args.nmeta : 0);
-#define M3S_SOLVE(TT)                                                                         \
+#define M3S_SOLVE(TT, NTT)                                                                    \
     do {                                                                                      \
         static bool attr = false;                                                             \
         if (!attr) {                                                                          \
-            hipError_t e = hipFuncSetAttribute((const void*)gn_solve_kernel<TT>,              \
+            hipError_t e = hipFuncSetAttribute((const void*)gn_solve_kernel<TT, NTT>,         \
                                                hipFuncAttributeMaxDynamicSharedMemorySize,    \
                                                (int)kSolveMaxLds);                            \
             if (e != hipSuccess) return e;                                                    \
             attr = true;                                                                      \
         }                                                                                     \
-        hipLaunchKernelGGL(gn_solve_kernel<TT>, dim3(1), dim3(kThreads), lds, st, args);      \
+        hipLaunchKernelGGL((gn_solve_kernel<TT, NTT>), dim3(1), dim3(NTT), lds, st, args);    \
     } while (0)
+    if (T == 0 && args.do_fwd && !args.do_back) {
+        M3S_SOLVE(0, kSolveRoundThreads);  // rounds only: more waves in flight
+        return hipGetLastError();
+    }
     switch (T) {
-        case 0: M3S_SOLVE(0); break;
-        case 2: M3S_SOLVE(2); break;
-        case 4: M3S_SOLVE(4); break;
-        case 6: M3S_SOLVE(6); break;
-        case 8: M3S_SOLVE(8); break;
-        case 10: M3S_SOLVE(10); break;
-        case 12: M3S_SOLVE(12); break;
+        case 0: M3S_SOLVE(0, kThreads); break;
+        case 2: M3S_SOLVE(2, kThreads); break;
+        case 4: M3S_SOLVE(4, kThreads); break;
+        case 6: M3S_SOLVE(6, kThreads); break;
+        case 8: M3S_SOLVE(8, kThreads); break;
+        case 10: M3S_SOLVE(10, kThreads); break;
+        case 12: M3S_SOLVE(12, kThreads); break;
         default: return hipErrorInvalidValue;
     }
 #undef M3S_SOLVE

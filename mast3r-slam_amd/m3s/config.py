@@ -1,6 +1,6 @@
 """Hot-path parameters of the reference configuration (values only).
 
-Source: /root/reference/config/base.yaml:8-14 (matching) and :35-50 (local_opt);
+Source: /root/reference/config/base.yaml:8-14 (matching), :16-33 (tracking), :35-50 (local_opt);
 calib.yaml:1-6 switches ``use_calib`` on.  ``load_config`` reads the reference's YAML
 format (``inherit:`` chaining, floats like ``1e-8``) with a SafeLoader, like
 mast3r_slam/config.py:7-48.
@@ -21,6 +21,25 @@ DEFAULT_CONFIG = {
         "dist_thresh": 1e-1,
         "radius": 3,
         "dilation_max": 5,
+    },
+    "tracking": {  # base.yaml:16-33
+        "min_match_frac": 0.05,
+        "max_iters": 50,
+        "C_conf": 0.0,
+        "Q_conf": 1.5,
+        "rel_error": 1e-3,
+        "delta_norm": 1e-3,
+        "huber": 1.345,
+        "match_frac_thresh": 0.333,
+        "sigma_ray": 0.003,
+        "sigma_dist": 1e1,
+        "sigma_pixel": 1.0,
+        "sigma_depth": 1e1,
+        "sigma_point": 0.05,
+        "pixel_border": -10,
+        "depth_eps": 1e-6,
+        "filtering_mode": "weighted_pointmap",
+        "filtering_score": "median",
     },
     "local_opt": {
         "pin": 1,

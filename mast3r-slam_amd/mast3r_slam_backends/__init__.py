@@ -23,6 +23,8 @@ __all__ = [
     "gauss_newton_points",
     "gauss_newton_rays",
     "gauss_newton_calib",
+    "track_sim3",
+    "CholeskyError",
     "library_path",
     "lib",
 ]
@@ -305,6 +307,128 @@ def gauss_newton_calib(Twc, Xs, Cs, K, ii, jj, idx_ii2jj, valid_match, Q, height
     return _run_gn(GN_CALIB, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter,
                    delta_thresh, sigma_pixel, sigma_depth, C_thresh, Q_thresh, K=K,
                    height=height, width=width, pixel_border=pixel_border, z_eps=z_eps)
+
+
+# ---------------------------------------------------------------------------------
+# frame tracking (extension: the reference runs this loop in torch, tracker.py:173-266)
+# ---------------------------------------------------------------------------------
+
+
+class TrackArgs(ctypes.Structure):
+    """Mirror of ``m3s_track_args`` (include/m3s_backend.h)."""
+
+    _fields_ = [
+        ("mode", _i),
+        ("Xf", _vp),
+        ("Xk", _vp),
+        ("Qk", _vp),
+        ("valid", _vp),
+        ("meas_k", _vp),
+        ("valid_meas", _vp),
+        ("K", _vp),
+        ("T_WCf", _vp),
+        ("T_WCk", _vp),
+        ("HW", _c_int64),
+        ("height", _i),
+        ("width", _i),
+        ("pixel_border", _i),
+        ("z_eps", ctypes.c_double),
+        ("sigma0", ctypes.c_double),
+        ("sigma1", ctypes.c_double),
+        ("huber_k", ctypes.c_double),
+        ("max_iters", _i),
+        ("rel_error", ctypes.c_double),
+        ("delta_norm", ctypes.c_double),
+        ("check_every", _i),
+        ("T_WCf_out", _vp),
+        ("T_CkCf_out", _vp),
+        ("info", _vp),
+        ("cost", _vp),
+        ("ws", _vp),
+        ("ws_bytes", ctypes.c_size_t),
+        ("stream", _vp),
+    ]
+
+
+lib.m3s_track_sim3.argtypes = [ctypes.POINTER(TrackArgs)]
+lib.m3s_track_workspace_bytes.restype = ctypes.c_size_t
+lib.m3s_track_workspace_bytes.argtypes = [_c_int64]
+
+
+class CholeskyError(RuntimeError):
+    """The 7x7 normal equations were not positive definite (torch.linalg.cholesky raises
+    torch.linalg.LinAlgError, a RuntimeError, in the reference; tracker.py:91 catches it)."""
+
+
+def track_sim3(mode, Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma0, sigma1, huber_k, max_iters,
+               rel_error, delta_norm, meas_k=None, valid_meas_k=None, K=None, img_size=None,
+               pixel_border=0, z_eps=0.0, check_every=4):
+    """Sim3 GN of one frame against its keyframe (tracker.py:173-266) on the GPU.
+
+    mode "rays" (opt_pose_ray_dist_sim3) or "calib" (opt_pose_calib_sim3); Xf [HW,3] the
+    gathered frame points, Xk [HW,3], Qk [HW,1], valid [HW,1] bool, T_WCf / T_WCk lietorch
+    Sim3 data [1,8] (or [8]).  Returns (T_WCf [1,8], T_CkCf [1,8], iterations, cost).
+    Raises CholeskyError when the normal equations are not positive definite."""
+    m = GN_RAYS if mode == "rays" else GN_CALIB
+    _check(Xf, "Xf", torch.float32, 2)
+    _check(Qk, "Qk", torch.float32, 2)
+    _check(valid, "valid", torch.bool, 2)
+    T_WCf = T_WCf.reshape(-1)
+    T_WCk = T_WCk.reshape(-1)
+    _check(T_WCf, "T_WCf", torch.float32, 1)
+    _check(T_WCk, "T_WCk", torch.float32, 1)
+    HW = Xf.shape[0]
+    if Xf.shape[1] != 3 or Qk.shape != (HW, 1) or valid.shape != (HW, 1) or T_WCf.numel() != 8 \
+            or T_WCk.numel() != 8:
+        raise RuntimeError("track_sim3: expected Xf [HW,3], Qk [HW,1], valid [HW,1], poses [8]")
+    tens = dict(Xf=Xf, Qk=Qk, valid=valid, T_WCf=T_WCf, T_WCk=T_WCk)
+    if m == GN_RAYS:
+        _check(Xk, "Xk", torch.float32, 2)
+        if Xk.shape != (HW, 3):
+            raise RuntimeError("track_sim3: Xk must be [HW,3]")
+        tens["Xk"] = Xk
+    else:
+        _check(meas_k, "meas_k", torch.float32, 2)
+        _check(valid_meas_k, "valid_meas_k", torch.bool, 2)
+        _check(K, "K", torch.float32, 2)
+        if meas_k.shape != (HW, 3) or valid_meas_k.shape != (HW, 1) or K.shape != (3, 3):
+            raise RuntimeError("track_sim3: expected meas_k [HW,3], valid_meas_k [HW,1], K [3,3]")
+        tens.update(meas_k=meas_k, valid_meas_k=valid_meas_k, K=K)
+    dev = _on_device(**tens)
+    out_f = torch.empty((1, 8), dtype=torch.float32, device=dev)
+    out_r = torch.empty((1, 8), dtype=torch.float32, device=dev)
+    info = torch.zeros((4,), dtype=torch.int32, device=dev)
+    cost = torch.zeros((1,), dtype=torch.float64, device=dev)
+    ws_bytes = lib.m3s_track_workspace_bytes(HW)
+    ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
+    a = TrackArgs()
+    a.mode = m
+    a.Xf, a.Qk, a.valid = Xf.data_ptr(), Qk.data_ptr(), valid.data_ptr()
+    a.Xk = Xk.data_ptr() if m == GN_RAYS else None
+    if m == GN_CALIB:
+        a.meas_k, a.valid_meas, a.K = meas_k.data_ptr(), valid_meas_k.data_ptr(), K.data_ptr()
+        a.height, a.width = int(img_size[0]), int(img_size[1])
+    a.T_WCf, a.T_WCk = T_WCf.data_ptr(), T_WCk.data_ptr()
+    a.HW = HW
+    a.pixel_border = int(pixel_border)
+    a.z_eps = float(z_eps)
+    a.sigma0, a.sigma1 = float(sigma0), float(sigma1)
+    a.huber_k = float(huber_k)
+    a.max_iters = int(max_iters)
+    a.rel_error, a.delta_norm = float(rel_error), float(delta_norm)
+    a.check_every = int(check_every)
+    a.T_WCf_out, a.T_CkCf_out = out_f.data_ptr(), out_r.data_ptr()
+    a.info, a.cost = info.data_ptr(), cost.data_ptr()
+    a.ws, a.ws_bytes = ws.data_ptr(), ws_bytes
+    with torch.cuda.device(dev):
+        a.stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = lib.m3s_track_sim3(ctypes.byref(a))
+    _raise(rc, "track_sim3")
+    it, _, failed, _ = info.tolist()
+    if failed:
+        raise CholeskyError("track_sim3: normal equations not positive definite "
+                            f"(iteration {it + 1})")
+    return out_f, out_r, it, float(cost.item())
 
 
 def version() -> str:

@@ -1,0 +1,110 @@
+"""Frame-tracker Sim3 GN on the GPU (mast3r_slam_backends.track_sim3, track.hip) against the
+float64 oracle (oracle/track_oracle.py) and the outputs of the REFERENCE tracker code
+(tests/golden/track_golden.npz).  Tolerances: the op computes residuals / Jacobians in f32
+like the reference, with f64 reductions and solve, so poses agree to ~1e-6; the tests use
+2e-5 absolute on the pose data (|t| ~ 1, unit quaternion, s ~ 1)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import track_oracle as TO
+
+pytestmark = pytest.mark.gpu
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "track_golden.npz"))
+CFG = TO.TRACKING_CFG
+DEV = "cuda"
+
+
+def _t(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return (t if dtype is None else t.to(dtype)).to(DEV)
+
+
+def _gpu(be, p, mode, hw, cfg=CFG, max_iters=None):
+    kw = {}
+    if mode == "calib":
+        kw = dict(meas_k=_t(p["meas_k"]), valid_meas_k=_t(p["valid_meas_k"]), K=_t(p["K"]), img_size=hw,
+                  pixel_border=cfg["pixel_border"], z_eps=cfg["depth_eps"])
+    s0, s1 = (cfg["sigma_ray"], cfg["sigma_dist"]) if mode == "rays" else (cfg["sigma_pixel"], cfg["sigma_depth"])
+    Tf, Tr, it, cost = be.track_sim3(mode, _t(p["Xf"]), _t(p["Xk"]), _t(p["T_WCf"]).reshape(1, 8),
+                                     _t(p["T_WCk"]).reshape(1, 8), _t(p["Qk"]), _t(p["valid"]), s0, s1,
+                                     cfg["huber"], cfg["max_iters"] if max_iters is None else max_iters,
+                                     cfg["rel_error"], cfg["delta_norm"], **kw)
+    return Tf.cpu().numpy().reshape(8), Tr.cpu().numpy().reshape(8), it, cost
+
+
+def _oracle(p, mode, hw, cfg=CFG, max_iters=None):
+    if mode == "rays":
+        return TO.opt_pose_ray_dist_sim3(p["Xf"], p["Xk"], p["T_WCf"], p["T_WCk"], p["Qk"], p["valid"], cfg, max_iters)
+    return TO.opt_pose_calib_sim3(p["Xf"], p["T_WCf"], p["T_WCk"], p["Qk"], p["valid"], p["meas_k"],
+                                  p["valid_meas_k"], p["K"], hw, cfg, max_iters)
+
+
+@pytest.mark.parametrize("c", range(4))
+def test_track_matches_reference_outputs(backend, c):
+    g = {k[len(f"c{c}_"):]: GOLD[k] for k in GOLD.files if k.startswith(f"c{c}_")}
+    mode = str(g["mode"])
+    Tf, Tr, it, _ = _gpu(backend, g, mode, (24, 32))
+    To, Tro, ito, _ = _oracle(g, mode, (24, 32))
+    assert it == ito
+    np.testing.assert_allclose(Tf, g["out_T_WCf"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(Tr, g["out_T_CkCf"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(Tf, To, rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_track_full_size_fixed_iterations(backend, mode):
+    """512x384 noisy pair, exactly 6 iterations (convergence test disabled) vs the oracle."""
+    hw = (384, 512)
+    p = TO.make_tracking_pair(hw, seed=21, mode=mode, noise=0.003)
+    cfg = dict(CFG, rel_error=0.0, delta_norm=0.0)
+    Tf, Tr, it, cost = _gpu(backend, p, mode, hw, cfg, max_iters=6)
+    To, Tro, ito, costo = _oracle(p, mode, hw, cfg, max_iters=6)
+    assert it == ito == 6
+    np.testing.assert_allclose(Tf, To, rtol=0, atol=2e-5)
+    np.testing.assert_allclose(Tr, Tro, rtol=0, atol=2e-5)
+    assert abs(cost - costo) <= 1e-4 * abs(costo)
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_track_converges_like_oracle(backend, mode):
+    hw = (96, 128)
+    p = TO.make_tracking_pair(hw, seed=4, mode=mode, noise=0.002)
+    Tf, _, it, _ = _gpu(backend, p, mode, hw)
+    To, _, ito, _ = _oracle(p, mode, hw)
+    assert abs(it - ito) <= 1
+    np.testing.assert_allclose(Tf, To, rtol=0, atol=5e-5)
+
+
+def test_track_noise_free_recovers_truth(backend):
+    hw = (48, 64)
+    p = TO.make_tracking_pair(hw, seed=8, mode="rays")
+    cfg = dict(CFG, rel_error=0.0, delta_norm=0.0)
+    Tf, _, _, _ = _gpu(backend, p, "rays", hw, cfg, max_iters=8)
+    np.testing.assert_allclose(Tf, p["T_WCf_true"], rtol=0, atol=2e-5)
+
+
+def test_track_singular_system_raises(backend):
+    p = TO.make_tracking_pair((24, 32), seed=2)
+    p["valid"] = np.zeros_like(p["valid"])
+    with pytest.raises(backend.CholeskyError):
+        _gpu(backend, p, "rays", (24, 32))
+
+
+def test_track_deterministic(backend):
+    p = TO.make_tracking_pair((96, 128), seed=3, noise=0.003)
+    a = _gpu(backend, p, "rays", (96, 128))
+    b = _gpu(backend, p, "rays", (96, 128))
+    assert np.array_equal(a[0], b[0]) and a[2] == b[2]
+
+
+def test_frame_tracker_wrapper(backend):
+    from m3s.tracker import FrameTracker
+
+    g = {k[len("c0_"):]: GOLD[k] for k in GOLD.files if k.startswith("c0_")}
+    trk = FrameTracker(device=DEV)
+    Tf, Tr = trk.opt_pose_ray_dist_sim3(_t(g["Xf"]), _t(g["Xk"]), _t(g["T_WCf"]).reshape(1, 8),
+                                        _t(g["T_WCk"]).reshape(1, 8), _t(g["Qk"]), _t(g["valid"]))
+    np.testing.assert_allclose(Tf.data.cpu().numpy().reshape(8), g["out_T_WCf"], rtol=0, atol=2e-5)

@@ -13,6 +13,7 @@ for v in ${VARIANTS:-default}; do
     case $v in
     default) run default M3S_X=0 ;;
     fused) run fused M3S_SOLVER=1 M3S_FUSED_MAX_ROUNDS=64 ;;
+    fused_nosplit) run fused_nosplit M3S_SOLVER=1 M3S_FUSED_MAX_ROUNDS=64 M3S_SOLVE_SPLIT=0 ;;
     fused_nommd) run fused_nommd M3S_SOLVER=1 M3S_SPARSE_MMD=0 M3S_FUSED_MAX_ROUNDS=64 ;;
     multi) run multi M3S_SOLVER=2 ;;
     multi_mmd) run multi_mmd M3S_SOLVER=2 M3S_MULTI_MMD=1 ;;

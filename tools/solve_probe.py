@@ -29,7 +29,7 @@ def graph(topo):
         N = int(topo[6:])
         und = [(a, b) for a in range(N) for b in range(a + 1, N)]
     else:
-        return synth.make_graph(topo, H=24, W=32, seed=6)
+        return synth.make_graph(topo, H=24, W=32, seed=int(os.environ.get("PROBE_SEED", "6")))
     return synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
 
 
