@@ -194,6 +194,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(g, mode, E_und)
     if rank == 0 and world == 1 and not args.no_matching:
         out["matching"] = matching_bench(dev)
+        out["tracking"] = tracking_bench(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
@@ -253,6 +254,49 @@ def matching_bench(dev, reps=10):
             "refine_GBps": 128 * npx / (t_rf * 1e-3) / 1e9,
             "refine_candidate_GBps": 245 * 48 * npx / (t_rf * 1e-3) / 1e9,
         }
+    return res
+
+
+def tracking_bench(dev, reps=20):
+    """Frame tracking (tracker.py:173-266) as one track_sim3 op at 512x384, calib and rays:
+    ms per frame with the reference's convergence test (base.yaml tracking), and ms per GN
+    iteration with exactly 10 iterations.  Bytes per point and iteration: rays Xf 12 + Xk 12 +
+    Q 4 + valid 1 = 29; calib Xf 12 + meas 12 + Q 4 + valid 1 + valid_meas 1 = 30."""
+    import mast3r_slam_backends as mb
+    from m3s.config import config as cfg0
+    from m3s.synth import make_tracking_inputs
+
+    c = cfg0["tracking"]
+    res = {}
+    for mode in ("calib", "rays"):
+        p = make_tracking_inputs((384, 512), seed=21, mode=mode, device=dev)
+        s0, s1 = (c["sigma_ray"], c["sigma_dist"]) if mode == "rays" else (c["sigma_pixel"], c["sigma_depth"])
+        kw = {} if mode == "rays" else dict(meas_k=p["meas_k"], valid_meas_k=p["valid_meas_k"], K=p["K"],
+                                            img_size=(384, 512), pixel_border=c["pixel_border"],
+                                            z_eps=c["depth_eps"])
+
+        def run(iters, rel, dn):
+            return mb.track_sim3(mode, p["Xf"], p["Xk"], p["T_WCf"], p["T_WCk"], p["Qk"], p["valid"],
+                                 s0, s1, c["huber"], iters, rel, dn, **kw)
+
+        out = {}
+        for tag, (iters, rel, dn) in (("frame", (c["max_iters"], c["rel_error"], c["delta_norm"])),
+                                      ("fixed10", (10, 0.0, 0.0))):
+            for _ in range(3):
+                run(iters, rel, dn)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                _, _, it, _ = run(iters, rel, dn)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / reps * 1e3
+            out[f"{tag}_ms"] = ms
+            out[f"{tag}_iters"] = it
+        bpp = 29 if mode == "rays" else 30
+        out["ms_per_iter"] = out["fixed10_ms"] / 10
+        out["frames_per_s"] = 1e3 / out["frame_ms"]
+        out["GBps_per_iter"] = bpp * 384 * 512 / (out["ms_per_iter"] * 1e-3) / 1e9
+        res[mode] = out
     return res
 
 

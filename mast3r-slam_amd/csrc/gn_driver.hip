@@ -937,6 +937,9 @@ int run(const m3s_gn_args& a) {
         const bool fused_ok = c.sp.fused && meta_fits && npose <= solve_max_poses() &&
                               (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <=
                                                                    env_int("M3S_FUSED_MAX_ROUNDS", 3)));
+        if (env_int("M3S_SOLVE_DEBUG", 0) && !fused_ok)
+            fprintf(stderr, "fused solve rejected: fused_tail %d (ntail %d) rounds %zu nints %zu meta_fits %d\n",
+                    (int)c.sp.fused, c.sp.ntail, c.sp.rounds.size(), c.sp.nints, (int)meta_fits);
         if (!fused_ok) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
         t2 = now();
         rc = upload_sparse_plan(c.sp, npose, c.st);

@@ -89,8 +89,8 @@ constexpr int kTailMax = 192;      // in-register dense tail: <= 192 unknowns (1
 constexpr int kTailPoseMax = 27;   // = kTailMax / 7
 constexpr int kLStoreRec = 40;     // per eliminated pose: packed lower L (28) + 1/diag (7) + pad
 constexpr int kSolveMaxLds = 160 * 1024 - 2048;  // dynamic LDS cap (static LDS besides)
-constexpr int kSolveWStage = 8192;    // doubles: a round's W blocks staged in LDS
-constexpr int kSolveRoundPoses = 256; // poses per round (their y vectors staged in LDS)
+constexpr int kSolveWStage = 6144;    // doubles: a round's W blocks staged in LDS
+constexpr int kSolveRoundPoses = 64;  // poses per round (their y vectors staged in LDS)
 struct SolveArgs {
     double *A, *b;          // block-format system (gn_assemble_kernel), updated in place
     double *y, *Lstore, *W, *Lg, *x;

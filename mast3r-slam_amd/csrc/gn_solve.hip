@@ -52,7 +52,6 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = kSolveThreads;
-constexpr int kWaves = kThreads / 64;
 constexpr int kGroups = 9;   // 7-lane groups (one pose each) per wave
 constexpr int kPS = 9;       // LDS row stride (doubles) of the panel buffers: conflict-free MFMA reads
 constexpr int kLRec = 28;    // tail per-pose record in LDS: packed lower L_KK^-1

@@ -338,3 +338,37 @@ def make_match_pair(B=1, H=384, W=512, F=24, seed=7, device="cpu") -> MatchPair:
     ui = (idx_gt % W + jit[..., 0]).clamp(0, W - 1)
     vi = (idx_gt // W + jit[..., 1]).clamp(0, H - 1)
     return MatchPair(X11.contiguous(), X21.contiguous(), D11, D21, idx_gt, vi * W + ui)
+
+
+def make_tracking_inputs(hw=(384, 512), seed=0, mode="rays", noise=0.003, device="cpu"):
+    """Synthetic frame/keyframe pair in the layout FrameTracker's optimisers take
+    (tracker.py:173-266): Xf [HW,3] (already gathered by the match), Xk [HW,3], T_WCf / T_WCk
+    [1,8], Qk [HW,1], valid [HW,1] bool; calib adds meas_k [HW,3], valid_meas_k [HW,1], K."""
+    rng = np.random.default_rng(seed)
+    h, w = hw
+    n = h * w
+    Kn = intrinsics(h, w)
+    uu, vv = np.meshgrid(np.arange(w), np.arange(h))
+    z = 2.0 + 0.3 * np.sin(uu / w * 6.0) * np.cos(vv / h * 4.0) + 0.05 * rng.standard_normal((h, w))
+    rays = np.stack([(uu - Kn[0, 2]) / Kn[0, 0], (vv - Kn[1, 2]) / Kn[1, 1], np.ones((h, w))], -1)
+    Xk = (rays * z[..., None]).reshape(n, 3)
+    T_kf = (rng.normal(0, 0.03, 3), axis_angle_quat(rng.normal(0, 0.02, 3)), math.exp(rng.normal(0, 0.02)))
+    t, q, s = sim3_inv(T_kf)
+    Xf = s * Xk @ quat_to_rot(q).T + t + noise * rng.standard_normal((n, 3))
+    T_WCk = (rng.normal(0, 0.5, 3), axis_angle_quat(rng.normal(0, 0.1, 3)), math.exp(rng.normal(0, 0.1)))
+    T_true = sim3_compose(T_WCk, T_kf)
+    dT = (rng.normal(0, 0.01, 3), axis_angle_quat(rng.normal(0, 0.01, 3)), math.exp(rng.normal(0, 0.005)))
+    T_WCf = sim3_compose(dT, T_true)
+    f32 = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
+    out = dict(Xf=f32(Xf), Xk=f32(Xk), T_WCf=f32(sim3_to_vec(T_WCf)).reshape(1, 8),
+               T_WCk=f32(sim3_to_vec(T_WCk)).reshape(1, 8),
+               Qk=f32(np.exp(rng.normal(1.0, 0.5, (n, 1)))),
+               valid=torch.tensor(rng.random((n, 1)) > 0.1, device=device), K=f32(Kn))
+    if mode == "calib":
+        zk = out["Xk"][:, 2:3]
+        valid_meas = zk > 1e-6
+        uv = torch.stack([torch.arange(n, device=device) % w, torch.arange(n, device=device) // w], -1)
+        meas = torch.cat([uv.float(), torch.log(zk)], -1)
+        meas[~valid_meas.repeat(1, 3)] = 0.0
+        out.update(meas_k=meas.contiguous(), valid_meas_k=valid_meas.contiguous())
+    return out
