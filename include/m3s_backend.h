@@ -217,6 +217,21 @@ typedef struct m3s_track_args {
 size_t m3s_track_workspace_bytes(int64_t HW);
 int m3s_track_sim3(const m3s_track_args* args);
 
+/* ---------------- keyframe point-map fusion ---------------- */
+
+enum { M3S_FILTER_WEIGHTED_POINTMAP = 0, M3S_FILTER_INDEP_CONF = 1, M3S_FILTER_RECENT = 2 };
+
+/*
+ * pointmap_update -- replaces Frame.update_pointmap (frame.py:41-105) for the per-point
+ * filtering modes (weighted_pointmap :74-77, indep_conf :69-73, recent :58-61), fused with
+ * the transform of the new observation the tracker applies first (tracker.py:98-99).
+ *   T      [8] f32 Sim3 data applied to X_new (lietorch act), or NULL for none
+ *   X_new  [HW,3], C_new [HW] f32; X [HW,3], C [HW] f32 updated in place
+ * Bit-exact against the torch expressions on the same (transformed) inputs.
+ */
+int m3s_pointmap_update(int mode, const float* T, const float* X_new, const float* C_new,
+                        float* X, float* C, int64_t HW, void* stream);
+
 /* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
 
 #define M3S_COMM_ID_BYTES 128

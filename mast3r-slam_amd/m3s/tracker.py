@@ -19,6 +19,7 @@ import torch
 import mast3r_slam_backends
 
 from .config import config as _global_config
+from .frame import Frame
 from .geometry import constrain_points_to_ray, get_pixel_coords
 from .global_opt import PoseBatch
 
@@ -97,7 +98,10 @@ class FrameTracker:
         except RuntimeError:
             return False, [], True
         frame.T_WC = T_WCf
-        keyframe.update_pointmap(_act(T_CkCf, Xkf), Ckf)
+        if isinstance(keyframe, Frame):  # the transform fused into the point-map update
+            keyframe.update_pointmap(Xkf, Ckf, T=_data(T_CkCf))
+        else:
+            keyframe.update_pointmap(_act(T_CkCf, Xkf), Ckf)
         n_valid = valid_kf.sum()
         match_frac_k = n_valid / valid_kf.numel()
         unique_frac_f = torch.unique(idx_f2k[valid_match_k[:, 0]]).shape[0] / valid_kf.numel()

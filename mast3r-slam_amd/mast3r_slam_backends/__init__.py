@@ -25,6 +25,7 @@ __all__ = [
     "gauss_newton_calib",
     "track_sim3",
     "CholeskyError",
+    "pointmap_update",
     "library_path",
     "lib",
 ]
@@ -429,6 +430,39 @@ def track_sim3(mode, Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma0, sigma1, huber_k, m
         raise CholeskyError("track_sim3: normal equations not positive definite "
                             f"(iteration {it + 1})")
     return out_f, out_r, it, float(cost.item())
+
+
+# ---------------------------------------------------------------------------------
+# keyframe point-map fusion (extension: frame.py:41-105 runs in torch in the reference)
+# ---------------------------------------------------------------------------------
+
+lib.m3s_pointmap_update.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _c_int64, _vp]
+FILTER_MODES = {"weighted_pointmap": 0, "indep_conf": 1, "recent": 2}
+
+
+def pointmap_update(mode, X, C, X_new, C_new, T=None):
+    """In-place X [HW,3], C [HW,1] <- fuse(X, C, T.act(X_new), C_new) for filtering ``mode``
+    (frame.py:58-77; T: optional Sim3 data [1,8] / [8], tracker.py:98-99)."""
+    if mode not in FILTER_MODES:
+        raise RuntimeError(f"pointmap_update: mode {mode!r} is not a per-point filtering mode")
+    for name, t in (("X", X), ("X_new", X_new)):
+        _check(t, name, torch.float32, 2)
+    for name, t in (("C", C), ("C_new", C_new)):
+        _check(t, name, torch.float32, 2)
+    HW = X.shape[0]
+    if X.shape != (HW, 3) or X_new.shape != (HW, 3) or C.shape != (HW, 1) or C_new.shape != (HW, 1):
+        raise RuntimeError("pointmap_update: expected X, X_new [HW,3] and C, C_new [HW,1]")
+    if T is not None:
+        T = T.reshape(-1)
+        _check(T, "T", torch.float32, 1)
+        if T.numel() != 8:
+            raise RuntimeError("pointmap_update: T must hold 8 floats")
+    dev = _on_device(X=X, C=C, X_new=X_new, C_new=C_new, T=T)
+    with torch.cuda.device(dev):
+        rc = lib.m3s_pointmap_update(FILTER_MODES[mode], _ptr(T), _ptr(X_new), _ptr(C_new), _ptr(X),
+                                     _ptr(C), HW, _stream(dev))
+    _raise(rc, "pointmap_update")
+    return X, C
 
 
 def version() -> str:

@@ -108,3 +108,34 @@ def test_frame_tracker_wrapper(backend):
     Tf, Tr = trk.opt_pose_ray_dist_sim3(_t(g["Xf"]), _t(g["Xk"]), _t(g["T_WCf"]).reshape(1, 8),
                                         _t(g["T_WCk"]).reshape(1, 8), _t(g["Qk"]), _t(g["valid"]))
     np.testing.assert_allclose(Tf.data.cpu().numpy().reshape(8), g["out_T_WCf"], rtol=0, atol=2e-5)
+
+
+def test_track_matched_glue(backend):
+    """tracker.py:28-127 after the network: gating, optimisation, fused keyframe update."""
+    from m3s.config import config
+    from m3s.frame import Frame
+    from m3s.synth import make_tracking_inputs
+    from m3s.tracker import FrameTracker
+
+    hw = (48, 64)
+    p = make_tracking_inputs(hw, seed=6, mode="rays", noise=0.0, device=DEV)
+    n = hw[0] * hw[1]
+    C = torch.full((n, 1), 3.0, device=DEV)
+    kf = Frame(img=torch.zeros(3, *hw), T_WC=p["T_WCk"].clone())
+    kf.update_pointmap(p["Xk"], C)
+    fr = Frame(img=torch.zeros(3, *hw), T_WC=p["T_WCf"].clone())
+    idx = torch.arange(n, device=DEV)[None]
+    valid = torch.ones((1, n, 1), dtype=torch.bool, device=DEV)
+    Q = torch.full((n, 1), 4.0, device=DEV)
+    trk = FrameTracker(device=DEV, cfg=dict(config, use_calib=False))
+    new_kf, out, reloc = trk.track_matched(fr, kf, idx, valid, p["Xf"], C, Q, p["Xf"], C, Q)
+    assert not reloc and len(out) == 6 and kf.N == 2 and not new_kf
+    T = fr.T_WC.data.reshape(8).cpu().numpy()
+    # noise-free: the optimiser lands on the generating pose (within its convergence test)
+    from m3s import synth
+
+    tk = synth.vec_to_sim3(p["T_WCk"].reshape(8).cpu().numpy())
+    tf = synth.vec_to_sim3(T)
+    rel = synth.sim3_compose(synth.sim3_inv(tk), tf)
+    Xk_pred = (rel[2] * (p["Xf"].double().cpu().numpy() @ synth.quat_to_rot(rel[1]).T)) + rel[0]
+    assert np.abs(Xk_pred - p["Xk"].double().cpu().numpy()).max() < 1e-3
