@@ -192,6 +192,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(g, mode, E_und)
+        out["accuracy"] = accuracy(g, mode, Twc0, Twc, cpu_baseline.last_poses,
+                                   cpu_baseline.exact_poses)
     if rank == 0 and world == 1 and not args.no_matching:
         out["matching"] = matching_bench(dev)
         out["tracking"] = tracking_bench(dev)
@@ -300,6 +302,46 @@ def tracking_bench(dev, reps=20):
     return res
 
 
+def accuracy(g, mode, Twc0, Twc_final, T_oracle_1, T_exact_1):
+    """'ATE-RMSE vs ref' (BASELINE.json metric): the GPU op's poses after ONE iteration
+    against the CPU oracle's (the reference backend restated) on the same inputs -- max
+    relative error of the pose data and the Sim(3)-aligned ATE-RMSE of the keyframe positions
+    (m3s.evaluate, evo_ape -as) -- and the ATE of the timed 10-iteration result against the
+    synthetic ground truth."""
+    import numpy as np
+
+    import mast3r_slam_backends as mb
+    from m3s.evaluate import ate_rmse
+
+    T1 = Twc0.clone()
+    if mode == "calib":
+        mb.gauss_newton_calib(T1, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
+                              LOCAL["pixel_border"], LOCAL["depth_eps"], LOCAL["sigma_pixel"],
+                              LOCAL["sigma_depth"], LOCAL["C_conf"], LOCAL["Q_conf"], 1, 0.0)
+    else:
+        mb.gauss_newton_rays(T1, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, LOCAL["sigma_ray"],
+                             LOCAL["sigma_dist"], LOCAL["C_conf"], LOCAL["Q_conf"], 1, 0.0)
+    T1 = T1.cpu().numpy().astype(np.float64)
+    To = np.asarray(T_oracle_1, np.float64)
+    Tx = np.asarray(T_exact_1, np.float64)
+    rel = lambda a, b: float(np.abs(a - b).max() / np.abs(b).max())
+    ts = np.arange(To.shape[0], dtype=np.float64)
+    ate_o, _ = ate_rmse((ts, To[:, :3]), (ts, T1[:, :3]))
+    gt = g.Twc_gt.cpu().numpy().astype(np.float64)
+    fin = Twc_final.cpu().numpy().astype(np.float64)
+    ate_gt, _ = ate_rmse((ts, gt[:, :3]), (ts, fin[:, :3]))
+    ate_init, _ = ate_rmse((ts, gt[:, :3]), (ts, Twc0.cpu().numpy().astype(np.float64)[:, :3]))
+    return {
+        "pose_max_rel_err_vs_oracle_1iter": rel(T1, To),
+        # the same comparison against float terms summed in double: how far each summation
+        # order (this op's, the reference's) is from the exactly summed system
+        "pose_max_rel_err_vs_exact_sum_1iter": rel(T1, Tx),
+        "reference_order_max_rel_err_vs_exact_sum_1iter": rel(To, Tx),
+        "ate_rmse_vs_oracle_1iter_m": ate_o,
+        "ate_rmse_vs_gt_m": {"initial": ate_init, "after_10_iters": ate_gt},
+    }
+
+
 def cpu_baseline(g, mode, E_und):
     """The CPU oracle (restatement of the reference backend) on a bounded sample: ONE GN
     iteration of the same graph (all directed edges, full 512x384), OpenMP threads =
@@ -317,8 +359,11 @@ def cpu_baseline(g, mode, E_und):
                           LOCAL["Q_conf"], max_iter=1, delta_thresh=0.0)
     arrs = [c(g.Twc), c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx), c(g.valid), c(g.Q)]
     t0 = time.perf_counter()
-    O.gauss_newton(P, *arrs)
+    T_o, _, _ = O.gauss_newton(P, *arrs)
     dt = time.perf_counter() - t0
+    cpu_baseline.last_poses = T_o  # the accuracy check compares the GPU's first iteration
+    with O.exact_sums():  # precision reference: the same float terms summed in double
+        cpu_baseline.exact_poses, _, _ = O.gauss_newton(P, *arrs)
     return {
         "value": E_und * 1 / dt,
         "unit": "keyframe-pair GN iters/s",

@@ -469,15 +469,30 @@ void oracle_pose_retr(float* Twc, const float* dx, int64_t N, int num_fix) {
 #define HDIM 105 /* 14*15/2 */
 #define NACC (HDIM + 14)
 
+/* Summation mode.  0 (default): every accumulation is the reference's float addition, in
+ * its order (values are stored in double but are always float-representable, and a float
+ * sum computed in double then rounded to float is the correctly rounded float sum).
+ * 1 ("exact sums", a precision reference for the tests / bench accuracy check, not the
+ * reference's arithmetic): the same float terms summed in double. */
+static int g_exact_sums = 0;
+void oracle_set_exact_sums(int on) { g_exact_sums = on != 0; }
+
+static inline double add_term(double a, float t) {
+    return g_exact_sums ? a + (double)t : (double)((float)a + t);
+}
+static inline double add_acc(double a, double b) {
+    return g_exact_sums ? a + b : (double)((float)a + (float)b);
+}
+
 /* blockReduce + warpReduce (gn_kernels.cu:36-55): 256 -> 128 -> 64 -> 32, then a
  * lock-step warp tree (every lane reads before any lane writes). */
-static float block_reduce(float* s) {
-    for (int t = 0; t < 128; t++) s[t] += s[t + 128];
-    for (int t = 0; t < 64; t++) s[t] += s[t + 64];
-    for (int t = 0; t < 32; t++) s[t] += s[t + 32];
+static double block_reduce(double* s) {
+    for (int t = 0; t < 128; t++) s[t] = add_acc(s[t], s[t + 128]);
+    for (int t = 0; t < 64; t++) s[t] = add_acc(s[t], s[t + 64]);
+    for (int t = 0; t < 32; t++) s[t] = add_acc(s[t], s[t + 32]);
     for (int o = 16; o >= 1; o >>= 1) {
-        float tmp[32];
-        for (int t = 0; t < 32; t++) tmp[t] = s[t] + s[t + o];
+        double tmp[32];
+        for (int t = 0; t < 32; t++) tmp[t] = add_acc(s[t], s[t + o]);
         for (int t = 0; t < 32; t++) s[t] = tmp[t];
     }
     return s[0];
@@ -485,7 +500,7 @@ static float block_reduce(float* s) {
 
 /* Accumulate one residual row: Jx = [Ji, Jj], Ji = -Jj after the adjoint
  * (gn_kernels.cu:999-1013). */
-static inline void accum_row(float* acc, const float* ti, const float* qi, const float* si,
+static inline void accum_row(double* acc, const float* ti, const float* qi, const float* si,
                              float* Jx, float w, float err) {
     float* Ji = &Jx[0];
     float* Jj = &Jx[7];
@@ -494,22 +509,22 @@ static inline void accum_row(float* acc, const float* ti, const float* qi, const
     int l = 0;
     for (int n = 0; n < 14; n++) {
         for (int m = 0; m <= n; m++) {
-            acc[l] += (w * Jx[n]) * Jx[m];
+            acc[l] = add_term(acc[l], (w * Jx[n]) * Jx[m]);
             l++;
         }
     }
-    float* vi = acc + HDIM;
-    float* vj = acc + HDIM + 7;
+    double* vi = acc + HDIM;
+    double* vj = acc + HDIM + 7;
     for (int n = 0; n < 7; n++) {
-        vi[n] += (w * err) * Ji[n];
-        vj[n] += (w * err) * Jj[n];
+        vi[n] = add_term(vi[n], (w * err) * Ji[n]);
+        vj[n] = add_term(vj[n], (w * err) * Jj[n]);
     }
 }
 
 static void align_point(const oracle_gn_params* P, const float* ti, const float* qi, const float* si,
                         const float* tij, const float* qij, const float* sij,
                         const float* Xi, const float* Xj, float q, float ci, float cj,
-                        int valid_match_ind, int64_t ind_Xi, float* acc) {
+                        int valid_match_ind, int64_t ind_Xi, double* acc) {
     float Xj_Ci[3];
     float Jx[14];
     float* Ji = &Jx[0];
@@ -637,15 +652,15 @@ static void align_point(const oracle_gn_params* P, const float* ti, const float*
     }
 }
 
-void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* Xs,
-                     const float* Cs, const int64_t* ii_edge, const int64_t* jj_edge,
-                     const int64_t* idx, const uint8_t* valid, const float* Q,
-                     int64_t N, int64_t HW, int64_t E, float* Hs, float* gs) {
+static void gn_align_impl(const oracle_gn_params* P, const float* Twc, const float* Xs,
+                          const float* Cs, const int64_t* ii_edge, const int64_t* jj_edge,
+                          const int64_t* idx, const uint8_t* valid, const float* Q,
+                          int64_t N, int64_t HW, int64_t E, double* Hs, double* gs) {
     (void)N;
 #pragma omp parallel
     {
-        float* acc = (float*)malloc(sizeof(float) * THREADS * NACC);
-        float* sdata = (float*)malloc(sizeof(float) * THREADS);
+        double* acc = (double*)malloc(sizeof(double) * THREADS * NACC);
+        double* sdata = (double*)malloc(sizeof(double) * THREADS);
 #pragma omp for schedule(dynamic, 1)
         for (int64_t e = 0; e < E; e++) {
             const int64_t ix = ii_edge[e], jx = jj_edge[e];
@@ -655,9 +670,9 @@ void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* X
             float tj[3] = {Tj[0], Tj[1], Tj[2]}, qj[4] = {Tj[3], Tj[4], Tj[5], Tj[6]}, sj[1] = {Tj[7]};
             float tij[3], qij[4], sij[1];
             relSim3(ti, qi, si, tj, qj, sj, tij, qij, sij);
-            memset(acc, 0, sizeof(float) * THREADS * NACC);
+            memset(acc, 0, sizeof(double) * THREADS * NACC);
             for (int t = 0; t < THREADS; t++) {
-                float* a = acc + (int64_t)t * NACC;
+                double* a = acc + (int64_t)t * NACC;
                 for (int64_t k = t; k < HW; k += THREADS) { /* GPU_1D_KERNEL_LOOP (:31-32) */
                     const int64_t pe = e * HW + k;
                     const int vm = valid[pe] != 0;
@@ -671,7 +686,7 @@ void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* X
             /* gs (gn_kernels.cu:1097-1112) */
             for (int n = 0; n < 14; n++) {
                 for (int t = 0; t < THREADS; t++) sdata[t] = acc[(int64_t)t * NACC + HDIM + n];
-                float v = block_reduce(sdata);
+                double v = block_reduce(sdata);
                 if (n < 7) gs[(0 * E + e) * 7 + n] = v;
                 else gs[(1 * E + e) * 7 + (n - 7)] = v;
             }
@@ -680,7 +695,7 @@ void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* X
             for (int n = 0; n < 14; n++) {
                 for (int m = 0; m <= n; m++) {
                     for (int t = 0; t < THREADS; t++) sdata[t] = acc[(int64_t)t * NACC + l];
-                    float v = block_reduce(sdata);
+                    double v = block_reduce(sdata);
                     if (n < 7 && m < 7) {
                         Hs[((0 * E + e) * 7 + n) * 7 + m] = v;
                         Hs[((0 * E + e) * 7 + m) * 7 + n] = v;
@@ -700,13 +715,40 @@ void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* X
     }
 }
 
+void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* Xs,
+                     const float* Cs, const int64_t* ii_edge, const int64_t* jj_edge,
+                     const int64_t* idx, const uint8_t* valid, const float* Q,
+                     int64_t N, int64_t HW, int64_t E, float* Hs, float* gs) {
+    double* Hd = (double*)malloc(sizeof(double) * 4 * E * 49 + 8);
+    double* gd = (double*)malloc(sizeof(double) * 2 * E * 7 + 8);
+    gn_align_impl(P, Twc, Xs, Cs, ii_edge, jj_edge, idx, valid, Q, N, HW, E, Hd, gd);
+    for (int64_t k = 0; k < 4 * E * 49; k++) Hs[k] = (float)Hd[k];
+    for (int64_t k = 0; k < 2 * E * 7; k++) gs[k] = (float)gd[k];
+    free(Hd);
+    free(gd);
+}
+
 /* ------------------------------------------------------------------------ */
 /* SparseBlock assembly + SimplicialLLT semantics (gn_kernels.cu:57-159)    */
 /* ------------------------------------------------------------------------ */
 
+static void gn_assemble_d(const double* Hs, const double* gs, const int64_t* ii_opt,
+                          const int64_t* jj_opt, int64_t N, int64_t E, double* H, double* b);
+
 void oracle_gn_assemble(const float* Hs, const float* gs, const int64_t* ii_opt,
                         const int64_t* jj_opt, int64_t N, int64_t E,
                         double* H, double* b) {
+    double* Hd = (double*)malloc(sizeof(double) * 4 * E * 49 + 8);
+    double* gd = (double*)malloc(sizeof(double) * 2 * E * 7 + 8);
+    for (int64_t k = 0; k < 4 * E * 49; k++) Hd[k] = (double)Hs[k];
+    for (int64_t k = 0; k < 2 * E * 7; k++) gd[k] = (double)gs[k];
+    gn_assemble_d(Hd, gd, ii_opt, jj_opt, N, E, H, b);
+    free(Hd);
+    free(gd);
+}
+
+static void gn_assemble_d(const double* Hs, const double* gs, const int64_t* ii_opt,
+                          const int64_t* jj_opt, int64_t N, int64_t E, double* H, double* b) {
     const int64_t n = 7 * (N - 1);
     memset(H, 0, sizeof(double) * n * n);
     memset(b, 0, sizeof(double) * n);
@@ -717,9 +759,9 @@ void oracle_gn_assemble(const float* Hs, const float* gs, const int64_t* ii_opt,
         for (int64_t e = 0; e < E; e++) {
             const int64_t i = rows[e], j = cols[e];
             if (i >= 0 && j >= 0) {
-                const float* A = Hs + ((int64_t)blk * E + e) * 49;
+                const double* A = Hs + ((int64_t)blk * E + e) * 49;
                 for (int k = 0; k < 7; k++)
-                    for (int l = 0; l < 7; l++) H[(7 * i + k) * n + 7 * j + l] += (double)A[k * 7 + l];
+                    for (int l = 0; l < 7; l++) H[(7 * i + k) * n + 7 * j + l] += A[k * 7 + l];
             }
         }
     }
@@ -729,8 +771,8 @@ void oracle_gn_assemble(const float* Hs, const float* gs, const int64_t* ii_opt,
         for (int64_t e = 0; e < E; e++) {
             const int64_t i = rows[e];
             if (i >= 0) {
-                const float* g = gs + ((int64_t)blk * E + e) * 7;
-                for (int j = 0; j < 7; j++) b[i * 7 + j] += (double)g[j];
+                const double* g = gs + ((int64_t)blk * E + e) * 7;
+                for (int j = 0; j < 7; j++) b[i * 7 + j] += g[j];
             }
         }
     }
@@ -824,15 +866,15 @@ int oracle_gauss_newton(const oracle_gn_params* P, float* Twc, const float* Xs,
         ii_opt[e] = ii_edge[e] - num_fix;
         jj_opt[e] = jj_edge[e] - num_fix;
     }
-    float* Hs = (float*)malloc(sizeof(float) * 4 * E * 49 + 4);
-    float* gs = (float*)malloc(sizeof(float) * 2 * E * 7 + 4);
+    double* Hs = (double*)malloc(sizeof(double) * 4 * E * 49 + 8);
+    double* gs = (double*)malloc(sizeof(double) * 2 * E * 7 + 8);
     double* H = (double*)malloc(sizeof(double) * (n * n + 1));
     double* b = (double*)malloc(sizeof(double) * (n + 1));
     double* x = (double*)malloc(sizeof(double) * (n + 1));
     int itr;
     for (itr = 0; itr < P->max_iter; itr++) {
-        oracle_gn_align(P, Twc, Xs, Cs, ii_edge, jj_edge, idx, valid, Q, N, HW, E, Hs, gs);
-        oracle_gn_assemble(Hs, gs, ii_opt, jj_opt, N, E, H, b);
+        gn_align_impl(P, Twc, Xs, Cs, ii_edge, jj_edge, idx, valid, Q, N, HW, E, Hs, gs);
+        gn_assemble_d(Hs, gs, ii_opt, jj_opt, N, E, H, b);
         oracle_cholesky_solve(H, b, x, n);
         double nrm = 0.0;
         for (int64_t k = 0; k < n; k++) {

@@ -121,6 +121,10 @@ void oracle_apply_sim3_adj_inv(const float* t, const float* q, const float* s,
 
 int oracle_num_threads(void);
 
+/* 1: sum the reference's float terms in double (a precision reference); 0 (default): the
+ * reference's float sums in its order */
+void oracle_set_exact_sums(int on);
+
 #ifdef __cplusplus
 }
 #endif

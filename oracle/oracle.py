@@ -34,6 +34,7 @@ _lib.oracle_f32_to_f16.argtypes = [_f]
 _lib.oracle_f16_to_f32.restype = _f
 _lib.oracle_f16_to_f32.argtypes = [ctypes.c_uint16]
 _lib.oracle_num_threads.restype = _i
+_lib.oracle_set_exact_sums.argtypes = [_i]
 
 
 class GNParams(ctypes.Structure):
@@ -81,6 +82,17 @@ def _p(a):
 
 def num_threads():
     return _lib.oracle_num_threads()
+
+
+class exact_sums:
+    """Context: the GN oracle sums the reference's float terms in double (a precision
+    reference, not the reference's arithmetic)."""
+
+    def __enter__(self):
+        _lib.oracle_set_exact_sums(1)
+
+    def __exit__(self, *a):
+        _lib.oracle_set_exact_sums(0)
 
 
 def f32_to_f16_bits(x: float) -> int:

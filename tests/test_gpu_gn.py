@@ -234,3 +234,24 @@ def test_packed_stream_gives_identical_system(backend, monkeypatch, mode):
     monkeypatch.setenv("M3S_GN_PACK", "2")
     H2, b2 = build_system_gpu(g, mode, LOCAL)
     assert np.array_equal(H0, H2) and np.array_equal(b0, b2)
+
+
+def test_full_size_cfg3_calib_within_1e5_of_exactly_summed_system(backend, oracle):
+    """BASELINE's graph (cfg3: 128 keyframes, 256 pairs, 512x384, calib), one iteration.
+    Summation order matters at this size: the reference's float order (the oracle mirrors
+    it, gn_kernels.cu:31-55) lands ~8e-5 (relative) from the poses obtained when the same
+    float terms are summed in double, so the HIP path (f32 lane partials, f64 across
+    workgroups) is pinned against that exactly summed system at the 1e-5 north-star bar,
+    and must be closer to it than the reference's own order."""
+    g = synth.make_graph("cfg3")
+    from m3s.geometry import constrain_points_to_ray
+
+    g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    T_gpu, _ = _run_gpu(backend, g, "calib", 1)
+    T_ref, _, _ = _run_oracle(oracle, g, "calib", 1)
+    with oracle.exact_sums():
+        T_exact, _, _ = _run_oracle(oracle, g, "calib", 1)
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    assert rel(T_gpu, T_exact) < 1e-5
+    assert rel(T_gpu, T_exact) <= rel(T_ref, T_exact)
+    assert rel(T_gpu, T_ref) < 2e-4  # the reference order's own rounding (see above)
