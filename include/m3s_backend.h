@@ -217,6 +217,21 @@ typedef struct m3s_track_args {
 size_t m3s_track_workspace_bytes(int64_t HW);
 int m3s_track_sim3(const m3s_track_args* args);
 
+/* ---------------- edge construction after matching ---------------- */
+
+/*
+ * edge_confidence -- the per-pixel glue of FactorGraph.add_factors (global_opt.py:53-67) in one
+ * pass over B keyframe pairs:
+ *   Qj = sqrt(Qii[b, idx_i2j] * Qji), Qi = sqrt(Qjj[b, idx_j2i] * Qij)     [B,HW] f32 out
+ *   counts[b] = (#(valid_match_j & Qj > Q_conf), #(valid_match_i & Qi > Q_conf))  [B,2] i32 out
+ *   idx_* [B,HW] i64, valid_match_* [B,HW] u8, Q* [B,HW] f32.  Bit-exact (same f32 ops).
+ */
+int m3s_edge_confidence(const int64_t* idx_i2j, const int64_t* idx_j2i,
+                        const uint8_t* valid_match_j, const uint8_t* valid_match_i,
+                        const float* Qii, const float* Qjj, const float* Qji, const float* Qij,
+                        float Q_conf, int64_t B, int64_t HW, float* Qj, float* Qi, int* counts,
+                        void* stream);
+
 /* ---------------- keyframe point-map fusion ---------------- */
 
 enum { M3S_FILTER_WEIGHTED_POINTMAP = 0, M3S_FILTER_INDEP_CONF = 1, M3S_FILTER_RECENT = 2 };

@@ -112,14 +112,11 @@ class FactorGraph:
     # -- edge construction after the network (global_opt.py:53-99) -------------------
     def add_matched_factors(self, ii, jj, idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qii,
                             Qjj, Qji, Qij, min_match_frac, is_reloc=False):
-        b = idx_i2j.shape[0]
-        bi = torch.arange(b, device=idx_i2j.device)[:, None].expand_as(idx_i2j)
-        Qj = torch.sqrt(Qii[bi, idx_i2j] * Qji)
-        Qi = torch.sqrt(Qjj[bi, idx_j2i] * Qij)
-        valid_j = valid_match_j & (Qj > self.cfg["Q_conf"])
-        valid_i = valid_match_i & (Qi > self.cfg["Q_conf"])
-        frac_j = valid_j.sum(dim=(1, 2)) / (valid_j.shape[1] * valid_j.shape[2])
-        frac_i = valid_i.sum(dim=(1, 2)) / (valid_i.shape[1] * valid_i.shape[2])
+        # Qj/Qi and the per-pair valid counts in one HIP pass (edges.hip; :53-67)
+        Qj, Qi, counts = mast3r_slam_backends.edge_confidence(
+            idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qii, Qjj, Qji, Qij, self.cfg["Q_conf"])
+        frac_j = counts[:, 0] / (valid_match_j.shape[1] * valid_match_j.shape[2])
+        frac_i = counts[:, 1] / (valid_match_i.shape[1] * valid_match_i.shape[2])
 
         ii_t = torch.as_tensor(ii, device=self.device)
         jj_t = torch.as_tensor(jj, device=self.device)

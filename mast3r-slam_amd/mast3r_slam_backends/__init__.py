@@ -26,6 +26,7 @@ __all__ = [
     "track_sim3",
     "CholeskyError",
     "pointmap_update",
+    "edge_confidence",
     "library_path",
     "lib",
 ]
@@ -430,6 +431,42 @@ def track_sim3(mode, Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma0, sigma1, huber_k, m
         raise CholeskyError("track_sim3: normal equations not positive definite "
                             f"(iteration {it + 1})")
     return out_f, out_r, it, float(cost.item())
+
+
+# ---------------------------------------------------------------------------------
+# edge construction after matching (extension: global_opt.py:53-67 runs in torch)
+# ---------------------------------------------------------------------------------
+
+lib.m3s_edge_confidence.argtypes = [_vp] * 8 + [_f, _c_int64, _c_int64, _vp, _vp, _vp, _vp]
+
+
+def edge_confidence(idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qii, Qjj, Qji, Qij, Q_conf):
+    """global_opt.py:53-67 fused: returns (Qj [B,HW,1], Qi [B,HW,1], counts [B,2] int32) with
+    counts = (#valid_j, #valid_i) per pair (the match-fraction numerators)."""
+    _check(idx_i2j, "idx_i2j", torch.int64, 2)
+    _check(idx_j2i, "idx_j2i", torch.int64, 2)
+    B, HW = idx_i2j.shape
+    for name, t in (("valid_match_j", valid_match_j), ("valid_match_i", valid_match_i)):
+        _check(t, name, torch.bool, 3)
+    for name, t in (("Qii", Qii), ("Qjj", Qjj), ("Qji", Qji), ("Qij", Qij)):
+        _check(t, name, torch.float32, 3)
+    for t in (valid_match_j, valid_match_i, Qii, Qjj, Qji, Qij):
+        if t.shape != (B, HW, 1):
+            raise RuntimeError("edge_confidence: expected [B,HW,1] masks / confidences")
+    if idx_j2i.shape != (B, HW):
+        raise RuntimeError("edge_confidence: idx_i2j and idx_j2i differ in shape")
+    dev = _on_device(idx_i2j=idx_i2j, idx_j2i=idx_j2i, valid_match_j=valid_match_j,
+                     valid_match_i=valid_match_i, Qii=Qii, Qjj=Qjj, Qji=Qji, Qij=Qij)
+    Qj = torch.empty((B, HW, 1), dtype=torch.float32, device=dev)
+    Qi = torch.empty((B, HW, 1), dtype=torch.float32, device=dev)
+    counts = torch.empty((B, 2), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.m3s_edge_confidence(_ptr(idx_i2j), _ptr(idx_j2i), _ptr(valid_match_j),
+                                     _ptr(valid_match_i), _ptr(Qii), _ptr(Qjj), _ptr(Qji), _ptr(Qij),
+                                     float(Q_conf), B, HW, _ptr(Qj), _ptr(Qi), _ptr(counts),
+                                     _stream(dev))
+    _raise(rc, "edge_confidence")
+    return Qj, Qi, counts
 
 
 # ---------------------------------------------------------------------------------
