@@ -253,19 +253,32 @@ __device__ __forceinline__ void block_partial(const float* accs, float* __restri
 
 // One pipeline stage of the packed accumulate: the records, Xj and the gathered matched points
 // of 4 consecutive points of one lane.
-template <int MODE>
+template <int MODE, bool RC = false>
 struct AccStage {
     int4 ka, kb;         // {code, sqrt q} x 2 points each
-    float4 xa, xb, xc;   // Xj of the 4 points
+    float4 xa, xb, xc;   // Xj of the 4 points (RC: xa = their depths, xb = tu[u..u+3], xc.x = tv[v])
     float g[4][3];       // gathered matched point (calib: depth only, in g[s][2])
+    const float* rc_tu = nullptr;  // RC: the ray tables (after Zs)
+    const float* rc_tv = nullptr;
+    unsigned rc_m = 0;             // RC: k / W by multiply-shift
+    int rc_sh = 0, rc_w = 1;
 
     // Zi_b: the dense depth array (packed path), or nullptr to read the depth from Xs
     template <int M>
     __device__ __forceinline__ void load(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
                                          const float* __restrict__ Zi_b, int k) {
-        xa = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
-        xb = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
-        xc = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
+        if constexpr (RC) {
+            // Xj_b = the depth row of keyframe j; the ray tables follow Zs (gn_depth_kernel)
+            xa = *reinterpret_cast<const float4*>(Xj_b + k);
+            const unsigned q = (unsigned)(((uint64_t)(unsigned)k * rc_m) >> rc_sh);
+            const int u = k - (int)q * rc_w;
+            xb = *reinterpret_cast<const float4*>(rc_tu + u);
+            xc.x = rc_tv[q];
+        } else {
+            xa = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
+            xb = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
+            xc = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
+        }
         const int ind[4] = {ka.x & 0x7fffffff, ka.z & 0x7fffffff, kb.x & 0x7fffffff, kb.z & 0x7fffffff};
 #pragma unroll
         for (int s = 0; s < 4; s++) {
@@ -285,7 +298,21 @@ struct AccStage {
     __device__ __forceinline__ void compute(const Sim3f& T, const AccParams& P, float* __restrict__ acc) const {
         const int codes[4] = {ka.x, ka.z, kb.x, kb.z};
         const int sqb[4] = {ka.y, ka.w, kb.y, kb.w};
-        const float xj[12] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w, xc.x, xc.y, xc.z, xc.w};
+        float xj[12];
+        if constexpr (RC) {  // x = z * ((u - cx) / fx), y = z * ((v - cy) / fy): constrain_points_to_ray
+            const float z4[4] = {xa.x, xa.y, xa.z, xa.w};
+            const float t4[4] = {xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                xj[3 * s] = z4[s] * t4[s];
+                xj[3 * s + 1] = z4[s] * xc.x;
+                xj[3 * s + 2] = z4[s];
+            }
+        } else {
+            const float t[12] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w, xc.x, xc.y, xc.z, xc.w};
+#pragma unroll
+            for (int q = 0; q < 12; q++) xj[q] = t[q];
+        }
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             PointsIn<float> p;
@@ -435,10 +462,68 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
 
 // Zs[n, k] = Xs[n, k, 2]: the only coordinate of the matched point calib mode reads, as a
 // dense 4-B array so the per-iteration gather touches 4 B per point instead of a 12-B stride.
+// Also the ray tables tu[u] = (u - cx) / fx, tv[v] = (v - cy) / fy (after Zs), and a check that
+// every point IS its pixel's ray times its depth, bit for bit, i.e. what solve_GN_calib's
+// constrain_points_to_ray (global_opt.py:172, geometry.py:37-42/107-123: z * ((u - cx) / fx))
+// produces.  If so (flag kFlagNotRay stays 0) the accumulate reads Xj as its 4-B depth and
+// rebuilds x, y with the same two roundings -- the identical values, so the identical result.
 __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__ Xs, int64_t total,
-                                                       float* __restrict__ Zs) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256)
-        Zs[i] = Xs[i * 3 + 2];
+                                                       float* __restrict__ Zs, AccParams P,
+                                                       int* __restrict__ flags) {
+    float* __restrict__ tu = Zs + total;
+    float* __restrict__ tv = tu + P.width;
+    const int n = blockIdx.y;  // keyframe row
+    const int t0 = blockIdx.x * 256 + threadIdx.x;
+    if (n == 0 && t0 < P.width) tu[t0] = ((float)t0 - P.cx) / P.fx;
+    if (n == 0 && t0 < P.height) tv[t0] = ((float)t0 - P.cy) / P.fy;
+    const float* __restrict__ Xn = Xs + (int64_t)n * P.HW * 3;
+    float* __restrict__ Zn = Zs + (int64_t)n * P.HW;
+    bool ray = true;
+    for (int k = t0; k < P.HW; k += gridDim.x * 256) {
+        const float x = Xn[(int64_t)k * 3], y = Xn[(int64_t)k * 3 + 1], z = Xn[(int64_t)k * 3 + 2];
+        Zn[k] = z;
+        float u, v;
+        pixel_of(k, P, u, v);
+        const float xr = z * ((u - P.cx) / P.fx);
+        const float yr = z * ((v - P.cy) / P.fy);
+        ray = ray && __float_as_uint(xr) == __float_as_uint(x) && __float_as_uint(yr) == __float_as_uint(y);
+    }
+    if (!ray) flags[kFlagNotRay] = 1;  // benign race: every writer stores 1
+}
+
+// One lane's steps of the packed accumulate (4 points per step); the records of the next step
+// are loaded one step ahead.  RC: Xj_b is keyframe j's depth row and x, y come from the ray
+// tables that follow Zs (total = N * HW floats of depth).
+template <int MODE, bool RC>
+__device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
+                                            const float* __restrict__ Zi_b, const int4* __restrict__ pk_b,
+                                            int k0, int k1, const Sim3f& T, const AccParams& P,
+                                            const float* __restrict__ Zs, float* __restrict__ acc) {
+    constexpr int S = 4 * kAccThreads;
+    AccStage<MODE, RC> cur;
+    if constexpr (RC) {
+        cur.rc_tu = Zs + (int64_t)P.nkf * P.HW;
+        cur.rc_tv = cur.rc_tu + P.width;
+        cur.rc_m = P.div_m;
+        cur.rc_sh = P.div_sh;
+        cur.rc_w = P.width;
+    }
+    int4 na = int4{0, 0, 0, 0}, nb = int4{0, 0, 0, 0};
+    int k = k0 + 4 * threadIdx.x;
+    if (k < k1) {
+        na = pk_b[k / 2];
+        nb = pk_b[k / 2 + 1];
+    }
+    for (; k < k1; k += S) {
+        cur.ka = na;
+        cur.kb = nb;
+        if (k + S < k1) {
+            na = pk_b[(k + S) / 2];
+            nb = pk_b[(k + S) / 2 + 1];
+        }
+        cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
+        cur.template compute<MODE>(T, P, acc);
+    }
 }
 
 // Per-iteration accumulate over the packed stream: 8 B {code, sqrt q} + Xj 12 B + the gather
@@ -475,7 +560,6 @@ void gn_accum_packed_kernel(
     const int4* __restrict__ pk_b = pack + ebase / 2;
     const int k0 = c * P.chunk;
     const int k1 = min(k0 + P.chunk, HW);
-    const int tid = threadIdx.x;
 
     float acc[kNacc];
 #pragma unroll
@@ -484,8 +568,9 @@ void gn_accum_packed_kernel(
     // ahead, so a step waits for one memory round trip (its gathers + Xj) instead of two
     // (records, then the gathers they index).  A deeper pipeline (gathers of the next step
     // in flight too) needs ~180 VGPRs, drops to 2 waves/SIMD and measured 8 % slower.
-    constexpr int S = 4 * kAccThreads;
 #if M3S_ACC_PIPE == 2
+    const int tid = threadIdx.x;
+    constexpr int S = 4 * kAccThreads;
     // two-deep: the gathers + Xj of step s+1 and the records of step s+2 are in flight while
     // step s is computed
     AccStage<MODE> cur, nxt;
@@ -512,23 +597,11 @@ void gn_accum_packed_kernel(
         nxt.kb = pb2;
     }
 #else
-    AccStage<MODE> cur;
-    int4 na = int4{0, 0, 0, 0}, nb = int4{0, 0, 0, 0};
-    int k = k0 + 4 * tid;
-    if (k < k1) {
-        na = pk_b[k / 2];
-        nb = pk_b[k / 2 + 1];
-    }
-    for (; k < k1; k += S) {
-        cur.ka = na;
-        cur.kb = nb;
-        if (k + S < k1) {
-            na = pk_b[(k + S) / 2];
-            nb = pk_b[(k + S) / 2 + 1];
-        }
-        cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
-        cur.template compute<MODE>(T, P, acc);
-    }
+    // calib with ray-constrained keyframe points (gn_depth_kernel's check): Xj from its depth
+    if (MODE == GN_CALIB && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
+        accum_steps<MODE, true>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
+    else
+        accum_steps<MODE, false>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
 #endif
     block_partial(acc, partials + ((int64_t)e * P.nchunks + c) * kNaccPad);
 }
@@ -562,8 +635,11 @@ hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, 
     }
     if (Zs) {
         const int64_t total = N * (int64_t)P.HW;
-        const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
-        hipLaunchKernelGGL(gn_depth_kernel, dim3(blocks), dim3(256), 0, st, Xs, total, Zs);
+        const int bx = (int)std::max<int64_t>(std::min<int64_t>((P.HW + 255) / 256,
+                                                                std::max<int64_t>(8192 / std::max<int64_t>(N, 1), 2)),
+                                              (std::max(P.width, P.height) + 255) / 256);
+        hipLaunchKernelGGL(gn_depth_kernel, dim3(bx, (unsigned)N), dim3(256), 0, st, Xs, total, Zs, P,
+                           const_cast<int*>(flags));
     }
     return hipGetLastError();
 }

@@ -179,7 +179,8 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
     L.pack = take(8 * (size_t)E_local * (size_t)HW);
-    L.zs = take(mode == M3S_GN_CALIB ? sizeof(float) * (size_t)N * (size_t)HW : 0);
+    // + the ray tables tu[W], tv[H] (gn_depth_kernel); HW floats is an upper bound for W + H
+    L.zs = take(mode == M3S_GN_CALIB ? sizeof(float) * ((size_t)N + 1) * (size_t)HW + 64 : 0);
     L.total = off;
     return L;
 }
@@ -691,6 +692,11 @@ int setup(const m3s_gn_args& a, Ctx& c) {
         char* h = g_stage_ws.get(hi - lo + sizeof(int) * nslot);
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
         std::memset(h, 0, L.ii_loc - lo);  // flags
+        // M3S_GN_RAYCHECK=1: let the packed calib accumulate take the ray-constrained path
+        // (Xj read as its depth, 16 instead of 24 B per point-edge) when every point passes the
+        // check.  Off by default: bitwise the same result, but only ~3 % faster on cfg3 -- the
+        // kernel is latency-bound, not HBM-bound.
+        if (env_int("M3S_GN_RAYCHECK", 0) == 0) reinterpret_cast<int*>(h)[kFlagNotRay] = 1;
         auto put = [&](size_t off, const std::vector<int>& v) {
             if (!v.empty()) std::memcpy(h + (off - lo), v.data(), sizeof(int) * v.size());
         };
@@ -735,6 +741,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     P.HW = (int)a.HW;
     P.chunk = chunk_points(a.HW, L.nchunks);
     P.nchunks = L.nchunks;
+    P.nkf = (int)a.N;
     auto al16 = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
     c.vec = (a.HW % 4 == 0) && al16(a.Xs) && al16(a.Cs) && al16(a.idx) && al16(a.valid) &&
             al16(a.Q);
@@ -964,6 +971,13 @@ int run(const m3s_gn_args& a) {
         g_prof.mark(c.st);
     }
     if (c.sp.dbuf) M3S_HIP_CHECK(hipFreeAsync(c.sp.dbuf, c.st));
+    if (env_int("M3S_GN_DEBUG_FLAGS", 0)) {  // diagnostics: the device flags after the call
+        int hf[kNumFlags];
+        M3S_HIP_CHECK(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c.st));
+        M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+        fprintf(stderr, "gn flags: done %d fail %d not_ray %d packed %d\n", hf[kFlagDone], hf[kFlagFail],
+                hf[kFlagNotRay], (int)c.packed);
+    }
     return M3S_OK;
 }
 

@@ -17,6 +17,7 @@ constexpr int kCholTile = 64;  // dense Cholesky tile
 
 constexpr int kFlagDone = 0;   // set once ||dx|| < delta_thresh (skips later iterations)
 constexpr int kFlagFail = 1;   // set by the factorisation when a pivot <= 0
+constexpr int kFlagNotRay = 2; // calib: some Xs point is not its pixel's ray times its depth
 constexpr int kNumFlags = 16;
 
 // Upper-triangle packing of a symmetric 7x7 block: index of (a,b), a <= b.
@@ -36,6 +37,7 @@ struct AccParams {
     int HW;
     int chunk;    // points per workgroup (multiple of 4)
     int nchunks;  // chunks per directed edge
+    int nkf;      // keyframes (rows of Xs / Zs)
 };
 
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,

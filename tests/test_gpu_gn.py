@@ -255,3 +255,29 @@ def test_full_size_cfg3_calib_within_1e5_of_exactly_summed_system(backend, oracl
     assert rel(T_gpu, T_exact) < 1e-5
     assert rel(T_gpu, T_exact) <= rel(T_ref, T_exact)
     assert rel(T_gpu, T_ref) < 2e-4  # the reference order's own rounding (see above)
+
+
+@pytest.mark.parametrize("iters", [3, 6])
+def test_ray_constrained_calib_path_is_identical(backend, oracle, monkeypatch, iters):
+    """solve_GN_calib hands the op ray-constrained points (global_opt.py:172); the packed calib
+    accumulate then reads Xj as its depth and rebuilds x, y with the same roundings
+    (gn_depth_kernel checks every point bit for bit).  The result must be bitwise the same as
+    with the check disabled, and the path must not be taken for unconstrained points."""
+    from m3s.geometry import constrain_points_to_ray
+
+    g = synth.make_graph("cfg2", H=96, W=128, mode="calib")
+    g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "1")
+    T_rc, _ = _run_gpu(backend, g, "calib", iters)
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "0")
+    T_gen, _ = _run_gpu(backend, g, "calib", iters)
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "1")
+    assert np.array_equal(T_rc, T_gen)
+    T_o, _, _ = _run_oracle(oracle, g, "calib", iters)
+    assert np.abs(T_rc - T_o).max() / np.abs(T_o).max() < 1e-5
+    # one point off its ray: the check must fall back (result == generic path on those inputs)
+    g.Xs[5, 77, 0] = torch.nextafter(g.Xs[5, 77, 0], torch.tensor(1e9))
+    T_fb, _ = _run_gpu(backend, g, "calib", iters)
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "0")
+    T_fb_gen, _ = _run_gpu(backend, g, "calib", iters)
+    assert np.array_equal(T_fb, T_fb_gen)
