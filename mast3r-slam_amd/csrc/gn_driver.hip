@@ -352,16 +352,23 @@ struct SparsePlan {
     bool enabled = false;
     bool fused = false;       // the whole solve in one gn_solve launch (else multi-launch)
     bool fused_tail = false;  // the dense tail fits the in-register factorisation of gn_solve
+    bool hybrid = false;      // multi-launch rounds, then gn_solve's core + back-substitution
     int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
     std::vector<SpRound> rounds;
     std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
+    // multi-launch rounds (sp_round_kernel), per contribution: (v, code_r, code_s) for block
+    // targets, (v, code_r, W id, owner node | -1) for RHS targets; code = block * 2 + transposed
+    std::vector<int> tc3, rc4;
     // device (one stream-ordered allocation per call)
     char* dbuf = nullptr;
     // block-format system: b (npose x 7, padded to bpad doubles), then 49-f64 blocks
     int bpad = 0;
     size_t o_sys = 0, o_y = 0, o_L = 0, o_W = 0, o_xd = 0, o_Lg = 0, o_int = 0;
+    // the plan integers, one array: [nodes fptr fronts tail tmap rounds] (nints_back: what the
+    // core + back-substitution launch stages in LDS) [tg tc rtg rc] (nints: the whole plan of
+    // the single-workgroup solve) [tc3 rc4] (multi-launch rounds only)
     size_t i_nodes = 0, i_fptr = 0, i_fronts = 0, i_tg = 0, i_tc = 0, i_rtg = 0, i_rc = 0,
-           i_tail = 0, i_tmap = 0, i_rounds = 0, nints = 0;
+           i_tail = 0, i_tmap = 0, i_rounds = 0, i_tc3 = 0, i_rc4 = 0, nints = 0, nints_back = 0;
     template <typename T>
     T* dptr(size_t off) const { return reinterpret_cast<T*>(dbuf + off); }
     const int* iptr(size_t i) const { return reinterpret_cast<const int*>(dbuf + o_int) + i; }
@@ -395,6 +402,14 @@ RoundPolicy fused_policy() {
 RoundPolicy multi_policy() {
     return {false, env_int("M3S_MULTI_DCAP", 16), env_int("M3S_MULTI_RMIN", 2),
             env_int("M3S_MULTI_RMAX", 64), 0, 0, env_int("M3S_MULTI_MMD", 0) != 0};
+}
+// hybrid: multi-launch rounds in minimum-degree order down to a core that fits the in-register
+// factorisation of gn_solve (which then also back-substitutes and retracts)
+RoundPolicy hybrid_policy() {
+    return {false, env_int("M3S_HYB_DCAP", 64), env_int("M3S_HYB_RMIN", 1),
+            env_int("M3S_HYB_RMAX", 64),
+            std::min(kTailPoseMax, env_int("M3S_HYB_TAILCAP", kTailPoseMax)),
+            env_int("M3S_HYB_KMIN", 4), env_int("M3S_HYB_MMD", 1) != 0};
 }
 
 void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparsePlan& sp) {
@@ -443,10 +458,10 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
     std::vector<char> alive(npose, 1), blocked(npose, 0);
     int nalive = npose;
     sp.fptr.assign(1, 0);
-    std::vector<int> cand, chosen, nb;
+    std::vector<int> cand, chosen, nb, codes;
     std::vector<std::vector<int>> F;
-    struct TC { int r, s, q, wx, wy; };
-    struct RC { int r, q, w; };
+    struct TC { int r, s, q, wx, wy, v, cr, cs; };
+    struct RC { int r, q, w, v, cr, owner; };
     std::vector<TC> tcs;
     std::vector<RC> rcs;
     for (int round = 0; round < rmax && nalive > 0; round++) {
@@ -501,18 +516,26 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
         for (size_t q = 0; q < chosen.size(); q++) {
             const int v = chosen[q];
             neighbours(v, F[q]);
+            const int node = (int)sp.nodes.size();
             sp.nodes.push_back(v);
             const int w0 = sp.nW;
+            codes.clear();
             for (int r : F[q]) {
                 const int blk = block_of(r, v);
                 sp.fronts.insert(sp.fronts.end(), {r, blk, r > v ? 1 : 0, sp.nW++});
+                codes.push_back(2 * blk + (r > v ? 1 : 0));
             }
             sp.fptr.push_back((int)sp.fronts.size() / 4);
             for (size_t i = 0; i < F[q].size(); i++) {
                 for (size_t j = i; j < F[q].size(); j++)
-                    tcs.push_back({F[q][i], F[q][j], (int)q, w0 + (int)i, w0 + (int)j});
-                rcs.push_back({F[q][i], pol.fused ? (int)q : v, w0 + (int)i});
+                    tcs.push_back({F[q][i], F[q][j], (int)q, w0 + (int)i, w0 + (int)j, v, codes[i],
+                                   codes[j]});
+                rcs.push_back({F[q][i], pol.fused ? (int)q : v, w0 + (int)i, v, codes[i],
+                               i == 0 ? node : -1});
             }
+            // multi-launch rounds: a pose without fronts (its neighbours pinned or eliminated)
+            // still needs L_v and y_v for the back-substitution -- a contribution to no target
+            if (!pol.fused && F[q].empty()) rcs.push_back({-1, v, -1, v, 2 * v, node});
         }
         // targets in (r, s) order, contributions in pose order (deterministic sums)
         std::sort(tcs.begin(), tcs.end(), [](const TC& x, const TC& y) {
@@ -525,6 +548,7 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
             const int c0 = (int)sp.tc.size() / 2;
             while (e < tcs.size() && tcs[e].r == tcs[k].r && tcs[e].s == tcs[k].s) {
                 sp.tc.insert(sp.tc.end(), {tcs[e].wx, tcs[e].wy});
+                if (!pol.fused) sp.tc3.insert(sp.tc3.end(), {tcs[e].v, tcs[e].cr, tcs[e].cs});
                 e++;
             }
             sp.tg.insert(sp.tg.end(), {block_of(tcs[k].r, tcs[k].s), c0, (int)sp.tc.size() / 2});
@@ -537,6 +561,8 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
             const int c0 = (int)sp.rc.size() / 2;
             while (e < rcs.size() && rcs[e].r == rcs[k].r) {
                 sp.rc.insert(sp.rc.end(), {rcs[e].w, rcs[e].q});  // (W id, node slot | pose)
+                if (!pol.fused)
+                    sp.rc4.insert(sp.rc4.end(), {rcs[e].v, rcs[e].cr, rcs[e].w, rcs[e].owner});
                 e++;
             }
             sp.rtg.insert(sp.rtg.end(), {rcs[k].r, c0, (int)sp.rc.size() / 2});
@@ -578,8 +604,9 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
         }
     sp.fused_tail = sp.ntail * 7 <= kTailMax;
     sp.fused = pol.fused && sp.fused_tail;
-    sp.nints = sp.nodes.size() + sp.fptr.size() + sp.fronts.size() + sp.tg.size() + sp.tc.size() +
-               sp.rtg.size() + sp.rc.size() + sp.tail.size() + sp.tmap.size() + 8 * sp.rounds.size();
+    sp.nints_back = sp.nodes.size() + sp.fptr.size() + sp.fronts.size() + sp.tail.size() +
+                    sp.tmap.size() + 8 * sp.rounds.size();
+    sp.nints = sp.nints_back + sp.tg.size() + sp.tc.size() + sp.rtg.size() + sp.rc.size();
     sp.enabled = true;
 }
 
@@ -597,19 +624,21 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     sp.o_W = take(sizeof(double) * 49 * (size_t)sp.nW);
     sp.o_xd = take(sizeof(double) * (size_t)std::max(sp.npad_tail, 1));
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
-    // the plan integers in one array: [nodes fptr fronts tg tc rtg rc tail tmap rounds]
-    std::vector<const std::vector<int>*> parts = {&sp.nodes, &sp.fptr, &sp.fronts, &sp.tg, &sp.tc,
-                                                  &sp.rtg, &sp.rc, &sp.tail, &sp.tmap};
-    size_t* offs[] = {&sp.i_nodes, &sp.i_fptr, &sp.i_fronts, &sp.i_tg, &sp.i_tc,
-                      &sp.i_rtg, &sp.i_rc, &sp.i_tail, &sp.i_tmap};
+    // the plan integers in one array (layout: SparsePlan), the rounds after tmap
+    std::vector<const std::vector<int>*> parts = {&sp.nodes, &sp.fptr, &sp.fronts, &sp.tail,
+                                                  &sp.tmap, &sp.tg, &sp.tc, &sp.rtg, &sp.rc,
+                                                  &sp.tc3, &sp.rc4};
+    size_t* offs[] = {&sp.i_nodes, &sp.i_fptr, &sp.i_fronts, &sp.i_tail, &sp.i_tmap, &sp.i_tg,
+                      &sp.i_tc, &sp.i_rtg, &sp.i_rc, &sp.i_tc3, &sp.i_rc4};
     size_t n = 0;
     for (size_t k = 0; k < parts.size(); k++) {
+        if (k == 5) {
+            sp.i_rounds = n;
+            n += 8 * sp.rounds.size();
+        }
         *offs[k] = n;
         n += parts[k]->size();
     }
-    sp.i_rounds = n;
-    n += 8 * sp.rounds.size();
-    sp.nints = n;
     sp.o_int = take(sizeof(int) * std::max<size_t>(n, 1));
     M3S_HIP_CHECK(hipMallocAsync((void**)&sp.dbuf, off, st));
     if (n > 0) {
@@ -784,8 +813,8 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
                                          a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
     }
     const int npose = (int)(a.N - 1);
-    if (c.sp.enabled && c.sp.fused) {
-        // block format for the single-workgroup solve, in the solver's buffer
+    if (c.sp.enabled) {
+        // block format for the sparse solves, in the solver's buffer
         SparsePlan& sp = c.sp;
         double* sys = sp.dptr<double>(sp.o_sys);
         M3S_HIP_CHECK(launch_assemble(c.st, c.at<double>(L.edgeblk), c.at<int>(L.blk_ptr),
@@ -896,14 +925,19 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     double* Ls = S.Lstore;
     double* W = S.W;
     double* x = S.x;
-    M3S_HIP_CHECK(launch_sp_init(c.st, c.at<double>(L.compact), c.plan.nblk, sp.nblocks, npose, A, b,
-                                 flags));
-    for (const SpRound& R : sp.rounds) {
-        M3S_HIP_CHECK(launch_sp_factor(c.st, R.nnodes, sp.iptr(sp.i_nodes), sp.iptr(sp.i_fptr),
-                                       sp.iptr(sp.i_fronts), R.node_begin, A, b, Ls, W, y, flags));
-        M3S_HIP_CHECK(launch_sp_schur(c.st, sp.iptr(sp.i_tg), sp.iptr(sp.i_tc), R.tbeg, R.nbt,
-                                      sp.iptr(sp.i_rtg), sp.iptr(sp.i_rc), R.rbeg, R.nrt, W, y, A, b,
-                                      flags));
+    for (const SpRound& R : sp.rounds)
+        M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_tg), sp.iptr(sp.i_tc3), R.tbeg, R.nbt,
+                                      sp.iptr(sp.i_rtg), sp.iptr(sp.i_rc4), R.rbeg, R.nrt, A, b, Ls,
+                                      W, y, flags));
+    if (sp.hybrid) {
+        // the <= 27-pose core in registers, the back-substitution through the rounds and the
+        // retraction: one single-workgroup launch (gn_solve.hip) reading the plan prefix
+        S.nmeta = (int)sp.nints_back;
+        S.meta_lds = 1;
+        S.do_fwd = 0;
+        S.do_tail = S.do_back = 1;
+        M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+        return M3S_OK;
     }
     M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
                                  sp.npad_tail, c.at<double>(L.dense), c.at<double>(L.linv),
@@ -947,7 +981,17 @@ int run(const m3s_gn_args& a) {
         if (env_int("M3S_SOLVE_DEBUG", 0) && !fused_ok)
             fprintf(stderr, "fused solve rejected: fused_tail %d (ntail %d) rounds %zu nints %zu meta_fits %d\n",
                     (int)c.sp.fused, c.sp.ntail, c.sp.rounds.size(), c.sp.nints, (int)meta_fits);
-        if (!fused_ok) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
+        if (!fused_ok) {
+            // M3S_SOLVER=3 / default: multi-launch rounds + the in-register core when it fits
+            bool hyb = false;
+            if (choice == 3 || (choice == 0 && env_int("M3S_HYBRID", 1) != 0)) {
+                build_sparse_plan(c.plan, npose, hybrid_policy(), c.sp);
+                hyb = c.sp.fused_tail && npose <= solve_max_poses() &&
+                      solve_lds_bytes((int)c.sp.nints_back) <= (size_t)kSolveMaxLds;
+            }
+            if (!hyb) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
+            c.sp.hybrid = hyb;
+        }
         t2 = now();
         rc = upload_sparse_plan(c.sp, npose, c.st);
         if (rc) return rc;
@@ -965,7 +1009,7 @@ int run(const m3s_gn_args& a) {
         rc = enqueue_solve(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
-        if (!c.sp.fused)  // the single-workgroup solve retracts inside its launch
+        if (!c.sp.fused && !c.sp.hybrid)  // gn_solve retracts inside its launch
             M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
                                          a.delta_thresh, flags));
         g_prof.mark(c.st);

@@ -67,15 +67,10 @@ hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotma
 constexpr int kMaxNpad = 8192;  // dense solve limit: N <= 1171 keyframes
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
                                      double* x, int* flags);
-// multi-launch block-sparse elimination (gn_sparse.hip)
-hipError_t launch_sp_init(hipStream_t st, const double* compact, int nblk, int nblocks, int npose,
-                          double* A, double* b, const int* flags);
-hipError_t launch_sp_factor(hipStream_t st, int nnodes, const int* nodes, const int* fptr,
-                            const int* fronts, int node_begin, const double* A, const double* b,
-                            double* Lstore, double* W, double* y, int* flags);
-hipError_t launch_sp_schur(hipStream_t st, const int* tg, const int* tc, int tbeg, int nbt,
-                           const int* rtg, const int* rc, int rbeg, int nrt, const double* W,
-                           const double* y, double* A, double* b, const int* flags);
+// multi-launch block-sparse elimination (gn_sparse.hip): one launch per round
+hipError_t launch_sp_round(hipStream_t st, const int* tg, const int* tc3, int tbeg, int nbt,
+                           const int* rtg, const int* rc4, int rbeg, int nrt, double* A, double* b,
+                           double* Lstore, double* W, double* y, int* flags);
 hipError_t launch_sp_back(hipStream_t st, int nnodes, const int* nodes, const int* fptr,
                           const int* fronts, int node_begin, const double* Lstore, const double* W,
                           const double* y, double* x, const int* flags);

@@ -1,200 +1,181 @@
 // gn_sparse.hip -- the multi-launch block-sparse solve of the pose-graph normal equations.
 //
-// The GN system is a graph Laplacian with 7x7 blocks: one block row per non-pinned pose,
-// a block per co-observing pose pair.  The driver (gn_driver.hip, build_sparse_plan) picks,
-// round by round, an independent set of low-degree poses; a round eliminates all of them at
-// once (they do not touch each other), one workgroup per pose:
-//   sp_factor : L_v = chol(A_vv) (7x7), Li_v = L_v^{-1}, W_rv = A_rv Li_v^T for every front
-//               pose r (the L blocks), y_v = Li_v b_v                    (the forward solve)
-//   sp_schur  : A_rs -= sum_v W_rv W_sv^T, b_r -= sum_v W_rv y_v over the round, each target
-//               summed by one workgroup over a host-ordered contribution list (deterministic)
-// The poses left after the rounds (a dense-ish core) are moved into the dense f64 matrix of
-// the tiled Cholesky (gn_kernels.hip, sp_tail_*); then sp_back runs the rounds in reverse:
-//   x_v = Li_v^T (y_v - sum_r W_rv^T x_r).
-// This path serves graphs whose elimination needs many rounds (many workgroups per round hide
-// the memory latency); small graphs run the single-workgroup solve of gn_solve.hip instead.
-// Failure semantics follow SimplicialLLT (gn_kernels.cu:142-150): a pivot <= 0 sets the
-// failure flag and the update becomes zero.
+// The GN system is a graph Laplacian with 7x7 blocks, in the block format of
+// gn_assemble_kernel: b (npose x 7), then one 49-f64 row-major block per pose and per
+// co-observing pose pair (block (x, y), x < y, holds the rows of pose x; fill blocks zeroed).
+// The driver (gn_driver.hip, build_sparse_plan) picks, round by round, an independent set V of
+// low-degree poses.  A round eliminates all of V in ONE launch, one workgroup per target:
+//   block target (r, s):  A_rs -= sum_{v in V} W_rv W_sv^T
+//   RHS target r:         b_r  -= sum_{v in V} W_rv y_v
+// with L_v L_v^T = A_vv, W_rv = A_rv L_v^-T, y_v = L_v^-1 b_v.  A workgroup recomputes the W
+// rows it needs (a 7-lane group per contribution factors A_vv in registers; lane ra
+// forward-substitutes row ra of A_rv) rather than reading them from a preceding factor launch:
+// a dependent launch costs more than the redundant 7x7 factors.  The RHS target r is the only
+// writer of W_rv, and the contribution through v's first front stores L_v and y_v: both are
+// kept for the back-substitution.
+// The poses left after the rounds are factored either by the in-register core of gn_solve.hip
+// (<= 27 poses; that launch also runs the back-substitution through the rounds and the
+// retraction) or by the tiled dense Cholesky of gn_kernels.hip (sp_tail_*), after which
+// sp_back runs the rounds in reverse: x_v = L_v^-T (y_v - sum_r W_rv^T x_r).
+// Each kernel issues its independent loads before it waits (the device flag with the plan
+// integers, then the blocks): a dependent global round trip is the unit of cost here.
+// Failure semantics follow SimplicialLLT (reference gn_kernels.cu:142-150): a pivot <= 0 sets
+// the failure flag and the update becomes zero.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
+#include "block7.h"
 #include "gn_kernels.h"
 
 namespace m3s {
 
 namespace {
-__host__ __device__ constexpr int symi(int a, int b) { return a * 7 - a * (a - 1) / 2 + (b - a); }
+constexpr int kGroups = 9;  // 7-lane groups per 64-lane workgroup (lane 63 idle)
+constexpr int kLd = 8;      // LDS row stride (doubles) of a staged 7x7 block
 }  // namespace
 
-// A blocks (49 f64, row-major, block (x,y) stores rows of pose x, x < y) from the compact
-// system; fill blocks are zeroed; b from the compact gradient.
-__global__ __launch_bounds__(64) void sp_init_kernel(const double* __restrict__ compact, int nblk,
-                                                     int nblocks, int npose,
-                                                     double* __restrict__ A,
-                                                     double* __restrict__ b,
-                                                     const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
-    const int s = blockIdx.x, t = threadIdx.x;
-    if (s < nblocks) {
-        if (t < 49) {
-            const int a = t / 7, c = t % 7;
-            A[(int64_t)s * 49 + t] =
-                s < nblk ? compact[(int64_t)s * 28 + (a <= c ? symi(a, c) : symi(c, a))] : 0.0;
-        }
-    } else {
-        for (int i = t; i < npose * 7; i += 64) b[i] = compact[(int64_t)nblk * 28 + i];
-    }
-}
-
-// One workgroup per eliminated pose.  fronts: 4 ints per entry (r, block, transposed, W id).
-__global__ __launch_bounds__(64) void sp_factor_kernel(
-    const int* __restrict__ nodes, const int* __restrict__ fptr, const int* __restrict__ fronts,
-    int node_begin, const double* __restrict__ A, const double* __restrict__ b,
-    double* __restrict__ Lstore, double* __restrict__ W, double* __restrict__ y,
-    int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
-    __shared__ double Li[49];
-    __shared__ double yv[7];
-    const int q = node_begin + blockIdx.x;
-    const int v = nodes[q];
-    const int t = threadIdx.x;
-    if (t == 0) {
-        double D[7][7], L[7][7], M[7][7];
-#pragma unroll
-        for (int i = 0; i < 7; i++)
-#pragma unroll
-            for (int j = 0; j < 7; j++) D[i][j] = A[(int64_t)v * 49 + i * 7 + j];
-        bool bad = false;
-#pragma unroll
-        for (int p = 0; p < 7; p++) {
-            double d = D[p][p];
-#pragma unroll
-            for (int k = 0; k < p; k++) d -= L[p][k] * L[p][k];
-            if (d <= 0.0) bad = true;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
-            L[p][p] = sqrt(d);
-            const double inv = 1.0 / L[p][p];
-#pragma unroll
-            for (int i = p + 1; i < 7; i++) {
-                double s = D[i][p];
-#pragma unroll
-                for (int k = 0; k < p; k++) s -= L[i][k] * L[p][k];
-                L[i][p] = s * inv;
+// Round targets: tg = (block, begin, end) with contributions tc3 = (v, code_r, code_s);
+// rtg = (pose r | -1, begin, end) with rc4 = (v, code_r, W id | -1, owner node | -1), where
+// code = block * 2 + transposed (the block holds the rows of the other pose).  r = -1 collects
+// the poses without fronts: only their L and y are stored.
+__global__ __launch_bounds__(64) void sp_round_kernel(
+    const int* __restrict__ tg, const int* __restrict__ tc3, int tbeg, int nbt,
+    const int* __restrict__ rtg, const int* __restrict__ rc4, int rbeg, double* __restrict__ A,
+    double* __restrict__ b, double* __restrict__ Lstore, double* __restrict__ W,
+    double* __restrict__ y, int* __restrict__ flags) {
+    __shared__ double sR[kGroups][7 * kLd];  // rows of W_rv, per contribution of the batch
+    __shared__ double sS[kGroups][7 * kLd];  // block target: rows of W_sv; RHS target: y_v
+    const int done = flags[kFlagDone];
+    const int gi = blockIdx.x, lane = threadIdx.x;
+    const bool blk = gi < nbt;
+    const int* T_ = blk ? tg + 3 * (tbeg + gi) : rtg + 3 * (rbeg + gi - nbt);
+    const int tgt = T_[0], c0 = T_[1], c1 = T_[2];
+    if (done) return;
+    const int g = lane / 7, ra = lane - 7 * g;
+    // this lane's output: entry (er, ec) of the block, or row er of the RHS
+    const int nact = tgt < 0 ? 0 : (blk ? 49 : 7);
+    const int er = blk ? lane / 7 : lane, ec = lane % 7;
+    double* dst = blk ? A + (int64_t)tgt * 49 + lane : b + (int64_t)tgt * 7 + lane;
+    const double d0 = lane < nact ? *dst : 0.0;
+    double acc = 0.0;
+    bool bad = false;
+    for (int base = c0; base < c1; base += kGroups) {
+        const int c = base + g;
+        if (g < kGroups && c < c1) {
+            int v, cr, cs = 0, wid = -1, owner = -1;
+            if (blk) {
+                v = tc3[3 * c];
+                cr = tc3[3 * c + 1];
+                cs = tc3[3 * c + 2];
+            } else {
+                v = rc4[4 * c];
+                cr = rc4[4 * c + 1];
+                wid = rc4[4 * c + 2];
+                owner = rc4[4 * c + 3];
             }
-        }
-        // M = L^{-1} (lower), forward substitution on the identity
+            double L[28], inv[7], rr[7], rs[7];
+            const double* Av = A + (int64_t)v * 49;
 #pragma unroll
-        for (int j = 0; j < 7; j++) {
+            for (int i = 0; i < 7; i++)
 #pragma unroll
-            for (int i = 0; i < 7; i++) {
-                if (i < j) {
-                    M[i][j] = 0.0;
-                } else {
-                    double s = (i == j) ? 1.0 : 0.0;
+                for (int j = 0; j <= i; j++) L[b7::pk(i, j)] = Av[i * 7 + j];
+            const double* Ar = A + (int64_t)(cr >> 1) * 49;
 #pragma unroll
-                    for (int k = 0; k < 7; k++)
-                        if (k >= j && k < i) s -= L[i][k] * M[k][j];
-                    M[i][j] = s / L[i][i];
+            for (int m = 0; m < 7; m++) rr[m] = (cr & 1) ? Ar[m * 7 + ra] : Ar[ra * 7 + m];
+            if (blk) {
+                const double* As = A + (int64_t)(cs >> 1) * 49;
+#pragma unroll
+                for (int m = 0; m < 7; m++) rs[m] = (cs & 1) ? As[m * 7 + ra] : As[ra * 7 + m];
+            } else {
+#pragma unroll
+                for (int m = 0; m < 7; m++) rs[m] = b[(int64_t)v * 7 + m];
+            }
+            b7::chol7(L, inv, bad);
+            double wr[7], ws[7];
+            b7::fwd7(L, inv, rr, wr);  // row ra of W_rv
+            b7::fwd7(L, inv, rs, ws);  // block: row ra of W_sv; RHS: y_v (the same in every lane)
+#pragma unroll
+            for (int m = 0; m < 7; m++) sR[g][ra * kLd + m] = wr[m];
+            if (blk) {
+#pragma unroll
+                for (int m = 0; m < 7; m++) sS[g][ra * kLd + m] = ws[m];
+            } else {
+                if (ra == 0) {
+#pragma unroll
+                    for (int m = 0; m < 7; m++) sS[g][m] = ws[m];
+                }
+                if (wid >= 0) {
+                    double* Wd = W + (int64_t)wid * 49 + ra * 7;
+#pragma unroll
+                    for (int m = 0; m < 7; m++) Wd[m] = wr[m];
+                }
+                if (owner >= 0) {
+                    y[(int64_t)v * 7 + ra] = b7::pick(ws, ra);
+                    double* Ls = Lstore + (int64_t)owner * kLStoreRec;
+                    for (int k = ra; k < 35; k += 7) Ls[k] = k < 28 ? b7::pick(L, k) : b7::pick(inv, k - 28);
                 }
             }
         }
+        __syncthreads();
+        const int n = min(kGroups, c1 - base);
+        if (lane < nact) {
+            for (int k = 0; k < n; k++) {
+                const double* R = &sR[k][er * kLd];
+                const double* S = blk ? &sS[k][ec * kLd] : &sS[k][0];
 #pragma unroll
-        for (int i = 0; i < 7; i++)
-#pragma unroll
-            for (int j = 0; j < 7; j++) Li[i * 7 + j] = M[i][j];
-#pragma unroll
-        for (int i = 0; i < 7; i++) {
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k <= i; k++) s += M[i][k] * b[(int64_t)v * 7 + k];
-            yv[i] = s;
-        }
-        if (bad) flags[kFlagFail] = 1;
-    }
-    __syncthreads();
-    if (t < 49) Lstore[(int64_t)q * 49 + t] = Li[t];
-    if (t < 7) y[(int64_t)v * 7 + t] = yv[t];
-    if (t < 49) {
-        const int ra = t / 7, cb = t % 7;
-        for (int f = fptr[q]; f < fptr[q + 1]; f++) {
-            const int blk = fronts[4 * f + 1], tr = fronts[4 * f + 2], wid = fronts[4 * f + 3];
-            const double* Ab = A + (int64_t)blk * 49;
-            // W[ra][cb] = sum_m A_rv[ra][m] * Li[cb][m]
-            double s = 0.0;
-#pragma unroll
-            for (int m = 0; m < 7; m++) {
-                const double arv = tr ? Ab[m * 7 + ra] : Ab[ra * 7 + m];
-                s = fma(arv, Li[cb * 7 + m], s);
+                for (int m = 0; m < 7; m++) acc = fma(R[m], S[m], acc);
             }
-            W[(int64_t)wid * 49 + t] = s;
         }
+        __syncthreads();
     }
+    if (lane < nact) *dst = d0 - acc;
+    if (bad) flags[kFlagFail] = 1;  // benign race: every writer stores 1
 }
 
-// Block targets: tg = (block, contribution begin, end); contributions (W_x id, W_y id).
-// RHS targets: rtg = (pose r, begin, end); contributions (W id, pose v).
-__global__ __launch_bounds__(64) void sp_schur_kernel(
-    const int* __restrict__ tg, const int* __restrict__ tc, int tbeg, int nbt,
-    const int* __restrict__ rtg, const int* __restrict__ rc, int rbeg, const double* __restrict__ W,
-    const double* __restrict__ y, double* __restrict__ A, double* __restrict__ b,
-    const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
-    const int g = blockIdx.x, t = threadIdx.x;
-    if (g < nbt) {
-        const int* T_ = tg + 3 * (tbeg + g);
-        if (t < 49) {
-            const int ra = t / 7, cb = t % 7;
-            double acc = 0.0;
-            for (int c = T_[1]; c < T_[2]; c++) {
-                const double* Wx = W + (int64_t)tc[2 * c] * 49 + ra * 7;
-                const double* Wy = W + (int64_t)tc[2 * c + 1] * 49 + cb * 7;
-#pragma unroll
-                for (int m = 0; m < 7; m++) acc = fma(Wx[m], Wy[m], acc);
-            }
-            A[(int64_t)T_[0] * 49 + t] -= acc;
-        }
-    } else {
-        const int* R = rtg + 3 * (rbeg + g - nbt);
-        if (t < 7) {
-            double acc = 0.0;
-            for (int c = R[1]; c < R[2]; c++) {
-                const double* Wr = W + (int64_t)rc[2 * c] * 49 + t * 7;
-                const double* yv = y + (int64_t)rc[2 * c + 1] * 7;
-#pragma unroll
-                for (int m = 0; m < 7; m++) acc = fma(Wr[m], yv[m], acc);
-            }
-            b[(int64_t)R[0] * 7 + t] -= acc;
-        }
-    }
-}
-
-// x_v = Li_v^T (y_v - sum_r W_rv^T x_r)
+// x_v = L_v^-T (y_v - sum_r W_rv^T x_r), one workgroup per pose of the round; 7-lane group g
+// takes the fronts f0 + g, f0 + g + 9, ...; the group partials are summed in fixed order.
 __global__ __launch_bounds__(64) void sp_back_kernel(
     const int* __restrict__ nodes, const int* __restrict__ fptr, const int* __restrict__ fronts,
     int node_begin, const double* __restrict__ Lstore, const double* __restrict__ W,
     const double* __restrict__ y, double* __restrict__ x, const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
-    __shared__ double z[7];
-    const int q = node_begin + blockIdx.x;
-    const int v = nodes[q];
-    const int t = threadIdx.x;
-    if (t < 7) {
-        double s = y[(int64_t)v * 7 + t];
-        for (int f = fptr[q]; f < fptr[q + 1]; f++) {
-            const int r = fronts[4 * f], wid = fronts[4 * f + 3];
-            const double* Wr = W + (int64_t)wid * 49;
+    __shared__ double part[kGroups][kLd];
+    const int done = flags[kFlagDone];
+    const int q = node_begin + blockIdx.x, lane = threadIdx.x;
+    const int v = nodes[q], f0 = fptr[q], f1 = fptr[q + 1];
+    if (done) return;
+    const int g = lane / 7, ra = lane - 7 * g;
+    double L[28], inv[7], z[7];
+    const double* Ls = Lstore + (int64_t)q * kLStoreRec;
 #pragma unroll
-            for (int m = 0; m < 7; m++) s = fma(-Wr[m * 7 + t], x[(int64_t)r * 7 + m], s);
+    for (int k = 0; k < 28; k++) L[k] = Ls[k];
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        inv[k] = Ls[28 + k];
+        z[k] = y[(int64_t)v * 7 + k];
+    }
+    if (g < kGroups) {
+        double s = 0.0;
+        for (int f = f0 + g; f < f1; f += kGroups) {
+            const int* F = fronts + 4 * f;
+            const double* Wr = W + (int64_t)F[3] * 49 + ra;
+            const double* xr = x + (int64_t)F[0] * 7;
+#pragma unroll
+            for (int i = 0; i < 7; i++) s = fma(Wr[i * 7], xr[i], s);
         }
-        z[t] = s;
+        part[g][ra] = s;
     }
     __syncthreads();
-    if (t < 7) {
-        const double* Li = Lstore + (int64_t)q * 49;
-        double s = 0.0;
+    if (lane < 7) {
 #pragma unroll
-        for (int m = 0; m < 7; m++) s = fma(Li[m * 7 + t], z[m], s);
-        x[(int64_t)v * 7 + t] = s;
+        for (int m = 0; m < 7; m++) {
+            double a = 0.0;
+#pragma unroll
+            for (int k = 0; k < kGroups; k++) a += part[k][m];
+            z[m] -= a;
+        }
+        b7::bwd7(L, inv, z);
+        x[(int64_t)v * 7 + lane] = b7::pick(z, lane);
     }
 }
 
@@ -244,28 +225,12 @@ __global__ __launch_bounds__(256) void sp_tail_scatter_kernel(const double* __re
 
 // ------------------------------------------------------------------ launchers
 
-hipError_t launch_sp_init(hipStream_t st, const double* compact, int nblk, int nblocks, int npose,
-                          double* A, double* b, const int* flags) {
-    hipLaunchKernelGGL(sp_init_kernel, dim3(nblocks + 1), dim3(64), 0, st, compact, nblk, nblocks,
-                       npose, A, b, flags);
-    return hipGetLastError();
-}
-
-hipError_t launch_sp_factor(hipStream_t st, int nnodes, const int* nodes, const int* fptr,
-                            const int* fronts, int node_begin, const double* A, const double* b,
-                            double* Lstore, double* W, double* y, int* flags) {
-    if (nnodes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sp_factor_kernel, dim3(nnodes), dim3(64), 0, st, nodes, fptr, fronts,
-                       node_begin, A, b, Lstore, W, y, flags);
-    return hipGetLastError();
-}
-
-hipError_t launch_sp_schur(hipStream_t st, const int* tg, const int* tc, int tbeg, int nbt,
-                           const int* rtg, const int* rc, int rbeg, int nrt, const double* W,
-                           const double* y, double* A, double* b, const int* flags) {
+hipError_t launch_sp_round(hipStream_t st, const int* tg, const int* tc3, int tbeg, int nbt,
+                           const int* rtg, const int* rc4, int rbeg, int nrt, double* A, double* b,
+                           double* Lstore, double* W, double* y, int* flags) {
     if (nbt + nrt <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sp_schur_kernel, dim3(nbt + nrt), dim3(64), 0, st, tg, tc, tbeg, nbt, rtg,
-                       rc, rbeg, W, y, A, b, flags);
+    hipLaunchKernelGGL(sp_round_kernel, dim3(nbt + nrt), dim3(64), 0, st, tg, tc3, tbeg, nbt, rtg,
+                       rc4, rbeg, A, b, Lstore, W, y, flags);
     return hipGetLastError();
 }
 

@@ -174,23 +174,29 @@ def test_full_size_cfg2_matches_oracle(backend, oracle):
     assert _rel(T1, T_o) < 1e-5, _rel(T1, T_o)
 
 
-@pytest.mark.parametrize("solver", ["1", "2"])
-@pytest.mark.parametrize("topo", ["cfg3", "cfg4", "chain", "clique", "clique27", "clique28"])
+@pytest.mark.parametrize("solver", ["1", "2", "3"])
+@pytest.mark.parametrize("topo", ["cfg3", "cfg4", "chain", "star", "clique", "clique27", "clique28"])
 def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, solver):
     """The block-sparse solvers against the dense blocked Cholesky (M3S_SOLVER_DENSE=1) on the
     same system: one GN step, f64 solves of the same matrix in different orders -> updates
     agree to ~1e-9 relative.  M3S_SOLVER=1: the single-workgroup solve (gn_solve.hip; graphs
-    whose tail does not fit it fall back to 2), 2: the multi-launch rounds + tiled tail
-    (gn_sparse.hip).  Topologies cover the BASELINE graphs, a chain (everything eliminated in
-    rounds) and cliques (no independent low-degree set: dense tail only; 27 non-pinned poses =
-    the largest in-register tail, 189 unknowns in 12 x 12 tiles of 16x16; 28 = beyond it)."""
+    whose tail does not fit it fall back to 2), 2: one launch per elimination round
+    (gn_sparse.hip) + tiled dense core, 3: the same rounds + gn_solve's in-register core,
+    back-substitution and retraction (falls back to 2 when the core does not fit).  Topologies
+    cover the BASELINE graphs, a chain (everything eliminated in rounds), a star around the
+    pinned pose (poses without fronts) and cliques (no independent low-degree set: dense tail
+    only; 27 non-pinned poses = the largest in-register tail, 189 unknowns in 12 x 12 tiles of
+    16x16; 28 = beyond it)."""
     if topo == "chain":
         N = 24
         und = [(k - 1, k) for k in range(1, N)]
+    elif topo == "star":
+        N = 6
+        und = [(0, k) for k in range(1, N)]
     elif topo.startswith("clique"):
         N = {"clique": 12, "clique27": 28, "clique28": 29}[topo]
         und = [(a, b) for a in range(N) for b in range(a + 1, N)]
-    if topo == "chain" or topo.startswith("clique"):
+    if topo in ("chain", "star") or topo.startswith("clique"):
         g = synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
     else:
         g = synth.make_graph(topo, H=24, W=32, seed=6)
@@ -204,15 +210,18 @@ def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, sol
     assert _rel(T_s, T_d) < 1e-6
 
 
+@pytest.mark.parametrize("solver", ["1", "3"])
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
-def test_single_workgroup_solve_matches_multilaunch(backend, monkeypatch, cfg):
+def test_single_workgroup_solve_matches_multilaunch(backend, monkeypatch, cfg, solver):
     """The single-workgroup solve (M3S_SOLVER=1: rounds, in-register tail, back-substitution and
-    retraction in one launch) against the multi-launch solve (M3S_SOLVER=2) over 3 GN
-    iterations: the same f64 elimination in different orders -> updates agree to ~1e-9."""
+    retraction in one launch) and the hybrid (3: one launch per round, then the in-register
+    core + back-substitution + retraction in one launch) against the multi-launch solve
+    (M3S_SOLVER=2) over 3 GN iterations: the same f64 elimination in different orders ->
+    updates agree to ~1e-9."""
     g = synth.make_graph(cfg, H=24, W=32, seed=6)
     monkeypatch.setenv("M3S_SOLVER", "2")
     T_m, dx_m = _run_gpu(backend, g, "rays", 3)
-    monkeypatch.setenv("M3S_SOLVER", "1")
+    monkeypatch.setenv("M3S_SOLVER", solver)
     T_f, dx_f = _run_gpu(backend, g, "rays", 3)
     assert np.isfinite(dx_f).all()
     assert np.abs(dx_f - dx_m).max() <= 1e-8 * max(np.abs(dx_m).max(), 1e-6)

@@ -17,6 +17,7 @@ for v in ${VARIANTS:-default}; do
     fused_nommd) run fused_nommd M3S_SOLVER=1 M3S_SPARSE_MMD=0 M3S_FUSED_MAX_ROUNDS=64 ;;
     multi) run multi M3S_SOLVER=2 ;;
     multi_mmd) run multi_mmd M3S_SOLVER=2 M3S_MULTI_MMD=1 ;;
+    hybrid) run hybrid M3S_SOLVER=3 ;;
     dense) run dense M3S_SOLVER_DENSE=1 ;;
     esac
 done
