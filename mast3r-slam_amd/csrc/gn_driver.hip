@@ -851,7 +851,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         return M3S_OK;
     }
     SparsePlan& sp = c.sp;
-    SolveArgs S;
+    SolveArgs S{};
     S.npose = npose;
     S.b = sp.dptr<double>(sp.o_sys);
     S.A = S.b + sp.bpad;
@@ -931,7 +931,13 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
                                       W, y, flags));
     if (sp.hybrid) {
         // the <= 27-pose core in registers, the back-substitution through the rounds and the
-        // retraction: one single-workgroup launch (gn_solve.hip) reading the plan prefix
+        // retraction: one single-workgroup launch (gn_solve.hip) reading the plan prefix; the
+        // core is first laid out densely by a many-workgroup fill (one CU gathering it block by
+        // block took ~28 us)
+        M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail),
+                                          sp.ntail, sp.npad_tail, c.at<double>(L.dense), flags));
+        S.Hd = sp.ntail > 0 ? c.at<double>(L.dense) : nullptr;
+        S.npad_h = sp.npad_tail;
         S.nmeta = (int)sp.nints_back;
         S.meta_lds = 1;
         S.do_fwd = 0;

@@ -74,6 +74,8 @@ hipError_t launch_sp_round(hipStream_t st, const int* tg, const int* tc3, int tb
 hipError_t launch_sp_back(hipStream_t st, int nnodes, const int* nodes, const int* fptr,
                           const int* fronts, int node_begin, const double* Lstore, const double* W,
                           const double* y, double* x, const int* flags);
+hipError_t launch_sp_tail_fill(hipStream_t st, const double* A, const double* b, const int* tmap,
+                               const int* tail, int ntail, int npad, double* Hd, const int* flags);
 hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, const int* tmap,
                           const int* tail, int ntail, int npad, double* Hd, double* Linv,
                           double* xd, double* x, int* flags);
@@ -91,6 +93,10 @@ constexpr int kSolveRoundPoses = 64;  // poses per round (their y vectors staged
 struct SolveArgs {
     double *A, *b;          // block-format system (gn_assemble_kernel), updated in place
     double *y, *Lstore, *W, *Lg, *x;
+    // the core as a dense row-major matrix (sp_tail_fill_kernel, leading dimension npad_h), or
+    // nullptr: the in-register core then gathers its entries from the blocks
+    const double* Hd;
+    int npad_h;
     // the host plan: one int array; offsets of its parts.  rounds: 8 ints each (node_begin,
     // nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount); rc: (W id, node slot)
     const int* meta;

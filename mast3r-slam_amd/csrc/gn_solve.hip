@@ -217,8 +217,21 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
     const int* __restrict__ Mtail = M + a.o_tail;
     const int* __restrict__ Mtmap = M + a.o_tmap;
     d4 acc[NS > 0 ? NS : 1];
-    // -A from the blocks: every load issued unconditionally (entries outside the tail or of
+    // -A from the dense fill (coalesced: 16 lanes read 16 consecutive doubles of a row), or
+    // from the blocks: every load issued unconditionally (entries outside the tail or of
     // absent blocks read the zero block)
+    if (a.Hd != nullptr) {
+        const double* __restrict__ Hd = a.Hd;
+#pragma unroll
+        for (int k = 0; k < NS; k++) {
+            const int col = 16 * SM.J[k] + (lane & 15);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int row = 16 * SM.I[k] + (lane >> 4) + 4 * e;
+                acc[k][e] = -((row < n && col < n) ? Hd[(int64_t)row * a.npad_h + col] : 0.0);
+            }
+        }
+    } else {
 #pragma unroll
     for (int k = 0; k < NS; k++) {
         const int col = 16 * SM.J[k] + (lane & 15);
@@ -232,6 +245,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
                                          : (int64_t)(code >> 1) * 49 + ((code & 1) ? c7 * 7 + r7 : r7 * 7 + c7);
             acc[k][e] = -A[off];
         }
+    }
     }
     for (int i = tid; i < kTailMax * kPS; i += kThreads) sPop[i] = 0.0;
     for (int i = tid; i < n; i += kThreads) sZ[i] = a.b[(int64_t)Mtail[i / 7] * 7 + i % 7];

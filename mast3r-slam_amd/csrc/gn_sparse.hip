@@ -243,15 +243,23 @@ hipError_t launch_sp_back(hipStream_t st, int nnodes, const int* nodes, const in
     return hipGetLastError();
 }
 
-hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, const int* tmap,
-                          const int* tail, int ntail, int npad, double* Hd, double* Linv,
-                          double* xd, double* x, int* flags) {
+hipError_t launch_sp_tail_fill(hipStream_t st, const double* A, const double* b, const int* tmap,
+                               const int* tail, int ntail, int npad, double* Hd, const int* flags) {
     if (ntail <= 0) return hipSuccess;
     const int64_t total = (int64_t)(npad + kCholTile) * npad;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     hipLaunchKernelGGL(sp_tail_fill_kernel, dim3(blocks), dim3(256), 0, st, A, b, tmap, tail, ntail,
                        npad, Hd, flags);
-    hipError_t e = launch_dense_factor_solve(st, npad, Hd, Linv, xd, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, const int* tmap,
+                          const int* tail, int ntail, int npad, double* Hd, double* Linv,
+                          double* xd, double* x, int* flags) {
+    if (ntail <= 0) return hipSuccess;
+    hipError_t e = launch_sp_tail_fill(st, A, b, tmap, tail, ntail, npad, Hd, flags);
+    if (e != hipSuccess) return e;
+    e = launch_dense_factor_solve(st, npad, Hd, Linv, xd, flags);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sp_tail_scatter_kernel, dim3((ntail * 7 + 255) / 256), dim3(256), 0, st, xd,
                        tail, ntail, x, flags);
