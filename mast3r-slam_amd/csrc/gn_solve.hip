@@ -35,7 +35,9 @@
 //                  extract them to LDS | barrier.
 //             Back-substitution right-looking (x_K = L_KK^-T z_K as a matvec), one barrier
 //             per pose, the L entries of the next pose prefetched.
-//   back      the rounds in reverse: x_v = L^-T (y_v - sum_r W_rv^T x_r), 7 lanes per pose.
+//   back      the rounds in reverse: x_v = L^-T (y_v - sum_r W_rv^T x_r), 7 lanes per pose;
+//             a round of <= 18 poses (the late, dense ones) splits each pose's fronts over
+//             36 / nn groups whose partials meet in LDS (one round trip instead of ~6).
 //   retract   dx = -x (0 if a pivot failed), Twc <- exp(dx) * Twc, ||dx|| < delta_thresh.
 // Failure semantics follow SimplicialLLT: a pivot <= 0 fails (NaN passes) => dx = 0.
 #include <hip/hip_runtime.h>
@@ -665,9 +667,68 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
 
     // ------------------------------------------------------------------ back rounds
     if (a.do_back) {
+        constexpr int NG = NW * kGroups;
+        const int gid = wave * kGroups + g;
+        double* __restrict__ sPart = smem + kOffPn;  // tail scratch, free once the tail is done
+        static_assert(NG * 7 <= kOffZ - kOffPn, "back-round partials exceed the tail scratch");
         for (int rd = a.nrounds - 1; rd >= 0; rd--) {
             const int* R = Mrounds + 8 * rd;
             const int nb = R[0], nn = R[1];
+            if (2 * nn <= NG) {
+                // a small round (the late, dense ones: few poses, many fronts each): S groups
+                // per pose, split s takes the front batches s, s + S, ...; one LDS exchange,
+                // then split 0 sums the partials in split order (deterministic) and solves
+                const int S = NG / nn;
+                const bool on = lane < 7 * kGroups && gid < nn * S;
+                const int qi = on ? gid / S : 0, s = on ? gid - S * (gid / S) : 0;
+                const int q = nb + qi;
+                double z = 0.0;
+                double L[28], inv[7];
+                if (on) {
+                    if (s == 0) {
+                        const double* Ls = a.Lstore + (int64_t)q * kLStoreRec;
+#pragma unroll
+                        for (int k = 0; k < 28; k++) L[k] = Ls[k];
+#pragma unroll
+                        for (int k = 0; k < 7; k++) inv[k] = Ls[28 + k];
+                        z = a.y[(int64_t)Mnodes[q] * 7 + ra];
+                    }
+                    const int f0 = Mfptr[q], f1 = Mfptr[q + 1];
+                    for (int fb = f0 + 4 * s; fb < f1; fb += 4 * S) {
+                        double wv[4][7], xv[4][7];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const int f = fb + u < f1 ? fb + u : fb;
+                            const int* F = Mfronts + 4 * f;
+                            const double* Wr = W + (int64_t)F[3] * 49 + ra;
+                            const double* xr = sX + F[0] * 7;
+#pragma unroll
+                            for (int i = 0; i < 7; i++) {
+                                wv[u][i] = Wr[i * 7];
+                                xv[u][i] = xr[i];
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+                            if (fb + u < f1)
+#pragma unroll
+                                for (int i = 0; i < 7; i++) z = fma(-wv[u][i], xv[u][i], z);
+                    }
+                    if (s > 0) sPart[gid * 7 + ra] = z;
+                }
+                lds_barrier();
+                if (on && s == 0)
+                    for (int k = 1; k < S; k++) z += sPart[(gid + k) * 7 + ra];
+                double zz[7];
+#pragma unroll
+                for (int m = 0; m < 7; m++) zz[m] = __shfl(z, (lane < 63 ? 7 * g : 0) + m, 64);
+                if (on && s == 0) {
+                    bwd7(L, inv, zz);
+                    sX[Mnodes[q] * 7 + ra] = pick7(zz, ra);
+                }
+                lds_barrier();
+                continue;
+            }
             for (int base = wave * kGroups; base < nn; base += NW * kGroups) {
                 const int qi = base + g;
                 const bool on = lane < 7 * kGroups && qi < nn;
