@@ -155,6 +155,9 @@ int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, double* b_host)
  * ms, summed over the *n_iter recorded iterations.  Not thread-safe; test/bench only.
  */
 int m3s_prof_begin(void);
+/* The same, recording only the two events around each accumulate launch (every timed event
+ * record idles the GPU ~5 us): m3s_prof_end then fills out[0] and *n_iter, out[1..3] = 0. */
+int m3s_prof_begin_accum(void);
 int m3s_prof_end(double* out /* [4] */, int* n_iter);
 
 /* ---------------- frame tracking (single-pair Sim3 GN) ---------------- */
