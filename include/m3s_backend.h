@@ -109,7 +109,20 @@ typedef struct m3s_gn_args {
     size_t ws_bytes;
     void* comm;
     void* stream;
+    /* summation order of the per-edge normal equations (M3S_GN_ORDER_*); 0 = the
+     * default, overridable by the environment variable M3S_GN_ORDER=reference|fast */
+    int order;
 } m3s_gn_args;
+enum {
+    M3S_GN_ORDER_DEFAULT = 0,
+    /* packed stream, pre-adjoint rows, f32 lane chains of <= 32 points + f64 chunk sums
+     * (gn_accum.hip): the fast path */
+    M3S_GN_ORDER_FAST = 1,
+    /* the reference kernels' own order and formulas (gn_refacc.hip): one 256-thread
+     * workgroup per edge, 768-long fp32 chains per thread, blockReduce tree, per-point
+     * apply_Sim3_adj_inv; the system read from its lower triangle like SimplicialLLT */
+    M3S_GN_ORDER_REFERENCE = 2
+};
 
 size_t m3s_gn_workspace_bytes(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_local);
 
@@ -147,6 +160,12 @@ int m3s_gauss_newton_calib(float* Twc, const float* Xs, const float* Cs, const f
  * pointers), i.e. the system SparseBlock builds (gn_kernels.cu:71-113).
  */
 int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, double* b_host);
+/*
+ * Debug / test entry: ONE reference-order accumulate pass (gn_refacc.hip) with the current
+ * Twc, returning exactly the tensors the reference's align kernels write
+ * (gn_kernels.cu:1096-1137): Hs [4, E_local, 7, 7] f32 and gs [2, E_local, 7] f32 (host).
+ */
+int m3s_gn_edge_hessians(const m3s_gn_args* args, float* Hs_host, float* gs_host);
 
 /*
  * Phase timing (bench.py): between m3s_prof_begin() and m3s_prof_end() every GN

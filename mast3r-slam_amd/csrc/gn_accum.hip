@@ -44,11 +44,13 @@ __device__ __forceinline__ bool vgt(float a, float b) { return a > b; }
 __device__ __forceinline__ bool vlt(float a, float b) { return a < b; }
 __device__ __forceinline__ bool vand(bool a, bool b) { return a && b; }
 
-// Huber weight (gn_kernels.cu:172-175): |r| < 1.345 ? 1 : 1.345/|r|, as min(1, 1.345/|r|)
-// (3 VALU, no compare/select; equal up to the 1-ulp reciprocal at |r| ~ 1.345).
+// Huber weight (gn_kernels.cu:172-175): |r| < 1.345 ? 1 : 1.345/|r| as a compare-select, so a
+// NaN residual gives a NaN weight like the reference (a min(1, .) form turns it into 1); the
+// reciprocal is v_rcp_f32 (1 ulp; DESIGN.md §2 measures what that costs).
 template <typename V>
 __device__ __forceinline__ V huber(V r) {
-    return vmin(vsplat(1.345f, r) * vrcp(vabs(r)), 1.0f);
+    const V a = vabs(r);
+    return vsel(vlt(a, 1.345f), vsplat(1.0f, r), vsplat(1.345f, r) * vrcp(a));
 }
 
 // Accumulate one raw Jacobian row r (compile-time nonzero mask) with weight w, residual e.

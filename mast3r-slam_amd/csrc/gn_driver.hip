@@ -146,7 +146,7 @@ int chunk_points(int64_t HW, int nchunks) {
 }
 
 struct Layout {
-    size_t partials, edgeblk, compact, dense, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent,
+    size_t partials, edgeblk, compact, dense, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent, blk_ref,
         grad_ptr, grad_ent, slotmap, linv, sched, pack, zs, total;
     int nchunks, npad, nblk_max;
 };
@@ -165,6 +165,9 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
         return o;
     };
     L.partials = take(sizeof(float) * (size_t)E_local * L.nchunks * kNaccPad);
+    // per-edge records: the fast path's f64 Hjj/vj (kEdgeBlk doubles), or the reference-order
+    // path's f32 D/g (kRefStride floats)
+    static_assert(sizeof(float) * kRefStride <= sizeof(double) * kEdgeBlk, "edge record");
     L.edgeblk = take(sizeof(double) * (size_t)E_local * kEdgeBlk);
     L.compact = take(sizeof(double) * ((size_t)L.nblk_max * 28 + (size_t)npose * 7));
     L.dense = take(sizeof(double) * (size_t)(L.npad + kCholTile) * L.npad);
@@ -174,6 +177,7 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.jj_loc = take(sizeof(int) * (size_t)E_local);
     L.blk_ptr = take(sizeof(int) * ((size_t)L.nblk_max + 1));
     L.blk_ent = take(sizeof(int) * (size_t)E_local * 4);
+    L.blk_ref = take(sizeof(int) * (size_t)E_local * 4);  // reference-order assembly codes
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
     L.sched = take(sizeof(int) * (size_t)E_local * L.nchunks);
@@ -193,6 +197,7 @@ struct Plan {
     int nblk = 0;
     std::vector<int> ii_loc, jj_loc;              // local edges: Twc/Xs rows
     std::vector<int> blk_ptr, blk_ent;            // CSR: slot -> (edge<<1 | neg)
+    std::vector<int> blk_ref;                     // the same entries as (edge<<3 | type), gn_refacc.hip
     std::vector<int> grad_ptr, grad_ent;          // CSR: pose -> (edge<<1 | neg)
     std::vector<int> slotmap;                     // (npose x npose) -> slot or -1
     std::vector<int> sched;                       // accumulate task order: e * nchunks + c
@@ -310,6 +315,7 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
             for (int k = 0; k < plan.nblk; k++) plan.blk_ptr[k + 1] += plan.blk_ptr[k];
             for (int k = 0; k < npose; k++) plan.grad_ptr[k + 1] += plan.grad_ptr[k];
             plan.blk_ent.assign(plan.blk_ptr[plan.nblk], 0);
+            plan.blk_ref.assign(plan.blk_ptr[plan.nblk], 0);
             plan.grad_ent.assign(plan.grad_ptr[npose], 0);
             bfill.assign(plan.blk_ptr.begin(), plan.blk_ptr.end() - 1);
             gfill.assign(plan.grad_ptr.begin(), plan.grad_ptr.end() - 1);
@@ -325,8 +331,16 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
             for (int b = 0; b < 4; b++) {
                 if (rr[b] >= 0 && cc[b] >= 0 && rr[b] <= cc[b]) {
                     const int sl = slot(rr[b], cc[b]);
-                    if (pass == 0) plan.blk_ptr[sl + 1]++;
-                    else plan.blk_ent[bfill[sl]++] = (int)(el << 1) | neg[b];
+                    if (pass == 0) {
+                        plan.blk_ptr[sl + 1]++;
+                    } else {
+                        // reference-order block types (gn_assemble_ref_kernel): Hs[0]/Hs[3] on
+                        // the diagonal, Hs[1] at (ii, jj) when ii < jj, Hs[2] at (jj, ii) when
+                        // jj < ii, a self-edge's Hs[1]/Hs[2] on its diagonal block
+                        const int type = (b == 0 || b == 3) ? 0 : (i == j ? (b == 1 ? 3 : 4) : (b == 1 ? 2 : 1));
+                        plan.blk_ref[bfill[sl]] = (int)(el << 3) | type;
+                        plan.blk_ent[bfill[sl]++] = (int)(el << 1) | neg[b];
+                    }
                 }
             }
             if (i >= 0) {  // vi = -vj
@@ -661,7 +675,20 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     return M3S_OK;
 }
 
+// M3S_GN_ORDER_*: the args field, else env M3S_GN_ORDER=reference|fast, else fast
+int gn_order(const m3s_gn_args& a) {
+    if (a.order == M3S_GN_ORDER_FAST || a.order == M3S_GN_ORDER_REFERENCE) return a.order;
+    static const int env = [] {
+        const char* e = getenv("M3S_GN_ORDER");
+        if (e && (!strcmp(e, "reference") || !strcmp(e, "ref") || !strcmp(e, "2"))) return (int)M3S_GN_ORDER_REFERENCE;
+        return (int)M3S_GN_ORDER_FAST;
+    }();
+    return env;
+}
+
 int validate(const m3s_gn_args& a) {
+    M3S_REQUIRE(a.order >= M3S_GN_ORDER_DEFAULT && a.order <= M3S_GN_ORDER_REFERENCE,
+                "gauss_newton: bad summation order %d", a.order);
     M3S_REQUIRE(a.mode == M3S_GN_POINTS || a.mode == M3S_GN_RAYS || a.mode == M3S_GN_CALIB,
                 "gauss_newton: bad mode %d", a.mode);
     M3S_REQUIRE(a.N >= 1 && a.HW >= 1, "gauss_newton: need N >= 1 poses and HW >= 1 points");
@@ -687,6 +714,8 @@ int validate(const m3s_gn_args& a) {
 struct Ctx {
     bool need_slotmap = false;  // dense solver / debug system: upload the slot table
     bool packed = false;  // per-call packed stream (gn_pack_kernel) feeds the accumulate
+    bool ref_order = false;  // M3S_GN_ORDER_REFERENCE: gn_refacc.hip accumulate + assembly
+    RefParams R;
     Layout L;
     Plan plan;
     SparsePlan sp;
@@ -736,6 +765,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
         put(L.jj_loc, p.jj_loc);
         put(L.blk_ptr, p.blk_ptr);
         put(L.blk_ent, p.blk_ent);
+        put(L.blk_ref, p.blk_ref);
         put(L.grad_ptr, p.grad_ptr);
         put(L.grad_ent, p.grad_ent);
         put(L.sched, p.sched);
@@ -780,6 +810,26 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     // M3S_GN_PACK: 0 never, 1 (default) when the call runs >= 3 iterations, 2 always
     const int pack_mode = env_int("M3S_GN_PACK", 1);
     c.packed = c.vec && a.E_local > 0 && (pack_mode == 2 || (pack_mode == 1 && a.max_iter >= 3));
+
+    c.ref_order = gn_order(a) == M3S_GN_ORDER_REFERENCE;
+    if (c.ref_order) {
+        c.packed = false;  // the reference-order kernel reads the reference's tensors
+        RefParams& R = c.R;
+        R.s0_inv = (float)(1.0 / (double)a.sigma0);  // `const float sigma_*_inv = 1.0/sigma_*`
+        R.s1_inv = (a.mode == M3S_GN_POINTS) ? 0.0f : (float)(1.0 / (double)a.sigma1);
+        R.C_thresh = a.C_thresh;
+        R.Q_thresh = a.Q_thresh;
+        R.fx = p.K[0];
+        R.fy = p.K[1];
+        R.cx = p.K[2];
+        R.cy = p.K[3];
+        R.z_eps = a.z_eps;
+        R.width = a.width > 0 ? a.width : 1;
+        R.height = a.height;
+        R.pixel_border = a.pixel_border;
+        R.HW = a.HW;
+        R.variant = env_int("M3S_GN_REF_VARIANT", 0);  // diagnostics
+    }
     return M3S_OK;
 }
 
@@ -798,6 +848,29 @@ int prepare_iterations(const m3s_gn_args& a, Ctx& c) {
 int enqueue_system(const m3s_gn_args& a, Ctx& c) {
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
+    const int npose_r = (int)(a.N - 1);
+    if (c.ref_order) {
+        // the reference kernels' order (gn_refacc.hip), then the block system from the lower
+        // triangle of the reference's matrix (the sparse solvers' format)
+        M3S_REQUIRE(c.sp.enabled, "gauss_newton: the reference order needs the block-sparse solver");
+        g_prof.mark(c.st, true);
+        M3S_HIP_CHECK(launch_accum_ref(a.mode, (int)a.E_local, c.st, a.Twc, a.Xs, a.Cs,
+                                       c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), a.idx, a.valid, a.Q,
+                                       c.R, c.at<float>(L.edgeblk), flags));
+        g_prof.mark(c.st, true);
+        SparsePlan& sp = c.sp;
+        double* sys = sp.dptr<double>(sp.o_sys);
+        M3S_HIP_CHECK(launch_assemble_ref(c.st, c.at<float>(L.edgeblk), c.at<int>(L.blk_ptr),
+                                          c.at<int>(L.blk_ref), c.at<int>(L.grad_ptr),
+                                          c.at<int>(L.grad_ent), c.plan.nblk, sp.nblocks, npose_r,
+                                          sp.bpad, sys, flags));
+        if (a.comm) {
+            const size_t count = (size_t)sp.bpad + (size_t)c.plan.nblk * 49;
+            int rc = comm_allreduce_sum_f64(a.comm, sys, count, c.st);
+            if (rc) return rc;
+        }
+        return M3S_OK;
+    }
     if (a.E_local > 0) {
         g_prof.mark(c.st, true);
         const dim3 grid((unsigned)(L.nchunks * a.E_local));
@@ -978,7 +1051,7 @@ int run(const m3s_gn_args& a) {
     rc = prepare_iterations(a, c);
     if (rc) return rc;
     std::chrono::steady_clock::time_point t2 = now(), t3 = t2;
-    if (env_int("M3S_SOLVER_DENSE", 0) == 0) {
+    if (env_int("M3S_SOLVER_DENSE", 0) == 0 || c.ref_order) {
         // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
         // single-workgroup solve when its plan needs few rounds, else multi-launch
         const int choice = env_int("M3S_SOLVER", 0);
@@ -1057,12 +1130,95 @@ extern "C" int m3s_gauss_newton(const m3s_gn_args* args) {
     return run(*args);
 }
 
+namespace {
+// Reference-order per-edge records (kRefStride floats: D[7][7], g[7]) of ONE accumulate pass,
+// copied to the host.
+int ref_edge_records(const m3s_gn_args& a0, Ctx& c, std::vector<float>& rec) {
+    m3s_gn_args a = a0;
+    a.order = M3S_GN_ORDER_REFERENCE;
+    int rc = setup(a, c);
+    if (rc) return rc;
+    rec.assign((size_t)a.E_local * kRefStride, 0.0f);
+    if (a.E_local == 0) return M3S_OK;
+    const Layout& L = c.L;
+    M3S_HIP_CHECK(launch_accum_ref(a.mode, (int)a.E_local, c.st, a.Twc, a.Xs, a.Cs, c.at<int>(L.ii_loc),
+                                   c.at<int>(L.jj_loc), a.idx, a.valid, a.Q, c.R, c.at<float>(L.edgeblk),
+                                   c.at<int>(L.flags)));
+    M3S_HIP_CHECK(hipMemcpyAsync(rec.data(), c.at<float>(L.edgeblk), sizeof(float) * rec.size(),
+                                 hipMemcpyDeviceToHost, c.st));
+    M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+    return M3S_OK;
+}
+
+// The reference's four blocks of one edge from its record (see gn_refacc.hip):
+// Hs[0] = Hs[3] = lower(D) mirrored, Hs[1] = -D^T, Hs[2] = -D.
+double ref_block(const float* D, int blk, int r, int cc) {
+    switch (blk) {
+        case 0:
+        case 3: return (double)D[std::max(r, cc) * 7 + std::min(r, cc)];
+        case 1: return -(double)D[cc * 7 + r];
+        default: return -(double)D[r * 7 + cc];
+    }
+}
+}  // namespace
+
+extern "C" int m3s_gn_edge_hessians(const m3s_gn_args* args, float* Hs_host, float* gs_host) {
+    if (!args || !Hs_host || !gs_host) {
+        set_error("gn_edge_hessians: null argument");
+        return M3S_ERR_INVALID;
+    }
+    Ctx c;
+    std::vector<float> rec;
+    int rc = ref_edge_records(*args, c, rec);
+    if (rc) return rc;
+    const int64_t E = args->E_local;
+    for (int64_t e = 0; e < E; e++) {
+        const float* D = rec.data() + e * kRefStride;
+        for (int blk = 0; blk < 4; blk++)
+            for (int r = 0; r < 7; r++)
+                for (int q = 0; q < 7; q++)
+                    Hs_host[((blk * E + e) * 7 + r) * 7 + q] = (float)ref_block(D, blk, r, q);
+        for (int q = 0; q < 7; q++) {
+            gs_host[(0 * E + e) * 7 + q] = -D[49 + q];
+            gs_host[(1 * E + e) * 7 + q] = D[49 + q];
+        }
+    }
+    return M3S_OK;
+}
+
 extern "C" int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, double* b_host) {
     if (!args) {
         set_error("gn_build_system: null args");
         return M3S_ERR_INVALID;
     }
     const m3s_gn_args& a = *args;
+    if (gn_order(a) == M3S_GN_ORDER_REFERENCE) {
+        // the full (not exactly symmetric) matrix SparseBlock::update_lhs/update_rhs builds
+        // from the reference-order Hs/gs (gn_kernels.cu:71-113)
+        Ctx c;
+        std::vector<float> rec;
+        int rc = ref_edge_records(a, c, rec);
+        if (rc) return rc;
+        const int64_t n = 7 * (a.N - 1);
+        std::fill(H_host, H_host + n * n, 0.0);
+        std::fill(b_host, b_host + n, 0.0);
+        for (int64_t el = 0; el < a.E_local; el++) {
+            const float* D = rec.data() + el * kRefStride;
+            const int i = c.plan.ii_loc[el] - 1, j = c.plan.jj_loc[el] - 1;
+            const int rr[4] = {i, i, j, j}, cc[4] = {i, j, i, j};
+            for (int blk = 0; blk < 4; blk++) {
+                if (rr[blk] < 0 || cc[blk] < 0) continue;
+                for (int r = 0; r < 7; r++)
+                    for (int q = 0; q < 7; q++)
+                        H_host[(7 * rr[blk] + r) * n + 7 * cc[blk] + q] += ref_block(D, blk, r, q);
+            }
+            for (int q = 0; q < 7; q++) {
+                if (i >= 0) b_host[7 * i + q] -= (double)D[49 + q];
+                if (j >= 0) b_host[7 * j + q] += (double)D[49 + q];
+            }
+        }
+        return M3S_OK;
+    }
     Ctx c;
     c.need_slotmap = true;
     int rc = setup(a, c);

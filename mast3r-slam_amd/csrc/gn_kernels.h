@@ -40,6 +40,31 @@ struct AccParams {
     int nkf;      // keyframes (rows of Xs / Zs)
 };
 
+// Reference-order ("parity") accumulate, gn_refacc.hip
+constexpr int kRefVals = 56;    // per edge: D[7][7] + g[7]
+constexpr int kRefStride = 64;  // floats per edge record
+struct RefParams {
+    float s0_inv, s1_inv;  // (float)(1.0 / sigma) as the reference computes them
+    float C_thresh, Q_thresh;
+    float fx, fy, cx, cy;
+    float z_eps;
+    int width, height, pixel_border;
+    int64_t HW;
+    int variant;  // diagnostics only (env M3S_GN_REF_VARIANT): kRefVar* formula substitutions
+};
+// Formula substitutions for measuring what each deviation of the fast path's residual model
+// from the reference costs in accuracy, under the reference's own summation order.
+constexpr int kRefVarLogRatio = 1;  // calib log depth as ln2 * log2(zj * rcp(zi))
+constexpr int kRefVarRcp = 2;       // 1/x by v_rcp_f32 instead of the double division
+constexpr int kRefVarHuberMin = 4;  // Huber weight as min(1, 1.345 rcp|r|)
+hipError_t launch_accum_ref(int mode, int E_local, hipStream_t st, const float* Twc, const float* Xs,
+                            const float* Cs, const int* ii_loc, const int* jj_loc, const int64_t* idx,
+                            const uint8_t* valid, const float* Q, const RefParams& P, float* out,
+                            const int* flags);
+hipError_t launch_assemble_ref(hipStream_t st, const float* ref, const int* blk_ptr, const int* blk_ref,
+                               const int* grad_ptr, const int* grad_ent, int nblk, int nblocks,
+                               int npose, int bpad, double* out, const int* flags);
+
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
                         const int64_t* idx, const uint8_t* valid, const float* Q,

@@ -57,6 +57,7 @@ def make_args(g, mode, L, Twc, edge_range=None, max_iter=1, delta=0.0, comm=None
     keep.append(ws)
     a.ws, a.ws_bytes = ws.data_ptr(), nbytes
     a.comm = comm
+    a.order = mb._gn_order[0]
     a.stream = torch.cuda.current_stream(torch.device(dev)).cuda_stream
     return a, keep
 
@@ -72,3 +73,18 @@ def build_system_gpu(g, mode, L, edge_range=None):
     mb._raise(rc, "gn_build_system")
     del keep
     return H, b
+
+
+def edge_hessians_gpu(g, mode, L, edge_range=None):
+    """One reference-order accumulate pass (gn_refacc.hip): the reference align kernels'
+    outputs Hs [4, E, 7, 7] and gs [2, E, 7] (f32) for the current poses."""
+    Twc = g.Twc.cuda().contiguous()
+    a, keep = make_args(g, mode, L, Twc, edge_range=edge_range)
+    E = a.E_local
+    Hs = np.zeros((4, E, 7, 7), np.float32)
+    gs = np.zeros((2, E, 7), np.float32)
+    rc = mb.lib.m3s_gn_edge_hessians(ctypes.byref(a), Hs.ctypes.data_as(ctypes.c_void_p),
+                                     gs.ctypes.data_as(ctypes.c_void_p))
+    mb._raise(rc, "gn_edge_hessians")
+    del keep
+    return Hs, gs

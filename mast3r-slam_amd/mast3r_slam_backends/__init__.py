@@ -28,6 +28,7 @@ __all__ = [
     "pointmap_update",
     "edge_confidence",
     "library_path",
+    "set_gn_order",
     "lib",
 ]
 
@@ -92,16 +93,33 @@ class GNArgs(ctypes.Structure):
         ("ws_bytes", ctypes.c_size_t),
         ("comm", _vp),
         ("stream", _vp),
+        ("order", _i),
     ]
 
 
 lib.m3s_gauss_newton.argtypes = [ctypes.POINTER(GNArgs)]
 lib.m3s_gn_build_system.argtypes = [ctypes.POINTER(GNArgs), _vp, _vp]
+lib.m3s_gn_edge_hessians.argtypes = [ctypes.POINTER(GNArgs), _vp, _vp]
 lib.m3s_comm_get_unique_id.argtypes = [_vp]
 lib.m3s_comm_init.argtypes = [_vp, _i, _i, ctypes.POINTER(_vp)]
 lib.m3s_comm_destroy.argtypes = [_vp]
 
 GN_POINTS, GN_RAYS, GN_CALIB = 0, 1, 2
+
+# Summation order of the GN normal equations (include/m3s_backend.h M3S_GN_ORDER_*):
+# "default" lets the library decide (env M3S_GN_ORDER, else the fast packed path); "reference"
+# reproduces the reference kernels' own float order and formulas (gn_refacc.hip).
+GN_ORDERS = {"default": 0, "fast": 1, "reference": 2}
+_gn_order = [0]
+
+
+def set_gn_order(order: str) -> str:
+    """Select the GN summation order for later gauss_newton_* calls; returns the previous."""
+    if order not in GN_ORDERS:
+        raise ValueError(f"unknown GN order {order!r} (expected one of {sorted(GN_ORDERS)})")
+    prev = [k for k, v in GN_ORDERS.items() if v == _gn_order[0]][0]
+    _gn_order[0] = GN_ORDERS[order]
+    return prev
 
 # ---------------------------------------------------------------------------------
 # argument checks (the reference's TORCH_CHECK / packed_accessor32 behaviour)
@@ -280,6 +298,7 @@ def _run_gn(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter, delt
     a.dx = dx.data_ptr()
     a.ws, a.ws_bytes = ws.data_ptr(), ws_bytes
     a.comm = comm
+    a.order = _gn_order[0]
     with torch.cuda.device(dev):
         a.stream = torch.cuda.current_stream(dev).cuda_stream
         rc = lib.m3s_gauss_newton(ctypes.byref(a))

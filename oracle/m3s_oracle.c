@@ -521,14 +521,24 @@ static inline void accum_row(double* acc, const float* ti, const float* qi, cons
     }
 }
 
-static void align_point(const oracle_gn_params* P, const float* ti, const float* qi, const float* si,
-                        const float* tij, const float* qij, const float* sij,
-                        const float* Xi, const float* Xj, float q, float ci, float cj,
-                        int valid_match_ind, int64_t ind_Xi, double* acc) {
+/* Per-point residual model of the align kernels: the transformed point, residuals, robust
+ * weights (Huber x confidence, gn_kernels.cu:963-978 / 1403-1418 / 598-613), the validity
+ * flag and the raw (pre-adjoint) Jacobian rows.  Returns the number of residual rows. */
+typedef struct {
     float Xj_Ci[3];
-    float Jx[14];
-    float* Ji = &Jx[0];
+    float err[4], w[4];
+    float J[4][7];
+    int valid;
+} point_res;
+
+static int point_residuals(const oracle_gn_params* P, const float* tij, const float* qij,
+                           const float* sij, const float* Xi, const float* Xj, float q, float ci,
+                           float cj, int valid_match_ind, int64_t ind_Xi, point_res* R) {
+    float* Xj_Ci = R->Xj_Ci;
+    float* err = R->err;
+    float* w = R->w;
     actSim3(tij, qij, sij, Xj, Xj_Ci);
+    memset(R->J, 0, sizeof(R->J));
     if (P->mode == ORACLE_GN_RAYS) {
         /* gn_kernels.cu:924-1089 */
         const float sigma_ray_inv = (float)(1.0 / (double)P->sigma0);
@@ -543,12 +553,12 @@ static void align_point(const oracle_gn_params* P, const float* ti, const float*
         const float norm1_j_inv = (float)(1.0 / (double)norm1_j);
         float rj[3];
         for (int i = 0; i < 3; i++) rj[i] = norm1_j_inv * Xj_Ci[i];
-        float err[4], w[4];
         err[0] = rj[0] - ri[0];
         err[1] = rj[1] - ri[1];
         err[2] = rj[2] - ri[2];
         err[3] = norm1_j - norm1_i;
         const int valid = valid_match_ind & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh);
+        R->valid = valid;
         const float sqrt_w_ray = valid ? sigma_ray_inv * sqrtf(q) : 0.0f;
         const float sqrt_w_dist = valid ? sigma_dist_inv * sqrtf(q) : 0.0f;
         w[0] = huber(sqrt_w_ray * err[0]);
@@ -568,18 +578,19 @@ static void align_point(const oracle_gn_params* P, const float* ti, const float*
         const float drx_dPy = ((-Xj_Ci[0]) * Xj_Ci[1]) * norm3_j_inv;
         const float drx_dPz = ((-Xj_Ci[0]) * Xj_Ci[2]) * norm3_j_inv;
         const float dry_dPz = ((-Xj_Ci[1]) * Xj_Ci[2]) * norm3_j_inv;
-        Ji[0] = drx_dPx; Ji[1] = drx_dPy; Ji[2] = drx_dPz;
-        Ji[3] = 0.0f; Ji[4] = rj[2]; Ji[5] = -rj[1]; Ji[6] = 0.0f;
-        accum_row(acc, ti, qi, si, Jx, w[0], err[0]);
-        Ji[0] = drx_dPy; Ji[1] = dry_dPy; Ji[2] = dry_dPz;
-        Ji[3] = -rj[2]; Ji[4] = 0.0f; Ji[5] = rj[0]; Ji[6] = 0.0f;
-        accum_row(acc, ti, qi, si, Jx, w[1], err[1]);
-        Ji[0] = drx_dPz; Ji[1] = dry_dPz; Ji[2] = drz_dPz;
-        Ji[3] = rj[1]; Ji[4] = -rj[0]; Ji[5] = 0.0f; Ji[6] = 0.0f;
-        accum_row(acc, ti, qi, si, Jx, w[2], err[2]);
-        Ji[0] = rj[0]; Ji[1] = rj[1]; Ji[2] = rj[2];
-        Ji[3] = 0.0f; Ji[4] = 0.0f; Ji[5] = 0.0f; Ji[6] = norm1_j;
-        accum_row(acc, ti, qi, si, Jx, w[3], err[3]);
+        float* J0 = R->J[0];
+        float* J1 = R->J[1];
+        float* J2 = R->J[2];
+        float* J3 = R->J[3];
+        J0[0] = drx_dPx; J0[1] = drx_dPy; J0[2] = drx_dPz;
+        J0[3] = 0.0f; J0[4] = rj[2]; J0[5] = -rj[1]; J0[6] = 0.0f;
+        J1[0] = drx_dPy; J1[1] = dry_dPy; J1[2] = dry_dPz;
+        J1[3] = -rj[2]; J1[4] = 0.0f; J1[5] = rj[0]; J1[6] = 0.0f;
+        J2[0] = drx_dPz; J2[1] = dry_dPz; J2[2] = drz_dPz;
+        J2[3] = rj[1]; J2[4] = -rj[0]; J2[5] = 0.0f; J2[6] = 0.0f;
+        J3[0] = rj[0]; J3[1] = rj[1]; J3[2] = rj[2];
+        J3[3] = 0.0f; J3[4] = 0.0f; J3[5] = 0.0f; J3[6] = norm1_j;
+        return 4;
     } else if (P->mode == ORACLE_GN_CALIB) {
         /* gn_kernels.cu:1360-1495 */
         const float fx = P->K[0], fy = P->K[4], cx = P->K[2], cy = P->K[5];
@@ -597,12 +608,12 @@ static void align_point(const oracle_gn_params* P, const float* ti, const float*
         const float v = fy * y_div_z + cy;
         const int valid_u = (u > (float)P->pixel_border) && (u < (float)(P->width - 1 - P->pixel_border));
         const int valid_v = (v > (float)P->pixel_border) && (v < (float)(P->height - 1 - P->pixel_border));
-        float err[3], w[3];
         err[0] = u - (float)u_target;
         err[1] = v - (float)v_target;
         err[2] = zj_log - zi_log;
         const int valid = valid_match_ind & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh) &
                           valid_u & valid_v & valid_z;
+        R->valid = valid;
         const float sqrt_w_pixel = valid ? sigma_pixel_inv * sqrtf(q) : 0.0f;
         const float sqrt_w_depth = valid ? sigma_depth_inv * sqrtf(q) : 0.0f;
         w[0] = huber(sqrt_w_pixel * err[0]);
@@ -613,25 +624,28 @@ static void align_point(const oracle_gn_params* P, const float* ti, const float*
         w[0] *= w_const_pixel;
         w[1] *= w_const_pixel;
         w[2] *= w_const_depth;
-        Ji[0] = fx * zj_inv; Ji[1] = 0.0f; Ji[2] = ((-fx) * x_div_z) * zj_inv;
-        Ji[3] = ((-fx) * x_div_z) * y_div_z; Ji[4] = fx * (1.0f + x_div_z * x_div_z);
-        Ji[5] = (-fx) * y_div_z; Ji[6] = 0.0f;
-        accum_row(acc, ti, qi, si, Jx, w[0], err[0]);
-        Ji[0] = 0.0f; Ji[1] = fy * zj_inv; Ji[2] = ((-fy) * y_div_z) * zj_inv;
-        Ji[3] = (-fy) * (1.0f + y_div_z * y_div_z); Ji[4] = (fy * x_div_z) * y_div_z;
-        Ji[5] = fy * x_div_z; Ji[6] = 0.0f;
-        accum_row(acc, ti, qi, si, Jx, w[1], err[1]);
-        Ji[0] = 0.0f; Ji[1] = 0.0f; Ji[2] = zj_inv;
-        Ji[3] = y_div_z; Ji[4] = -x_div_z; Ji[5] = 0.0f; Ji[6] = 1.0f;
-        accum_row(acc, ti, qi, si, Jx, w[2], err[2]);
+        float* J0 = R->J[0];
+        float* J1 = R->J[1];
+        float* J2 = R->J[2];
+        J0[0] = fx * zj_inv; J0[1] = 0.0f; J0[2] = ((-fx) * x_div_z) * zj_inv;
+        J0[3] = ((-fx) * x_div_z) * y_div_z; J0[4] = fx * (1.0f + x_div_z * x_div_z);
+        J0[5] = (-fx) * y_div_z; J0[6] = 0.0f;
+        J1[0] = 0.0f; J1[1] = fy * zj_inv; J1[2] = ((-fy) * y_div_z) * zj_inv;
+        J1[3] = (-fy) * (1.0f + y_div_z * y_div_z); J1[4] = (fy * x_div_z) * y_div_z;
+        J1[5] = fy * x_div_z; J1[6] = 0.0f;
+        J2[0] = 0.0f; J2[1] = 0.0f; J2[2] = zj_inv;
+        J2[3] = y_div_z; J2[4] = -x_div_z; J2[5] = 0.0f; J2[6] = 1.0f;
+        err[3] = 0.0f;
+        w[3] = 0.0f;
+        return 3;
     } else {
         /* point_align_kernel, gn_kernels.cu:564-674 */
         const float sigma_point_inv = (float)(1.0 / (double)P->sigma0);
-        float err[3], w[3];
         err[0] = Xj_Ci[0] - Xi[0];
         err[1] = Xj_Ci[1] - Xi[1];
         err[2] = Xj_Ci[2] - Xi[2];
         const int valid = valid_match_ind & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh);
+        R->valid = valid;
         const float sqrt_w_point = valid ? sigma_point_inv * sqrtf(q) : 0.0f;
         w[0] = huber(sqrt_w_point * err[0]);
         w[1] = huber(sqrt_w_point * err[1]);
@@ -640,15 +654,31 @@ static void align_point(const oracle_gn_params* P, const float* ti, const float*
         w[0] *= w_const_point;
         w[1] *= w_const_point;
         w[2] *= w_const_point;
-        Ji[0] = 1.0f; Ji[1] = 0.0f; Ji[2] = 0.0f; Ji[3] = 0.0f;
-        Ji[4] = Xj_Ci[2]; Ji[5] = -Xj_Ci[1]; Ji[6] = Xj_Ci[0];
-        accum_row(acc, ti, qi, si, Jx, w[0], err[0]);
-        Ji[0] = 0.0f; Ji[1] = 1.0f; Ji[2] = 0.0f; Ji[3] = -Xj_Ci[2];
-        Ji[4] = 0.0f; Ji[5] = Xj_Ci[0]; Ji[6] = Xj_Ci[1];
-        accum_row(acc, ti, qi, si, Jx, w[1], err[1]);
-        Ji[0] = 0.0f; Ji[1] = 0.0f; Ji[2] = 1.0f; Ji[3] = Xj_Ci[1];
-        Ji[4] = -Xj_Ci[0]; Ji[5] = 0.0f; Ji[6] = Xj_Ci[2];
-        accum_row(acc, ti, qi, si, Jx, w[2], err[2]);
+        float* J0 = R->J[0];
+        float* J1 = R->J[1];
+        float* J2 = R->J[2];
+        J0[0] = 1.0f; J0[1] = 0.0f; J0[2] = 0.0f; J0[3] = 0.0f;
+        J0[4] = Xj_Ci[2]; J0[5] = -Xj_Ci[1]; J0[6] = Xj_Ci[0];
+        J1[0] = 0.0f; J1[1] = 1.0f; J1[2] = 0.0f; J1[3] = -Xj_Ci[2];
+        J1[4] = 0.0f; J1[5] = Xj_Ci[0]; J1[6] = Xj_Ci[1];
+        J2[0] = 0.0f; J2[1] = 0.0f; J2[2] = 1.0f; J2[3] = Xj_Ci[1];
+        J2[4] = -Xj_Ci[0]; J2[5] = 0.0f; J2[6] = Xj_Ci[2];
+        err[3] = 0.0f;
+        w[3] = 0.0f;
+        return 3;
+    }
+}
+
+static void align_point(const oracle_gn_params* P, const float* ti, const float* qi, const float* si,
+                        const float* tij, const float* qij, const float* sij,
+                        const float* Xi, const float* Xj, float q, float ci, float cj,
+                        int valid_match_ind, int64_t ind_Xi, double* acc) {
+    point_res R;
+    const int nrows = point_residuals(P, tij, qij, sij, Xi, Xj, q, ci, cj, valid_match_ind, ind_Xi, &R);
+    float Jx[14];
+    for (int r = 0; r < nrows; r++) {
+        memcpy(Jx, R.J[r], sizeof(float) * 7);
+        accum_row(acc, ti, qi, si, Jx, R.w[r], R.err[r]);
     }
 }
 
@@ -712,6 +742,35 @@ static void gn_align_impl(const oracle_gn_params* P, const float* Twc, const flo
         }
         free(acc);
         free(sdata);
+    }
+}
+
+void oracle_gn_residuals(const oracle_gn_params* P, const float* Twc, const float* Xs,
+                         const float* Cs, const int64_t* ii_edge, const int64_t* jj_edge,
+                         const int64_t* idx, const uint8_t* valid, const float* Q,
+                         int64_t N, int64_t HW, int64_t E, float* Xj_Ci, float* err, float* w,
+                         uint8_t* valid_out) {
+    (void)N;
+    for (int64_t e = 0; e < E; e++) {
+        const int64_t ix = ii_edge[e], jx = jj_edge[e];
+        const float* Ti = Twc + ix * 8;
+        const float* Tj = Twc + jx * 8;
+        float ti[3] = {Ti[0], Ti[1], Ti[2]}, qi[4] = {Ti[3], Ti[4], Ti[5], Ti[6]}, si[1] = {Ti[7]};
+        float tj[3] = {Tj[0], Tj[1], Tj[2]}, qj[4] = {Tj[3], Tj[4], Tj[5], Tj[6]}, sj[1] = {Tj[7]};
+        float tij[3], qij[4], sij[1];
+        relSim3(ti, qi, si, tj, qj, sj, tij, qij, sij);
+        for (int64_t k = 0; k < HW; k++) {
+            const int64_t pe = e * HW + k;
+            const int vm = valid[pe] != 0;
+            const int64_t ind = vm ? idx[pe] : 0;
+            point_res R;
+            point_residuals(P, tij, qij, sij, Xs + (ix * HW + ind) * 3, Xs + (jx * HW + k) * 3, Q[pe],
+                            Cs[ix * HW + ind], Cs[jx * HW + k], vm, ind, &R);
+            memcpy(Xj_Ci + pe * 3, R.Xj_Ci, sizeof(float) * 3);
+            memcpy(err + pe * 4, R.err, sizeof(float) * 4);
+            memcpy(w + pe * 4, R.w, sizeof(float) * 4);
+            valid_out[pe] = (uint8_t)(R.valid != 0);
+        }
     }
 }
 

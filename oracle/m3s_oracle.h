@@ -76,6 +76,17 @@ typedef struct oracle_gn_params {
  * follow the reference's 256-thread strided loop and shared-memory tree
  * (gn_kernels.cu:31-55, 910-1137) so the float summation order matches.
  */
+/*
+ * The per-point residual model of the align kernels (no accumulation), for pinning it to the
+ * reference's own Python (tests/golden/make_residual_golden.py): per directed point-edge the
+ * transformed point T_ij Xj [E,HW,3], residuals [E,HW,4] and robust weights (Huber x
+ * confidence) [E,HW,4] (calib/points: 3 rows, the 4th is 0) and the validity flag [E,HW].
+ */
+void oracle_gn_residuals(const oracle_gn_params* P, const float* Twc, const float* Xs,
+                         const float* Cs, const int64_t* ii_edge, const int64_t* jj_edge,
+                         const int64_t* idx, const uint8_t* valid, const float* Q,
+                         int64_t N, int64_t HW, int64_t E, float* Xj_Ci, float* err, float* w,
+                         uint8_t* valid_out);
 void oracle_gn_align(const oracle_gn_params* P, const float* Twc, const float* Xs,
                      const float* Cs, const int64_t* ii_edge, const int64_t* jj_edge,
                      const int64_t* idx, const uint8_t* valid, const float* Q,

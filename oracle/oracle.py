@@ -56,6 +56,7 @@ class GNParams(ctypes.Structure):
 
 _P = ctypes.POINTER(GNParams)
 _lib.oracle_gn_align.argtypes = [_P] + [_vp] * 8 + [_i64] * 3 + [_vp, _vp]
+_lib.oracle_gn_residuals.argtypes = [_P] + [_vp] * 8 + [_i64] * 3 + [_vp] * 4
 _lib.oracle_gn_assemble.argtypes = [_vp] * 4 + [_i64, _i64, _vp, _vp]
 _lib.oracle_cholesky_solve.argtypes = [_vp, _vp, _vp, _i64]
 _lib.oracle_cholesky_solve.restype = _i
@@ -173,6 +174,24 @@ def gn_align(P, Twc, Xs, Cs, ii_edge, jj_edge, idx, valid, Q):
     _lib.oracle_gn_align(ctypes.byref(P), _p(Twc), _p(Xs), _p(Cs), _p(ii_edge), _p(jj_edge),
                          _p(idx), _p(valid), _p(Q), N, HW, E, _p(Hs), _p(gs))
     return Hs, gs
+
+
+def gn_residuals(P, Twc, Xs, Cs, ii_edge, jj_edge, idx, valid, Q):
+    """Per directed point-edge: T_ij Xj [E,HW,3], residuals [E,HW,4], robust weights [E,HW,4]
+    (3-row modes: the 4th is 0) and the validity flag [E,HW] of the align kernels."""
+    Twc, Xs, Cs = _c(Twc, np.float32), _c(Xs, np.float32), _c(Cs, np.float32)
+    ii_edge, jj_edge, idx = _c(ii_edge, np.int64), _c(jj_edge, np.int64), _c(idx, np.int64)
+    valid = _c(valid, np.uint8)
+    Q = _c(Q, np.float32)
+    N, HW = Xs.shape[0], Xs.shape[1]
+    E = ii_edge.shape[0]
+    X = np.zeros((E, HW, 3), np.float32)
+    err = np.zeros((E, HW, 4), np.float32)
+    w = np.zeros((E, HW, 4), np.float32)
+    vo = np.zeros((E, HW), np.uint8)
+    _lib.oracle_gn_residuals(ctypes.byref(P), _p(Twc), _p(Xs), _p(Cs), _p(ii_edge), _p(jj_edge),
+                             _p(idx), _p(valid), _p(Q), N, HW, E, _p(X), _p(err), _p(w), _p(vo))
+    return X, err, w, vo.astype(bool)
 
 
 def gn_assemble(Hs, gs, ii_opt, jj_opt, N):
