@@ -271,10 +271,22 @@ int m3s_pointmap_update(int mode, const float* T, const float* X_new, const floa
 
 /* ---------------- multi-GPU (RCCL over xGMI) ---------------- */
 
+/*
+ * Communicator of the edge-sharded GN op (m3s_gn_args.comm): every iteration the compact
+ * block-sparse system (f64) is sum-all-reduced in place before the replicated solve.  The
+ * reference is single-GPU (its solve runs in Eigen on the host, gn_kernels.cu:1201-1209);
+ * this is the seam SURVEY.md section 8(e) adds.
+ */
 #define M3S_COMM_ID_BYTES 128
-/* rank 0 creates the id, the caller broadcasts it (e.g. torch.distributed) */
+/* RCCL over xGMI (production).  Rank 0 creates the id, the caller broadcasts it (e.g.
+ * torch.distributed), every rank calls m3s_comm_init. */
 int m3s_comm_get_unique_id(void* id_out /* M3S_COMM_ID_BYTES */);
 int m3s_comm_init(const void* id, int nranks, int rank, void** comm_out);
+/* Host-callback collective (test hook): the library drains the stream, stages the `count`
+ * doubles in pinned host memory and calls fn(user, buf, count), which must replace buf with
+ * the element-wise sum over ranks (e.g. a torch.distributed gloo all_reduce) and return 0. */
+typedef int (*m3s_host_allreduce_fn)(void* user, double* buf, size_t count);
+int m3s_comm_init_host(m3s_host_allreduce_fn fn, void* user, int nranks, int rank, void** comm_out);
 int m3s_comm_destroy(void* comm);
 
 #ifdef __cplusplus

@@ -1,10 +1,18 @@
-// comm.hip -- RCCL (librccl.so.1, resolved with dlopen so the single-GPU path has no RCCL
-// dependency) for edge-sharded Gauss-Newton: one in-place f64 sum all-reduce of the
-// compact block-sparse system per iteration, enqueued on the GN stream (no host sync).
-// When torch is imported first, dlopen returns torch's already-loaded RCCL.
+// comm.hip -- the per-iteration collective of edge-sharded Gauss-Newton: one in-place f64 sum
+// all-reduce of the compact block-sparse system per iteration.
+//
+// A communicator handle is one of
+//   * RCCL (production): librccl.so.1 resolved with dlopen so the single-GPU path has no RCCL
+//     dependency; the all-reduce is enqueued on the GN stream (no host sync).  When torch is
+//     imported first, dlopen returns torch's already-loaded RCCL.
+//   * host callback (test hook, m3s_comm_init_host): the stream is drained, the buffer staged
+//     to pinned host memory, handed to the callback (e.g. a torch.distributed gloo
+//     all_reduce), and copied back.  Lets several processes sharing one GPU (or a CPU-only
+//     rehearsal of the exchange) run the product op's sharded path.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/m3s_backend.h"
@@ -53,16 +61,61 @@ Rccl* rccl() {
 
 const char* estr(Rccl* r, nccl_result_t e) { return (r && r->err_str) ? r->err_str(e) : "?"; }
 
+enum { kCommRccl = 1, kCommHost = 2 };
+constexpr unsigned kCommMagic = 0x6d33636du;  // "m3cm"
+
+struct Comm {
+    unsigned magic = kCommMagic;
+    int kind = 0;
+    int nranks = 1, rank = 0;
+    nccl_comm_t nccl = nullptr;
+    m3s_host_allreduce_fn fn = nullptr;
+    void* user = nullptr;
+    double* host = nullptr;  // pinned staging buffer (host kind)
+    size_t host_cap = 0;
+};
+
+Comm* as_comm(void* h) {
+    Comm* c = static_cast<Comm*>(h);
+    return (c && c->magic == kCommMagic) ? c : nullptr;
+}
+
 }  // namespace
 
 namespace m3s {
 int comm_allreduce_sum_f64(void* comm, double* buf, size_t count, hipStream_t stream) {
+    Comm* c = as_comm(comm);
+    if (!c) {
+        set_error("all-reduce: not an m3s communicator handle");
+        return M3S_ERR_COMM;
+    }
+    if (count == 0) return M3S_OK;
+    if (c->kind == kCommHost) {
+        if (c->host_cap < count) {
+            if (c->host) M3S_HIP_CHECK(hipHostFree(c->host));
+            c->host = nullptr;
+            c->host_cap = 0;
+            M3S_HIP_CHECK(hipHostMalloc((void**)&c->host, count * sizeof(double), hipHostMallocDefault));
+            c->host_cap = count;
+        }
+        M3S_HIP_CHECK(hipMemcpyAsync(c->host, buf, count * sizeof(double), hipMemcpyDeviceToHost, stream));
+        M3S_HIP_CHECK(hipStreamSynchronize(stream));
+        const int rc = c->fn(c->user, c->host, count);
+        if (rc != 0) {
+            set_error("host all-reduce callback failed (%d)", rc);
+            return M3S_ERR_COMM;
+        }
+        M3S_HIP_CHECK(hipMemcpyAsync(buf, c->host, count * sizeof(double), hipMemcpyHostToDevice, stream));
+        // the staging buffer is reused by the next call: the copy must have read it
+        M3S_HIP_CHECK(hipStreamSynchronize(stream));
+        return M3S_OK;
+    }
     Rccl* r = rccl();
     if (!r) {
         set_error("RCCL not available (dlopen librccl.so.1 failed)");
         return M3S_ERR_COMM;
     }
-    nccl_result_t e = r->all_reduce(buf, buf, count, kNcclFloat64, kNcclSum, (nccl_comm_t)comm, stream);
+    nccl_result_t e = r->all_reduce(buf, buf, count, kNcclFloat64, kNcclSum, c->nccl, stream);
     if (e != 0) {
         set_error("ncclAllReduce failed: %s", estr(r, e));
         return M3S_ERR_COMM;
@@ -95,18 +148,50 @@ extern "C" int m3s_comm_init(const void* id_in, int nranks, int rank, void** com
     }
     nccl_unique_id_t id;
     std::memcpy(id.internal, id_in, M3S_COMM_ID_BYTES);
-    nccl_comm_t c = nullptr;
-    nccl_result_t e = r->comm_init_rank(&c, nranks, id, rank);
+    M3S_REQUIRE(comm_out, "comm init: null output");
+    nccl_comm_t nc = nullptr;
+    nccl_result_t e = r->comm_init_rank(&nc, nranks, id, rank);
     if (e != 0) {
         m3s::set_error("ncclCommInitRank failed: %s", estr(r, e));
         return M3S_ERR_COMM;
     }
+    Comm* c = new Comm();
+    c->kind = kCommRccl;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->nccl = nc;
+    *comm_out = c;
+    return M3S_OK;
+}
+
+extern "C" int m3s_comm_init_host(m3s_host_allreduce_fn fn, void* user, int nranks, int rank,
+                                  void** comm_out) {
+    M3S_REQUIRE(fn && comm_out, "comm init (host): null callback or output");
+    M3S_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "comm init (host): bad rank %d of %d",
+                rank, nranks);
+    Comm* c = new Comm();
+    c->kind = kCommHost;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->fn = fn;
+    c->user = user;
     *comm_out = c;
     return M3S_OK;
 }
 
 extern "C" int m3s_comm_destroy(void* comm) {
-    Rccl* r = rccl();
-    if (!r || !r->comm_destroy) return M3S_ERR_COMM;
-    return r->comm_destroy((nccl_comm_t)comm) == 0 ? M3S_OK : M3S_ERR_COMM;
+    Comm* c = as_comm(comm);
+    if (!c) {
+        m3s::set_error("comm destroy: not an m3s communicator handle");
+        return M3S_ERR_COMM;
+    }
+    int rc = M3S_OK;
+    if (c->kind == kCommRccl) {
+        Rccl* r = rccl();
+        if (!r || !r->comm_destroy || r->comm_destroy(c->nccl) != 0) rc = M3S_ERR_COMM;
+    }
+    if (c->host) (void)hipHostFree(c->host);
+    c->magic = 0;
+    delete c;
+    return rc;
 }

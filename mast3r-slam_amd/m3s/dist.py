@@ -10,11 +10,15 @@ without a broadcast.
 
 The RCCL communicator is created by the backend library (``m3s_comm_init``) from a unique
 id that rank 0 broadcasts through ``torch.distributed`` (gloo or nccl process group).
+``HostComm`` plugs a ``torch.distributed`` all_reduce (e.g. gloo) into the same seam
+(``m3s_comm_init_host``): the op's sharded path then runs unchanged with several processes on
+one GPU -- the test hook for the exchange (tests/test_gpu_dist.py).
 """
 from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -57,8 +61,39 @@ class RcclComm:
             self.handle = None
 
 
+class HostComm:
+    """Host-callback communicator: each iteration the library hands the staged compact
+    system (f64, host memory) to ``dist.all_reduce(SUM)`` over ``group``."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.calls = 0
+
+        def _allreduce(user, buf, count):
+            try:
+                t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(count,)))
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+                self.calls += 1
+                return 0
+            except Exception:  # noqa: BLE001 -- reported as an m3s error code
+                return 1
+
+        self._fn = mb.HOST_ALLREDUCE_FN(_allreduce)  # keep the trampoline alive
+        h = ctypes.c_void_p()
+        mb._raise(mb.lib.m3s_comm_init_host(self._fn, None, self.world, self.rank, ctypes.byref(h)),
+                  "comm init (host)")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            mb.lib.m3s_comm_destroy(self.handle)
+            self.handle = None
+
+
 def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx_local, valid_local, Q_local, edge_offset,
-                         comm: RcclComm | None, max_iter, delta_thresh, **p):
+                         comm: RcclComm | HostComm | None, max_iter, delta_thresh, **p):
     """Sharded variant of gauss_newton_{rays,calib,points}: ``ii``/``jj`` hold ALL directed
     edges, ``idx_local``/``valid_local``/``Q_local`` the rank's range starting at
     ``edge_offset``.  Twc is updated in place identically on every rank."""

@@ -1,0 +1,135 @@
+"""The product's edge-sharded GN op with two ranks, on the one GPU of the box.
+
+Two spawned processes share cuda:0 and a gloo process group.  Each calls
+``m3s.dist.gauss_newton_sharded`` -- the same op as bench.py --gpus N, with its accumulate,
+the in-op per-iteration exchange of the compact block system and the replicated solve +
+retraction -- on its contiguous directed-edge range; the exchange goes through the library's
+host-callback communicator (``m3s_comm_init_host``: stream drained, system staged, gloo
+all_reduce, copied back) instead of RCCL, which needs one GPU per rank.
+
+Checked: Twc is bitwise identical on both ranks after 3 iterations (no broadcast in the op),
+the callback ran once per iteration, and the result equals the unsharded op to f64
+summation-reorder level (1e-6 relative; the shards' f64 partial systems are added in a
+different order than one process's chunk sums) and the oracle at the north-star 1e-5.
+Reference seam: global_opt.py:104-110 (two-way edges), gn_kernels.cu:1201-1209 (the solve).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+LOCAL = dict(sigma_ray=0.003, sigma_dist=10.0, sigma_pixel=1.0, sigma_depth=10.0,
+             C_conf=0.0, Q_conf=1.5, pixel_border=-10, depth_eps=1e-6)
+ITERS = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _graph(mode):
+    from m3s import synth
+
+    g = synth.make_graph("cfg2", H=96, W=128, seed=7)
+    if mode == "calib":
+        from m3s.geometry import constrain_points_to_ray
+
+        g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    return g
+
+
+def _params(g, mode):
+    p = dict(LOCAL)
+    if mode == "calib":
+        p.update(K=g.K.cuda(), height=g.H, width=g.W)
+    return p
+
+
+def _worker(rank, world, port, mode, out_q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mast3r-slam_amd")]
+    import torch.distributed as dist
+
+    from m3s.dist import HostComm, gauss_newton_sharded, shard_range
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        g = _graph(mode)
+        lo, hi = shard_range(g.ii.shape[0], world, rank)
+        c = lambda t: t.cuda().contiguous()
+        Twc = c(g.Twc)
+        comm = HostComm()
+        gauss_newton_sharded(mode, Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx[lo:hi]),
+                             c(g.valid[lo:hi]), c(g.Q[lo:hi]), lo, comm, ITERS, 0.0,
+                             **_params(g, mode))
+        torch.cuda.synchronize()
+        out_q.put((rank, Twc.cpu().numpy(), comm.calls, (lo, hi), None))
+        comm.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        out_q.put((rank, None, 0, None, repr(e)))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in res:
+        assert r[4] is None, r[4]
+    assert all(p.exitcode == 0 for p in procs)
+    (_, T0, calls0, rng0, _), (_, T1, calls1, rng1, _) = res
+    assert rng0[0] == 0 and rng0[1] == rng1[0] and rng0[1] > 0 and rng1[1] > rng1[0]
+    assert calls0 == calls1 == ITERS  # one exchange per iteration
+    # bitwise identical poses on every rank: same all-reduced system, same deterministic solve
+    assert np.array_equal(T0, T1)
+
+    g = _graph(mode)
+    c = lambda t: t.cuda()
+    Twc = c(g.Twc)
+    if mode == "rays":
+        backend.gauss_newton_rays(Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx), c(g.valid), c(g.Q),
+                                  LOCAL["sigma_ray"], LOCAL["sigma_dist"], LOCAL["C_conf"],
+                                  LOCAL["Q_conf"], ITERS, 0.0)
+        P = oracle.make_params("rays", LOCAL["sigma_ray"], LOCAL["sigma_dist"], LOCAL["C_conf"],
+                               LOCAL["Q_conf"], max_iter=ITERS, delta_thresh=0.0)
+    else:
+        backend.gauss_newton_calib(Twc, c(g.Xs), c(g.Cs), c(g.K), c(g.ii), c(g.jj), c(g.idx),
+                                   c(g.valid), c(g.Q), g.H, g.W, LOCAL["pixel_border"],
+                                   LOCAL["depth_eps"], LOCAL["sigma_pixel"], LOCAL["sigma_depth"],
+                                   LOCAL["C_conf"], LOCAL["Q_conf"], ITERS, 0.0)
+        P = oracle.make_params("calib", LOCAL["sigma_pixel"], LOCAL["sigma_depth"], LOCAL["C_conf"],
+                               LOCAL["Q_conf"], K=g.K.numpy(), height=g.H, width=g.W,
+                               pixel_border=LOCAL["pixel_border"], z_eps=LOCAL["depth_eps"],
+                               max_iter=ITERS, delta_thresh=0.0)
+    torch.cuda.synchronize()
+    T_full = Twc.cpu().numpy()
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    assert rel(T0, T_full) < 1e-6, rel(T0, T_full)
+    T_o, _, _ = oracle.gauss_newton(P, g.Twc.numpy(), g.Xs.numpy(), g.Cs.numpy(), g.ii.numpy(),
+                                    g.jj.numpy(), g.idx.numpy(), g.valid.numpy(), g.Q.numpy())
+    assert rel(T0, T_o) < 1e-5, rel(T0, T_o)

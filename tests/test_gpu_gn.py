@@ -315,3 +315,37 @@ def test_cfg3_bench_graph_10_iterations_within_1e5_of_oracle(backend, oracle):
     assert _rel(T_gpu, T_ref) < 1e-5, _rel(T_gpu, T_ref)
     # converged: the last update is tiny on both sides
     assert np.abs(dx_gpu).max() < 1e-4 and np.abs(dx_ref).max() < 1e-4
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_cfg1_keyframe_pair_matches_oracle(backend, oracle, mode):
+    """BASELINE config 1: one keyframe pair (N=2, E=1, 2 directed edges) at 512x384, 5 GN
+    iterations -- the smallest graph (a single 7-unknown system, pose 0 pinned)."""
+    g = synth.make_graph("cfg1", mode=mode)
+    if mode == "calib":
+        from m3s.geometry import constrain_points_to_ray
+
+        g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    T_g, dx_g = _run_gpu(backend, g, mode, 5)
+    T_o, dx_o, it = _run_oracle(oracle, g, mode, 5)
+    assert it == 5 and np.isfinite(T_g).all()
+    assert _rel(T_g, T_o) < 1e-5, _rel(T_g, T_o)
+    assert np.array_equal(T_g[0], g.Twc[0].numpy())  # pinned
+    assert np.abs(dx_g - dx_o).max() < 1e-5 * max(np.abs(T_o).max(), 1.0)
+
+
+@pytest.mark.timeout(400)
+def test_cfg4_full_size_one_iteration_and_ten_iteration_properties(backend, oracle):
+    """BASELINE config 4 at full size on one GPU (256 keyframes, 1024 pairs = 2048 directed
+    edges, 512x384, gauss_newton_rays): one iteration against the oracle at 1e-5, then the
+    timed 10-iteration call's properties -- finite, deterministic (two runs bitwise equal),
+    converging (the last update far below the first)."""
+    g = synth.make_graph("cfg4")
+    T1, _ = _run_gpu(backend, g, "rays", 1)
+    T_o, _, _ = _run_oracle(oracle, g, "rays", 1)
+    assert _rel(T1, T_o) < 1e-5, _rel(T1, T_o)
+    Ta, dxa = _run_gpu(backend, g, "rays", 10)
+    Tb, dxb = _run_gpu(backend, g, "rays", 10)
+    assert np.isfinite(Ta).all() and np.array_equal(Ta, Tb) and np.array_equal(dxa, dxb)
+    _, dx1 = _run_gpu(backend, g, "rays", 1)
+    assert np.abs(dxa).max() < 1e-2 * np.abs(dx1).max()
