@@ -55,7 +55,8 @@ int m3s_iter_proj(const float* rays, const float* pts, const float* p_init,
 
 /*
  * refine_matches -- replaces refine_matches (gn.cpp:101-114 -> matching_kernels.cu:84-116).
- *   D11 [B,H,W,F], D21 [B,N,F]  (fp16 bit patterns or f32)
+ *   D11 [B,H,W,F], D21 [B,N,F]  (fp16 bit patterns, f32 or f64: the reference's
+ *   AT_DISPATCH_FLOATING_TYPES_AND_HALF, matching_kernels.cu:103)
  *   p1  [B,N,2] i64 (u,v) -> p1_new [B,N,2] i64
  */
 int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
@@ -63,6 +64,10 @@ int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
                            int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
                            int radius, int dilation_max, void* stream);
 int m3s_refine_matches_f32(const float* D11, const float* D21,
+                           const int64_t* p1, int64_t* p1_new,
+                           int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
+                           int radius, int dilation_max, void* stream);
+int m3s_refine_matches_f64(const double* D11, const double* D21,
                            const int64_t* p1, int64_t* p1_new,
                            int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
                            int radius, int dilation_max, void* stream);

@@ -146,8 +146,8 @@ int chunk_points(int64_t HW, int nchunks) {
 }
 
 struct Layout {
-    size_t partials, edgeblk, compact, dense, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent, blk_ref,
-        grad_ptr, grad_ent, slotmap, linv, sched, pack, zs, total;
+    size_t partials, edgeblk, compact, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent, blk_ref, grad_ptr,
+        grad_ent, sched, pack, zs, total;
     int nchunks, npad, nblk_max;
 };
 
@@ -170,7 +170,9 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     static_assert(sizeof(float) * kRefStride <= sizeof(double) * kEdgeBlk, "edge record");
     L.edgeblk = take(sizeof(double) * (size_t)E_local * kEdgeBlk);
     L.compact = take(sizeof(double) * ((size_t)L.nblk_max * 28 + (size_t)npose * 7));
-    L.dense = take(sizeof(double) * (size_t)(L.npad + kCholTile) * L.npad);
+    // (the dense f64 matrices -- the dense solver's / debug system's (npad+64) x npad, the sparse
+    // solvers' core -- are sized by the solver actually used, in per-call stream-ordered
+    // allocations: see Ctx::alloc_dense and upload_sparse_plan)
     L.x = take(sizeof(double) * (size_t)L.npad);
     L.flags = take(sizeof(int) * kNumFlags);
     L.ii_loc = take(sizeof(int) * (size_t)E_local);
@@ -181,8 +183,6 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
     L.sched = take(sizeof(int) * (size_t)E_local * L.nchunks);
-    L.slotmap = take(sizeof(int) * (size_t)npose * npose);  // dense solver / debug only
-    L.linv = take(sizeof(double) * (size_t)L.npad * kCholTile);
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
     L.pack = take(8 * (size_t)E_local * (size_t)HW);
@@ -378,6 +378,7 @@ struct SparsePlan {
     std::vector<int> tc3, rc4;
     // device (one stream-ordered allocation per call)
     char* dbuf = nullptr;
+    size_t o_dense = 0, o_linv = 0;  // the dense core (npad_tail + 64) x npad_tail and its tile inverses
     // block-format system: b (npose x 7, padded to bpad doubles), then 49-f64 blocks
     int bpad = 0;
     size_t o_sys = 0, o_y = 0, o_L = 0, o_W = 0, o_xd = 0, o_Lg = 0, o_int = 0;
@@ -640,6 +641,10 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     sp.o_L = take(sizeof(double) * std::max(kLStoreRec, 49) * sp.nodes.size());
     sp.o_W = take(sizeof(double) * 49 * (size_t)sp.nW);
     sp.o_xd = take(sizeof(double) * (size_t)std::max(sp.npad_tail, 1));
+    if (sp.npad_tail > 0) {
+        sp.o_dense = take(sizeof(double) * (size_t)(sp.npad_tail + kCholTile) * sp.npad_tail);
+        sp.o_linv = take(sizeof(double) * (size_t)sp.npad_tail * kCholTile);
+    }
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
     // the plan integers in one array (layout: SparsePlan), the rounds after tmap
     std::vector<const std::vector<int>*> parts = {&sp.nodes, &sp.fptr, &sp.fronts, &sp.tail,
@@ -697,9 +702,12 @@ int validate(const m3s_gn_args& a) {
                 "gauss_newton: bad edge range");
     M3S_REQUIRE(a.HW < ((int64_t)1 << 31) && a.E_local < (1 << 30),
                 "gauss_newton: sizes exceed int32 indexing");
-    M3S_REQUIRE(7 * (a.N - 1) <= kMaxNpad,
-                "gauss_newton: %lld poses exceed the dense solve limit (%d unknowns)",
-                (long long)a.N, kMaxNpad);
+    // the dense solver (M3S_SOLVER_DENSE=1, diagnostics) factors the whole system; the sparse
+    // solvers check their dense core against the same limit after planning (run())
+    if (env_int("M3S_SOLVER_DENSE", 0) != 0 && a.order != M3S_GN_ORDER_REFERENCE)
+        M3S_REQUIRE(7 * (a.N - 1) <= kMaxNpad,
+                    "gauss_newton: %lld poses exceed the dense solve limit (%d unknowns)",
+                    (long long)a.N, kMaxNpad);
     M3S_REQUIRE(a.mode != M3S_GN_CALIB || (a.K != nullptr && a.width > 0 && a.height > 0),
                 "gauss_newton_calib: K / image size required");
     M3S_REQUIRE(a.Twc && a.Xs && a.Cs && a.dx, "gauss_newton: null pointer");
@@ -722,9 +730,36 @@ struct Ctx {
     AccParams P;
     bool vec;
     char* ws;
-    hipStream_t st;
+    hipStream_t st = nullptr;
+    // dense solver / debug system: (npad+64) x npad f64 matrix (RHS as a border row), its 64x64
+    // tile inverses and the (npose x npose) slot table, one stream-ordered allocation
+    char* dyn = nullptr;
+    size_t o_dense = 0, o_linv = 0, o_slot = 0;
     template <typename T>
     T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
+    template <typename T>
+    T* dyn_at(size_t off) const { return reinterpret_cast<T*>(dyn + off); }
+    int alloc_dense(int npad, int npose) {
+        size_t off = 0;
+        auto take = [&](size_t bytes) {
+            size_t o = off;
+            off = align_up(off + std::max<size_t>(bytes, 8), 256);
+            return o;
+        };
+        o_dense = take(sizeof(double) * (size_t)(npad + kCholTile) * npad);
+        o_linv = take(sizeof(double) * (size_t)npad * kCholTile);
+        o_slot = take(sizeof(int) * (size_t)npose * npose);
+        M3S_HIP_CHECK(hipMallocAsync((void**)&dyn, off, st));
+        return M3S_OK;
+    }
+    Ctx() = default;
+    Ctx(const Ctx&) = delete;
+    Ctx& operator=(const Ctx&) = delete;
+    // every return path of a call releases its per-call buffers (stream-ordered)
+    ~Ctx() {
+        if (sp.dbuf) (void)hipFreeAsync(sp.dbuf, st);
+        if (dyn) (void)hipFreeAsync(dyn, st);
+    }
 };
 
 int setup(const m3s_gn_args& a, Ctx& c) {
@@ -750,6 +785,10 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     {
         const size_t lo = L.flags, hi = L.sched + sizeof(int) * p.sched.size();
         const size_t nslot = c.need_slotmap ? p.slotmap.size() : 0;
+        if (c.need_slotmap) {
+            rc = c.alloc_dense(L.npad, (int)std::max<int64_t>(a.N - 1, 0));
+            if (rc) return rc;
+        }
         char* h = g_stage_ws.get(hi - lo + sizeof(int) * nslot);
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
         std::memset(h, 0, L.ii_loc - lo);  // flags
@@ -772,7 +811,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
         M3S_HIP_CHECK(hipMemcpyAsync(c.ws + lo, h, hi - lo, hipMemcpyHostToDevice, c.st));
         if (nslot) {  // the dense (npose x npose) slot table
             std::memcpy(h + (hi - lo), p.slotmap.data(), sizeof(int) * nslot);
-            M3S_HIP_CHECK(hipMemcpyAsync(c.ws + L.slotmap, h + (hi - lo), sizeof(int) * nslot,
+            M3S_HIP_CHECK(hipMemcpyAsync(c.dyn + c.o_slot, h + (hi - lo), sizeof(int) * nslot,
                                          hipMemcpyHostToDevice, c.st));
         }
         M3S_HIP_CHECK(g_stage_ws.mark(c.st));
@@ -921,9 +960,9 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     const int npose = (int)(a.N - 1);
     int* flags = c.at<int>(L.flags);
     if (!c.sp.enabled) {
-        M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.at<int>(L.slotmap), c.plan.nblk,
-                                   npose, 7 * npose, L.npad, c.at<double>(L.dense),
-                                   c.at<double>(L.linv), c.at<double>(L.x), flags));
+        M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.dyn_at<int>(c.o_slot), c.plan.nblk,
+                                   npose, 7 * npose, L.npad, c.dyn_at<double>(c.o_dense),
+                                   c.dyn_at<double>(c.o_linv), c.at<double>(L.x), flags));
         return M3S_OK;
     }
     SparsePlan& sp = c.sp;
@@ -1011,8 +1050,8 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         // core is first laid out densely by a many-workgroup fill (one CU gathering it block by
         // block took ~28 us)
         M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail),
-                                          sp.ntail, sp.npad_tail, c.at<double>(L.dense), flags));
-        S.Hd = sp.ntail > 0 ? c.at<double>(L.dense) : nullptr;
+                                          sp.ntail, sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
+        S.Hd = sp.ntail > 0 ? sp.dptr<double>(sp.o_dense) : nullptr;
         S.npad_h = sp.npad_tail;
         S.nmeta = (int)sp.nints_back;
         S.meta_lds = 1;
@@ -1022,7 +1061,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         return M3S_OK;
     }
     M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
-                                 sp.npad_tail, c.at<double>(L.dense), c.at<double>(L.linv),
+                                 sp.npad_tail, sp.dptr<double>(sp.o_dense), sp.dptr<double>(sp.o_linv),
                                  sp.dptr<double>(sp.o_xd), x, flags));
     for (auto it = sp.rounds.rbegin(); it != sp.rounds.rend(); ++it)
         M3S_HIP_CHECK(launch_sp_back(c.st, it->nnodes, sp.iptr(sp.i_nodes), sp.iptr(sp.i_fptr),
@@ -1075,6 +1114,9 @@ int run(const m3s_gn_args& a) {
             c.sp.hybrid = hyb;
         }
         t2 = now();
+        M3S_REQUIRE(c.sp.npad_tail <= kMaxNpad,
+                    "gauss_newton: the dense core of the elimination (%d unknowns) exceeds the "
+                    "dense solve limit (%d)", c.sp.npad_tail, kMaxNpad);
         rc = upload_sparse_plan(c.sp, npose, c.st);
         if (rc) return rc;
         t3 = now();
@@ -1096,7 +1138,7 @@ int run(const m3s_gn_args& a) {
                                          a.delta_thresh, flags));
         g_prof.mark(c.st);
     }
-    if (c.sp.dbuf) M3S_HIP_CHECK(hipFreeAsync(c.sp.dbuf, c.st));
+    // (the per-call solver buffers are released by ~Ctx on this and every error path)
     if (env_int("M3S_GN_DEBUG_FLAGS", 0)) {  // diagnostics: the device flags after the call
         int hf[kNumFlags];
         M3S_HIP_CHECK(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c.st));
@@ -1231,12 +1273,12 @@ extern "C" int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, doub
     rc = enqueue_system(a, c);
     if (rc) return rc;
     const Layout& L = c.L;
-    M3S_HIP_CHECK(launch_fill_only(c.st, c.at<double>(L.compact), c.at<int>(L.slotmap), c.plan.nblk,
-                                   npose, n, L.npad, c.at<double>(L.dense), c.at<int>(L.flags)));
-    M3S_HIP_CHECK(hipMemcpy2DAsync(H_host, sizeof(double) * n, c.at<double>(L.dense),
+    M3S_HIP_CHECK(launch_fill_only(c.st, c.at<double>(L.compact), c.dyn_at<int>(c.o_slot), c.plan.nblk,
+                                   npose, n, L.npad, c.dyn_at<double>(c.o_dense), c.at<int>(L.flags)));
+    M3S_HIP_CHECK(hipMemcpy2DAsync(H_host, sizeof(double) * n, c.dyn_at<double>(c.o_dense),
                                    sizeof(double) * L.npad, sizeof(double) * n, n,
                                    hipMemcpyDeviceToHost, c.st));
-    M3S_HIP_CHECK(hipMemcpyAsync(b_host, c.at<double>(L.dense) + (size_t)L.npad * L.npad,
+    M3S_HIP_CHECK(hipMemcpyAsync(b_host, c.dyn_at<double>(c.o_dense) + (size_t)L.npad * L.npad,
                                  sizeof(double) * n, hipMemcpyDeviceToHost, c.st));
     M3S_HIP_CHECK(hipStreamSynchronize(c.st));
     return M3S_OK;

@@ -139,8 +139,9 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
 // cuda::std::numeric_limits<c10::Half>::min() is value-initialised (no libcu++
 // specialisation for c10::Half) => 0.0.  Single named constant, see DESIGN.md.
 constexpr float kRefineHalfMaxInit = 0.0f;
-// For float the limits are specialised: FLT_MIN.
+// For float and double the limits are specialised: FLT_MIN, DBL_MIN.
 constexpr float kRefineFloatMaxInit = 1.17549435e-38f;
+constexpr double kRefineDoubleMaxInit = 2.2250738585072014e-308;
 
 __device__ __forceinline__ bool inside_image(int64_t u, int64_t v, int W, int H) {
     return v >= 0 && v < H && u >= 0 && u < W;  // matching_kernels.cu:17-19
@@ -281,19 +282,22 @@ __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
     p1_new[g * 2 + 1] = v_new;
 }
 
-// Generic F (any descriptor width), fp16 or f32, scalar loads.
+// Generic F (any descriptor width), fp16, f32 or f64 (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
+// matching_kernels.cu:103), scalar loads.
 template <typename T>
 __device__ __forceinline__ T zero_score();
 template <>
 __device__ __forceinline__ half_t zero_score<half_t>() { return (half_t)0.0f; }
 template <>
 __device__ __forceinline__ float zero_score<float>() { return 0.0f; }
+template <>
+__device__ __forceinline__ double zero_score<double>() { return 0.0; }
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void refine_generic_kernel(
     const T* __restrict__ D11, const T* __restrict__ D21, const int64_t* __restrict__ p1,
     int64_t* __restrict__ p1_new, int H, int W, int64_t N, int64_t F, int64_t total, int radius,
-    int dilation_max, float max_init) {
+    int dilation_max, T max_init) {
     const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (g >= total) return;
     const int64_t b = g / N;
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void refine_generic_kernel(
     const T* __restrict__ img = D11 + b * (int64_t)H * W * F;
     int64_t u0 = p1[g * 2 + 0];
     int64_t v0 = p1[g * 2 + 1];
-    T max_score = (T)max_init;
+    T max_score = max_init;
     int64_t u_new = u0, v_new = v0;
     const int S = 2 * radius + 1;
     for (int d = dilation_max; d > 0; d--) {
@@ -391,7 +395,7 @@ extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, 
         hipLaunchKernelGGL(refine_generic_kernel<half_t>, dim3(grid_for(total)), dim3(kBlock), 0,
                            (hipStream_t)stream, reinterpret_cast<const half_t*>(D11),
                            reinterpret_cast<const half_t*>(D21), p1, p1_new, (int)H, (int)W, N, F,
-                           total, radius, dilation_max, kRefineHalfMaxInit);
+                           total, radius, dilation_max, (half_t)kRefineHalfMaxInit);
     }
     M3S_LAUNCH_CHECK();
     return M3S_OK;
@@ -407,6 +411,20 @@ extern "C" int m3s_refine_matches_f32(const float* D11, const float* D21, const 
     hipLaunchKernelGGL(refine_generic_kernel<float>, dim3(grid_for(total)), dim3(kBlock), 0,
                        (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, F, total,
                        radius, dilation_max, kRefineFloatMaxInit);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+}
+
+extern "C" int m3s_refine_matches_f64(const double* D11, const double* D21, const int64_t* p1,
+                                      int64_t* p1_new, int64_t B, int64_t H, int64_t W, int64_t N,
+                                      int64_t F, int radius, int dilation_max, void* stream) {
+    int rc = refine_checks(D11, D21, p1, p1_new, B, H, W, N, F, radius, dilation_max);
+    if (rc) return rc;
+    const int64_t total = B * N;
+    if (total == 0) return M3S_OK;
+    hipLaunchKernelGGL(refine_generic_kernel<double>, dim3(grid_for(total)), dim3(kBlock), 0,
+                       (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, F, total,
+                       radius, dilation_max, kRefineDoubleMaxInit);
     M3S_LAUNCH_CHECK();
     return M3S_OK;
 }

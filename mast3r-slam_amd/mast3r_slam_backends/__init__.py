@@ -55,6 +55,7 @@ lib.m3s_version.restype = ctypes.c_char_p
 lib.m3s_iter_proj.argtypes = [_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _vp]
 lib.m3s_refine_matches_f16.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_refine_matches_f32.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
+lib.m3s_refine_matches_f64.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_gn_workspace_bytes.restype = ctypes.c_size_t
 lib.m3s_gn_workspace_bytes.argtypes = [_i, _c_int64, _c_int64, _c_int64, _c_int64]
 
@@ -220,7 +221,8 @@ def refine_matches(D11, D21, p1, window_size, dilation_max):
     """gn.cpp:101-114 / matching_kernels.cu:84-116 -> [p1_new i64[B,N,2]].
 
     ``window_size`` is the search radius (config ``matching.radius``)."""
-    _check(D11, "D11", (torch.float16, torch.float32), 4)
+    # AT_DISPATCH_FLOATING_TYPES_AND_HALF (matching_kernels.cu:103): half, float, double
+    _check(D11, "D11", (torch.float16, torch.float32, torch.float64), 4)
     _check(D21, "D21", D11.dtype, 3)
     _check(p1, "p1", torch.int64, 3)
     dev = _on_device(D11=D11, D21=D21, p1=p1)
@@ -229,7 +231,8 @@ def refine_matches(D11, D21, p1, window_size, dilation_max):
     if p1.shape[2] != 2 or D21.shape[0] != Bq or D21.shape[1] != N or D21.shape[2] != F or Bq != B:
         raise RuntimeError("refine_matches: expected D11 [B,H,W,F], D21 [B,N,F], p1 [B,N,2]")
     p1_new = torch.zeros((Bq, N, 2), dtype=p1.dtype, device=dev)
-    fn = lib.m3s_refine_matches_f16 if D11.dtype == torch.float16 else lib.m3s_refine_matches_f32
+    fn = {torch.float16: lib.m3s_refine_matches_f16, torch.float32: lib.m3s_refine_matches_f32,
+          torch.float64: lib.m3s_refine_matches_f64}[D11.dtype]
     with torch.cuda.device(dev):
         rc = fn(
             _ptr(D11), _ptr(D21), _ptr(p1), _ptr(p1_new), B, H, W, N, F,

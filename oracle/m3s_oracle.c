@@ -238,46 +238,51 @@ void oracle_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
     }
 }
 
-void oracle_refine_matches_f32(const float* D11, const float* D21,
-                               const int64_t* p1, int64_t* p1_new,
-                               int64_t B, int64_t H, int64_t W, int64_t N,
-                               int64_t F, int radius, int dilation_max) {
-    const int64_t total = B * N;
-#pragma omp parallel for schedule(dynamic, 256)
-    for (int64_t g = 0; g < total; g++) {
-        const int64_t b = g / N;
-        const float* d21 = D21 + g * F;
-        int64_t u0 = p1[g * 2 + 0];
-        int64_t v0 = p1[g * 2 + 1];
-        /* For scalar_t = float the limits ARE specialised: min() = FLT_MIN. */
-        float max_score = 1.17549435e-38f;
-        int64_t u_new = u0, v_new = v0;
-        for (int d = dilation_max; d > 0; d--) {
-            const int rd = radius * d;
-            const int diam = 2 * rd + 1;
-            for (int i = 0; i < diam; i += d) {
-                for (int j = 0; j < diam; j += d) {
-                    const int64_t u = u0 - rd + i;
-                    const int64_t v = v0 - rd + j;
-                    if (inside_image(u, v, W, H)) {
-                        const float* d11 = D11 + ((b * H + v) * W + u) * F;
-                        float score = 0.0f;
-                        for (int64_t k = 0; k < F; k++) score += d21[k] * d11[k];
-                        if (score > max_score) {
-                            max_score = score;
-                            u_new = u;
-                            v_new = v;
-                        }
-                    }
-                }
-            }
-            u0 = u_new;
-            v0 = v_new;
-        }
-        p1_new[g * 2 + 0] = u_new;
-        p1_new[g * 2 + 1] = v_new;
+/* refine_matches_kernel<float> / <double>: the same loop in the accumulator type T, with
+ * max_score starting at numeric_limits<T>::min() (specialised for float and double: FLT_MIN,
+ * DBL_MIN).  matching_kernels.cu:25-81, dispatched by AT_DISPATCH_FLOATING_TYPES_AND_HALF
+ * (:103). */
+#define ORACLE_REFINE_REAL(NAME, T, MIN_INIT)                                               \
+    void NAME(const T* D11, const T* D21, const int64_t* p1, int64_t* p1_new, int64_t B,     \
+              int64_t H, int64_t W, int64_t N, int64_t F, int radius, int dilation_max) {     \
+        const int64_t total = B * N;                                                          \
+        _Pragma("omp parallel for schedule(dynamic, 256)")                                   \
+        for (int64_t g = 0; g < total; g++) {                                                 \
+            const int64_t b = g / N;                                                          \
+            const T* d21 = D21 + g * F;                                                       \
+            int64_t u0 = p1[g * 2 + 0];                                                       \
+            int64_t v0 = p1[g * 2 + 1];                                                       \
+            T max_score = MIN_INIT;                                                           \
+            int64_t u_new = u0, v_new = v0;                                                   \
+            for (int d = dilation_max; d > 0; d--) {                                          \
+                const int rd = radius * d;                                                    \
+                const int diam = 2 * rd + 1;                                                  \
+                for (int i = 0; i < diam; i += d) {                                           \
+                    for (int j = 0; j < diam; j += d) {                                       \
+                        const int64_t u = u0 - rd + i;                                        \
+                        const int64_t v = v0 - rd + j;                                        \
+                        if (inside_image(u, v, W, H)) {                                       \
+                            const T* d11 = D11 + ((b * H + v) * W + u) * F;                   \
+                            T score = 0;                                                      \
+                            for (int64_t k = 0; k < F; k++) score += d21[k] * d11[k];         \
+                            if (score > max_score) {                                          \
+                                max_score = score;                                            \
+                                u_new = u;                                                    \
+                                v_new = v;                                                    \
+                            }                                                                 \
+                        }                                                                     \
+                    }                                                                         \
+                }                                                                             \
+                u0 = u_new;                                                                   \
+                v0 = v_new;                                                                   \
+            }                                                                                 \
+            p1_new[g * 2 + 0] = u_new;                                                        \
+            p1_new[g * 2 + 1] = v_new;                                                        \
+        }                                                                                     \
     }
-}
+
+ORACLE_REFINE_REAL(oracle_refine_matches_f32, float, 1.17549435e-38f)
+ORACLE_REFINE_REAL(oracle_refine_matches_f64, double, 2.2250738585072014e-308)
 
 /* ------------------------------------------------------------------------ */
 /* Sim3 device library (gn_kernels.cu:172-413), restated in float           */

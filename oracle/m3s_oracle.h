@@ -49,6 +49,11 @@ void oracle_refine_matches_f32(const float* D11, const float* D21,
                                const int64_t* p1, int64_t* p1_new,
                                int64_t B, int64_t H, int64_t W, int64_t N,
                                int64_t F, int radius, int dilation_max);
+/* matching_kernels.cu:25-81 (refine_matches_kernel<double>) */
+void oracle_refine_matches_f64(const double* D11, const double* D21,
+                               const int64_t* p1, int64_t* p1_new,
+                               int64_t B, int64_t H, int64_t W, int64_t N,
+                               int64_t F, int radius, int dilation_max);
 
 /* fp16 helpers (c10::Half semantics: round-to-nearest-even, subnormals kept) */
 uint16_t oracle_f32_to_f16(float f);

@@ -29,6 +29,7 @@ _vp, _i64, _i, _f = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_floa
 _lib.oracle_iter_proj.argtypes = [_vp] * 5 + [_i64] * 4 + [_i, _f, _f]
 _lib.oracle_refine_matches_f16.argtypes = [_vp] * 4 + [_i64] * 5 + [_i, _i]
 _lib.oracle_refine_matches_f32.argtypes = [_vp] * 4 + [_i64] * 5 + [_i, _i]
+_lib.oracle_refine_matches_f64.argtypes = [_vp] * 4 + [_i64] * 5 + [_i, _i]
 _lib.oracle_f32_to_f16.restype = ctypes.c_uint16
 _lib.oracle_f32_to_f16.argtypes = [_f]
 _lib.oracle_f16_to_f32.restype = _f
@@ -127,6 +128,11 @@ def refine_matches(D11, D21, p1, radius, dilation_max):
         d11 = _c(D11, np.float16).view(np.uint16)
         d21 = _c(D21, np.float16).view(np.uint16)
         _lib.oracle_refine_matches_f16(_p(d11), _p(d21), _p(p1), _p(out), B, H, W, N, F,
+                                       int(radius), int(dilation_max))
+    elif D11.dtype == np.float64:
+        d11 = _c(D11, np.float64)
+        d21 = _c(D21, np.float64)
+        _lib.oracle_refine_matches_f64(_p(d11), _p(d21), _p(p1), _p(out), B, H, W, N, F,
                                        int(radius), int(dilation_max))
     else:
         d11 = _c(D11, np.float32)

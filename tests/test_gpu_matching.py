@@ -79,7 +79,8 @@ def test_refine_matches_f16_bit_exact(backend, oracle, B, H, W):
     assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
 
 
-@pytest.mark.parametrize("dtype,F", [(torch.float16, 24), (torch.float16, 5), (torch.float32, 24), (torch.float32, 3)])
+@pytest.mark.parametrize("dtype,F", [(torch.float16, 24), (torch.float16, 5), (torch.float32, 24), (torch.float32, 3),
+                                     (torch.float64, 24), (torch.float64, 7)])
 def test_refine_matches_generic(backend, oracle, dtype, F):
     g = torch.Generator().manual_seed(F)
     B, H, W, N = 2, 13, 17, 40

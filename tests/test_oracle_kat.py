@@ -314,3 +314,54 @@ def test_cholesky_solve_and_failure(oracle):
     H2[:, 5] = 0
     x2, rc2 = oracle.cholesky_solve(H2, b)
     assert rc2 == 1 and np.all(x2 == 0)
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_oracle_residuals_match_reference_python(oracle, mode):
+    """The oracle's per-point residual model (the align kernels restated, gn_kernels.cu:905-978
+    rays, :1346-1410 calib) against the reference's own Python statement of it, evaluated by
+    tests/golden/make_residual_golden.py on the same points: point_to_ray_dist / project_calib
+    (geometry.py:17-104) and huber (nonlinear_optimizer.py:28-33).
+      * validity (match, Q, C, image border, depth) exactly;
+      * residuals to 2 ulps of the operands' magnitude: the unit ray's (1) for the ray rows, the
+        distance / log-depth terms, and |u| + cx (|v| + cy) for the pixel rows -- the kernel
+        and the torch front end form u as fx*(x/z)+cx vs (fx*x+cx*z)/z and the norms
+        differently, then cancel;
+      * weights on identical residuals to 4 ulps (the kernel's huber divides k/|r| in double,
+        torch multiplies by the reciprocal)."""
+    import os
+
+    O = oracle
+    G = np.load(os.path.join(os.path.dirname(__file__), "golden", "residual_golden.npz"))
+    g = lambda k: G[f"{mode}_{k}"]
+    H, W = (int(v) for v in g("hw"))
+    if mode == "rays":
+        P = O.make_params("rays", 0.003, 10.0, 0.0, 1.5)
+    else:
+        P = O.make_params("calib", 1.0, 10.0, 0.0, 1.5, K=g("K"), height=H, width=W,
+                          pixel_border=-10, z_eps=1e-6)
+    ie, je, _ = O.remap(g("ii"), g("jj"))
+    X, err, w, valid = O.gn_residuals(P, g("Twc"), g("Xs"), g("Cs"), ie, je, g("idx"), g("valid"), g("Q"))
+    assert np.array_equal(X, g("Xj_Ci"))  # the fixture's reference functions saw these points
+    ok = g("validity_ref")
+    assert np.array_equal(valid, ok)
+    assert 0.5 < ok.mean() < 1.0  # both valid and rejected points are covered
+    R = int(g("rows"))
+    scale = g("err_scale").copy()
+    if mode == "rays":
+        scale[..., :3] = 1.0
+    else:
+        K = g("K")
+        scale[..., 0] += abs(K[0, 2])
+        scale[..., 1] += abs(K[1, 2])
+    d = np.abs(err[..., :R] - g("err_ref"))[ok]
+    assert (d <= 2 * np.spacing(scale[ok])).all(), (d / np.spacing(scale[ok])).max()
+    w_ref = g("w_ref_on_oracle_err")
+    dw = np.abs(w[..., :R] - w_ref)
+    assert (dw[ok] <= 4 * np.spacing(np.abs(w_ref[ok]))).all()
+    assert np.all(w[..., :R][~ok] == 0) and np.all(w_ref[~ok] == 0)
+    # both branches of huber (weight 1 and k/|r|) were exercised
+    s_inv = np.float32(1.0 / (0.003 if mode == "rays" else 1.0))
+    full = (s_inv * np.sqrt(g("Q")[..., 0])) ** 2
+    down = w_ref[..., 0] < np.float32(0.999) * full
+    assert down[ok].any() and (~down[ok]).any()
