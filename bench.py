@@ -246,6 +246,17 @@ def matching_bench(dev, reps=10):
             if r >= 2:
                 t_ip += ev[0].elapsed_time(ev[1]) / reps
                 t_rf += ev[1].elapsed_time(ev[2]) / reps
+        # A/B: the LDS-tiled refine kernel (M3S_REFINE_LDS=1, opt-in) vs the default gather kernel
+        os.environ["M3S_REFINE_LDS"] = "1"
+        t_gather = 0.0
+        for r in range(reps + 2):
+            ev[1].record()
+            mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r >= 2:
+                t_gather += ev[1].elapsed_time(ev[2]) / reps
+        del os.environ["M3S_REFINE_LDS"]
         for _ in range(2):
             match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init)
         torch.cuda.synchronize()
@@ -260,6 +271,7 @@ def matching_bench(dev, reps=10):
             "pairs_per_s_glue": B / (t_glue * 1e-3),
             "iter_proj_ms": t_ip,
             "refine_ms": t_rf,
+            "refine_lds_tile_kernel_ms": t_gather,
             "match_iterative_proj_ms": t_glue,
             "iter_proj_GBps": 65 * npx / (t_ip * 1e-3) / 1e9,
             "refine_GBps": 128 * npx / (t_rf * 1e-3) / 1e9,

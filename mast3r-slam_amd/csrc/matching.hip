@@ -14,7 +14,9 @@
 // so the bilinear / window gathers of a wave hit the same L1/L2 lines.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/m3s_backend.h"
 #include "m3s_common.h"
@@ -199,6 +201,32 @@ __device__ __forceinline__ half_t score_f16(const half2_t (&q2)[F / 2], const ui
     return score;
 }
 
+// SC candidates' scores at once, each exactly score_f16 (the same per-candidate sequence of
+// roundings), but with the k loop outermost so the SC dependent add chains interleave: a
+// single chain is one dependent v_add_f16 after another, and the compiler does not interleave
+// independent chains on its own.
+template <int F, int SC>
+__device__ __forceinline__ void score_f16_multi(const half2_t (&q2)[F / 2], const uint4 (&rows)[SC][F / 8],
+                                                half_t (&score)[SC]) {
+#pragma unroll
+    for (int j = 0; j < SC; j++) score[j] = (half_t)0.0f;
+#pragma unroll
+    for (int c = 0; c < F / 8; c++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            half2_t p[SC];
+#pragma unroll
+            for (int j = 0; j < SC; j++) p[j] = q2[c * 4 + k] * reinterpret_cast<const half2_t*>(&rows[j][c])[k];
+#pragma unroll
+            for (int j = 0; j < SC; j++) score[j] = score[j] + p[j].x;
+            __builtin_amdgcn_sched_barrier(0);  // keep the chains interleaved (see above)
+#pragma unroll
+            for (int j = 0; j < SC; j++) score[j] = score[j] + p[j].y;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 // F = 24 fp16 fast path: the query descriptor lives in registers (3 x 16 B loads), each
 // candidate row is 48 B = 3 x dwordx4.  R = radius when it is a compile-time constant (the
 // window column of 2R+1 candidates is unrolled: its loads are issued together and the
@@ -248,11 +276,12 @@ __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
 #pragma unroll
                     for (int c = 0; c < F / 8; c++) rows[j][c] = src[c];
                 }
+                half_t score[SC];
+                score_f16_multi<F, SC>(q2, rows, score);
 #pragma unroll
                 for (int j = 0; j < SC; j++) {
-                    const half_t score = score_f16<F>(q2, rows[j]);
-                    if (ok[j] && score > max_score) {
-                        max_score = score;
+                    if (ok[j] && score[j] > max_score) {
+                        max_score = score[j];
                         u_new = u;
                         v_new = v0 - rd + (int64_t)j * d;
                     }
@@ -280,6 +309,223 @@ __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
     }
     p1_new[g * 2 + 0] = u_new;
     p1_new[g * 2 + 1] = v_new;
+}
+
+// ---------------------------------------------------------------------------------
+// refine_matches, LDS-tiled (F = 24 fp16, radius 3): opt-in (M3S_REFINE_LDS=1), measured slower.
+//
+// The gather kernel above reads every candidate row (48 B) through the vector L1 / texture path:
+// 735 dwordx4 gathers per pixel, ~16 TA cycles each per wave -- the PMC profile shows it
+// issue-stalled (SQ_WAIT_INST_ANY 72 % of wave cycles), not arithmetic-bound.  Here a
+// 512-thread workgroup takes a 32x16 pixel tile; for each dilation level it
+// stages, once, the descriptor rows of the bounding box of all its pixels' (image-clipped)
+// candidate windows into LDS (row by row, coalesced 16-B loads), then every pixel scores its
+// candidates from LDS (3 x ds_read_b128 per candidate).  Same candidate order, same c10::Half
+// arithmetic (score_f16), same strict '>' updates => bitwise the gather kernel's result.  A
+// level whose box exceeds the LDS budget (widely scattered matches) reads the candidates from
+// global memory for that level only.  Measured (MI355X, bench data = GT matches +- 2 px per
+// pixel): 0.93-0.96 vs 0.86 ms for 8 pairs: one 158-KB workgroup per CU leaves 2 waves per SIMD
+// waiting on LDS (SQ_WAIT_ANY 64 %), the per-pixel +-2 px jitter makes the ds_read_b128s 2-way
+// bank-conflicted on average, and every level's staging is a workgroup-wide stall; prefetching
+// the next window column's rows (two register buffers) did not change it.
+// ---------------------------------------------------------------------------------
+constexpr int kLdsTx = 32, kLdsTy = 16, kLdsThreads = kLdsTx * kLdsTy;
+constexpr int kLdsCapPx = 3300;  // 3300 x 48 B = 158,400 B of the CU's 160 KiB
+struct LdsTileMap {
+    int tiles_x, tiles_y, ntiles;  // per image
+};
+
+__device__ __forceinline__ void block_minmax4(int (&v)[4], int* red /* [8 waves][4] */) {
+    // v[0], v[2] reduced with min, v[1], v[3] with max, over the workgroup
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        v[0] = min(v[0], __shfl_xor(v[0], off, 64));
+        v[1] = max(v[1], __shfl_xor(v[1], off, 64));
+        v[2] = min(v[2], __shfl_xor(v[2], off, 64));
+        v[3] = max(v[3], __shfl_xor(v[3], off, 64));
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[wave * 4 + 0] = v[0];
+        red[wave * 4 + 1] = v[1];
+        red[wave * 4 + 2] = v[2];
+        red[wave * 4 + 3] = v[3];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kLdsThreads / 64; w++) {
+        v[0] = min(v[0], red[w * 4 + 0]);
+        v[1] = max(v[1], red[w * 4 + 1]);
+        v[2] = min(v[2], red[w * 4 + 2]);
+        v[3] = max(v[3], red[w * 4 + 3]);
+    }
+}
+
+template <int F, int R>
+__global__ __launch_bounds__(kLdsThreads) void refine_lds_kernel(
+    const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21,
+    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int H, int W, int64_t B,
+    LdsTileMap tm, int dilation_max, int* __restrict__ stats) {
+    static_assert(F == 24, "LDS tile path is for 24-d fp16 descriptors (48-B rows)");
+    constexpr int SC = 2 * R + 1;
+    constexpr int RU4 = F / 8;  // uint4 per descriptor row
+    __shared__ uint4 tile[kLdsCapPx * RU4];
+    __shared__ int red[(kLdsThreads / 64) * 4];
+
+    // XCD-banded tile order, as refine_f16_kernel
+    const int64_t nblk = (int64_t)gridDim.x;
+    const int64_t blk = blockIdx.x;
+    const int64_t per = (nblk + 7) / 8;
+    const int64_t lb = (blk % 8) * per + blk / 8;
+    if (lb >= (int64_t)tm.ntiles * B) return;  // block-uniform
+    const int64_t b = lb / tm.ntiles;
+    const int t = (int)(lb - b * tm.ntiles);
+    const int ty = t / tm.tiles_x, tx = t - ty * tm.tiles_x;
+    const int lx = threadIdx.x & (kLdsTx - 1), ly = threadIdx.x / kLdsTx;
+    const int pu = tx * kLdsTx + lx, pv = ty * kLdsTy + ly;
+    const bool active = pu < W && pv < H;
+    const int64_t N = (int64_t)H * W;
+    const int64_t g = b * N + (int64_t)pv * W + pu;
+    const uint16_t* __restrict__ img = D11 + b * N * F;
+
+    half2_t q2[F / 2];
+    int64_t u0 = 0, v0 = 0;
+    if (active) {
+        const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
+#pragma unroll
+        for (int c = 0; c < RU4; c++) {
+            uint4 w = src[c];
+            const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
+#pragma unroll
+            for (int k = 0; k < 4; k++) q2[c * 4 + k] = hp[k];
+        }
+        u0 = p1[g * 2 + 0];
+        v0 = p1[g * 2 + 1];
+    }
+    half_t max_score = (half_t)kRefineHalfMaxInit;
+    int64_t u_new = u0, v_new = v0;
+    int n_global_levels = 0;
+
+    for (int d = dilation_max; d > 0; d--) {
+        const int64_t rd = (int64_t)R * d;
+        // this pixel's candidate window clipped to the image (empty: lo > hi)
+        int w4[4] = {INT_MAX, INT_MIN, INT_MAX, INT_MIN};
+        if (active) {
+            const int64_t ulo = max(u0 - rd, (int64_t)0), uhi = min(u0 + rd, (int64_t)W - 1);
+            const int64_t vlo = max(v0 - rd, (int64_t)0), vhi = min(v0 + rd, (int64_t)H - 1);
+            if (ulo <= uhi && vlo <= vhi) {
+                w4[0] = (int)ulo;
+                w4[1] = (int)uhi;
+                w4[2] = (int)vlo;
+                w4[3] = (int)vhi;
+            }
+        }
+        block_minmax4(w4, red);
+        const int umin = w4[0], umax = w4[1], vmin = w4[2], vmax = w4[3];
+        const bool any = umin <= umax;
+        const int Rw = any ? umax - umin + 1 : 0, Rh = any ? vmax - vmin + 1 : 0;
+        const bool use_lds = any && (int64_t)Rw * Rh <= kLdsCapPx;
+        if (use_lds) {
+            // stage the box: row r of the box is Rw * RU4 contiguous uint4 in global memory
+            const int rw4 = Rw * RU4;
+            const int n4 = rw4 * Rh;
+            const float inv = 1.0f / (float)rw4;
+            const uint4* __restrict__ src0 = reinterpret_cast<const uint4*>(img) + ((int64_t)vmin * W + umin) * RU4;
+            auto at = [&](int c) {  // box chunk c -> its global source
+                int r = (int)((float)c * inv);
+                r -= (r * rw4 > c);
+                r += ((r + 1) * rw4 <= c);
+                return src0 + ((int64_t)r * W * RU4 + (c - r * rw4));
+            };
+            const int last = n4 - 1;
+            for (int c0 = threadIdx.x; c0 < n4; c0 += 4 * kLdsThreads) {
+                // four independent loads in flight per lane (clamped indices: the tail re-reads
+                // the box's last chunk and does not store it)
+                const int c1 = c0 + kLdsThreads, c2 = c0 + 2 * kLdsThreads, c3 = c0 + 3 * kLdsThreads;
+                const uint4 a0 = *at(c0);
+                const uint4 a1 = *at(min(c1, last));
+                const uint4 a2 = *at(min(c2, last));
+                const uint4 a3 = *at(min(c3, last));
+                tile[c0] = a0;
+                if (c1 < n4) tile[c1] = a1;
+                if (c2 < n4) tile[c2] = a2;
+                if (c3 < n4) tile[c3] = a3;
+            }
+            __syncthreads();
+        } else if (any) {
+            n_global_levels++;
+        }
+        if (active && any && use_lds) {
+            // candidates from the staged box (inside the image => inside the box); the rows of the
+            // next window column are read from LDS while this column is scored (two register
+            // buffers, the column loop fully unrolled so they alternate without copies)
+            uint4 ra[SC][RU4], rb[SC][RU4];
+            bool oka[SC], okb[SC];
+            auto fetch = [&](int i, uint4 (&rw)[SC][RU4], bool (&okk)[SC]) {
+                const int64_t u = u0 - rd + (int64_t)i * d;
+#pragma unroll
+                for (int j = 0; j < SC; j++) {
+                    const int64_t v = v0 - rd + (int64_t)j * d;
+                    okk[j] = inside_image(u, v, W, H);
+                    const int off = okk[j] ? ((int)(v - vmin) * Rw + (int)(u - umin)) * RU4 : 0;
+#pragma unroll
+                    for (int c = 0; c < RU4; c++) rw[j][c] = tile[off + c];
+                }
+            };
+            auto consume = [&](int i, const uint4 (&rw)[SC][RU4], const bool (&okk)[SC]) {
+                half_t score[SC];
+                score_f16_multi<F, SC>(q2, rw, score);
+                const int64_t u = u0 - rd + (int64_t)i * d;
+#pragma unroll
+                for (int j = 0; j < SC; j++) {  // v offset inner (:55)
+                    if (okk[j] && score[j] > max_score) {
+                        max_score = score[j];
+                        u_new = u;
+                        v_new = v0 - rd + (int64_t)j * d;
+                    }
+                }
+            };
+            fetch(0, ra, oka);
+#pragma nounroll
+            for (int i = 0; i < SC; i += 2) {  // u offset outer (matching_kernels.cu:54)
+                if (i + 1 < SC) fetch(i + 1, rb, okb);
+                consume(i, ra, oka);
+                if (i + 1 < SC) {
+                    if (i + 2 < SC) fetch(i + 2, ra, oka);
+                    consume(i + 1, rb, okb);
+                }
+            }
+        } else if (active && any) {
+            // the box does not fit the LDS budget: this level gathers from global memory
+            for (int i = 0; i < SC; i++) {
+                const int64_t u = u0 - rd + (int64_t)i * d;
+                for (int j = 0; j < SC; j++) {
+                    const int64_t v = v0 - rd + (int64_t)j * d;
+                    if (inside_image(u, v, W, H)) {
+                        uint4 row[RU4];
+                        const uint4* src = reinterpret_cast<const uint4*>(img + (v * W + u) * F);
+#pragma unroll
+                        for (int c = 0; c < RU4; c++) row[c] = src[c];
+                        const half_t score = score_f16<F>(q2, row);
+                        if (score > max_score) {
+                            max_score = score;
+                            u_new = u;
+                            v_new = v;
+                        }
+                    }
+                }
+            }
+        }
+        u0 = u_new;
+        v0 = v_new;
+        if (use_lds) __syncthreads();  // the next level's staging overwrites the tile
+    }
+    if (active) {
+        p1_new[g * 2 + 0] = u_new;
+        p1_new[g * 2 + 1] = v_new;
+    }
+    if (stats && threadIdx.x == 0 && n_global_levels)
+        atomicAdd(stats, n_global_levels);  // diagnostics: levels that did not fit the LDS tile
 }
 
 // Generic F (any descriptor width), fp16, f32 or f64 (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
@@ -376,7 +622,20 @@ extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, 
     const int64_t total = B * N;
     if (total == 0) return M3S_OK;
     const bool aligned = ((uintptr_t)D11 % 16 == 0) && ((uintptr_t)D21 % 16 == 0);
-    if (F == 24 && aligned && N == H * W) {
+    // M3S_REFINE_LDS=1 selects the LDS-tiled kernel (A/B; slower on the bench data, see above)
+    const char* lds_env = getenv("M3S_REFINE_LDS");
+    const bool lds_ok = lds_env && atoi(lds_env) != 0;
+    if (F == 24 && aligned && N == H * W && radius == 3 && lds_ok) {
+        LdsTileMap tm;
+        tm.tiles_x = (int)((W + kLdsTx - 1) / kLdsTx);
+        tm.tiles_y = (int)((H + kLdsTy - 1) / kLdsTy);
+        tm.ntiles = tm.tiles_x * tm.tiles_y;
+        const int64_t nblk = (int64_t)tm.ntiles * B;
+        const int64_t grid = (nblk + 7) / 8 * 8;
+        hipLaunchKernelGGL((refine_lds_kernel<24, 3>), dim3((unsigned)grid), dim3(kLdsThreads), 0,
+                           (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, B, tm,
+                           dilation_max, (int*)nullptr);
+    } else if (F == 24 && aligned && N == H * W) {
         TileMap tm;
         tm.tiles_x = (int)((W + kTile - 1) / kTile);
         tm.tiles_y = (int)((H + kTile - 1) / kTile);

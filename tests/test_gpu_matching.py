@@ -79,6 +79,29 @@ def test_refine_matches_f16_bit_exact(backend, oracle, B, H, W):
     assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
 
 
+@pytest.mark.parametrize("scatter", [0, 3, 40, 10**6])
+def test_refine_lds_tile_and_fallback(backend, oracle, monkeypatch, scatter):
+    """The LDS-tiled kernel (M3S_REFINE_LDS=1) against the oracle and against the default
+    candidate-gather kernel (M3S_REFINE_LDS=0), bitwise.  ``scatter`` spreads the starting
+    matches: 0/3 px keeps every tile's candidate box in LDS; 40 px makes the large-dilation
+    boxes exceed the LDS budget (those levels gather from global memory); 10**6 puts most
+    starts far outside the image (clipped windows, many empty)."""
+    B, H, W = 2, 96, 128
+    mp = synth.make_match_pair(B=B, H=H, W=W, seed=31)
+    g = torch.Generator().manual_seed(scatter + 1)
+    p1 = torch.stack((mp.idx_init % W, mp.idx_init // W), -1).long()
+    if scatter:
+        p1 = p1 + torch.randint(-scatter, scatter + 1, p1.shape, generator=g)
+    D11 = mp.D11.half()
+    D21 = mp.D21.reshape(B, H * W, -1).half()
+    monkeypatch.setenv("M3S_REFINE_LDS", "1")
+    out_l, out_o = _refine_both(backend, oracle, D11, D21, p1)
+    monkeypatch.setenv("M3S_REFINE_LDS", "0")
+    (out_gth,) = backend.refine_matches(D11.cuda(), D21.cuda(), p1.cuda(), 3, 5)
+    assert np.array_equal(out_l, out_o), f"{(out_l != out_o).any(-1).sum()} matches differ"
+    assert np.array_equal(out_l, out_gth.cpu().numpy())
+
+
 @pytest.mark.parametrize("dtype,F", [(torch.float16, 24), (torch.float16, 5), (torch.float32, 24), (torch.float32, 3),
                                      (torch.float64, 24), (torch.float64, 7)])
 def test_refine_matches_generic(backend, oracle, dtype, F):
