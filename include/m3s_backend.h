@@ -117,6 +117,16 @@ typedef struct m3s_gn_args {
     /* summation order of the per-edge normal equations (M3S_GN_ORDER_*); 0 = the
      * default, overridable by the environment variable M3S_GN_ORDER=reference|fast */
     int order;
+    /* Optional second half of the local edges' idx / valid / Q (NULL = one contiguous
+     * tensor, the reference's layout): local directed edges 0 .. E_a-1 are rows of idx / valid
+     * / Q, edges E_a .. E_local-1 are rows 0 .. E_local-E_a-1 of idx_b / valid_b / Q_b.  A
+     * two-way edge store (forward edges, then the same pairs backward) is passed as its two
+     * halves instead of the per-call concatenation of prep_two_way_edges
+     * (global_opt.py:104-110). */
+    const int64_t* idx_b;
+    const uint8_t* valid_b;
+    const float* Q_b;
+    int64_t E_a;
 } m3s_gn_args;
 enum {
     M3S_GN_ORDER_DEFAULT = 0,

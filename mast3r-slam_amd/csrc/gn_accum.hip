@@ -346,8 +346,7 @@ struct AccStage {
 template <int MODE, bool VEC>
 __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
-    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int64_t* __restrict__ idx,
-    const uint8_t* __restrict__ valid, const float* __restrict__ Q, AccParams P,
+    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, EdgeSrc es, AccParams P,
     const int* __restrict__ sched, float* __restrict__ partials, const int* __restrict__ flags) {
     if (flags[kFlagDone]) return;
     const int task = sched[blockIdx.x];
@@ -357,7 +356,13 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
     const Sim3f T = rel_sim3(load_sim3(Twc + (int64_t)ix * 8), load_sim3(Twc + (int64_t)jx * 8));
 
     const int HW = P.HW;
-    const int64_t ebase = (int64_t)e * HW;
+    const int64_t* idx_e;
+    const uint8_t* valid_e;
+    const float* Q_e;
+    es.at(e, HW, idx_e, valid_e, Q_e);
+    const int64_t* __restrict__ idx = idx_e;
+    const uint8_t* __restrict__ valid = valid_e;
+    const float* __restrict__ Q = Q_e;
     const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
     const float* __restrict__ Ci_b = Cs + (int64_t)ix * HW;
     const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
@@ -373,10 +378,10 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
 #pragma unroll
         for (int q = 0; q < kNacc; q++) accs[q] = 0.0f;
         for (int k = k0 + 4 * tid; k < k1; k += 4 * kAccThreads) {
-            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + ebase + k);
-            const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + ebase + k);
-            const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + ebase + k + 2);
-            const float4 q4 = *reinterpret_cast<const float4*>(Q + ebase + k);
+            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + k);
+            const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + k);
+            const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + k + 2);
+            const float4 q4 = *reinterpret_cast<const float4*>(Q + k);
             const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
             const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
             const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
@@ -402,9 +407,9 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
         for (int q = 0; q < kNacc; q++) accs[q] = 0.0f;
         for (int k = k0 + tid; k < k1; k += kAccThreads) {
             PointsIn<float> p;
-            const bool vm = valid[ebase + k] != 0;
-            const int ind = match_index(idx[ebase + k], vm, HW);
-            const float q = Q[ebase + k];
+            const bool vm = valid[k] != 0;
+            const int ind = match_index(idx[k], vm, HW);
+            const float q = Q[k];
             p.xj0 = Xj_b[(int64_t)k * 3 + 0];
             p.xj1 = Xj_b[(int64_t)k * 3 + 1];
             p.xj2 = Xj_b[(int64_t)k * 3 + 2];
@@ -430,20 +435,26 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
     const float* __restrict__ Cs, const int* __restrict__ ii_loc, const int* __restrict__ jj_loc,
-    const int64_t* __restrict__ idx, const uint8_t* __restrict__ valid, const float* __restrict__ Q,
-    AccParams P, int4* __restrict__ pack, const int* __restrict__ flags) {
+    EdgeSrc es, AccParams P, int4* __restrict__ pack, const int* __restrict__ flags) {
     if (flags[kFlagDone]) return;
     const int e = blockIdx.y;
     const int HW = P.HW;
     const int64_t ebase = (int64_t)e * HW;
+    const int64_t* idx_e;
+    const uint8_t* valid_e;
+    const float* Q_e;
+    es.at(e, HW, idx_e, valid_e, Q_e);
+    const int64_t* __restrict__ idx = idx_e;
+    const uint8_t* __restrict__ valid = valid_e;
+    const float* __restrict__ Q = Q_e;
     const float* __restrict__ Ci_b = Cs + (int64_t)ii_loc[e] * HW;
     const float* __restrict__ Cj_b = Cs + (int64_t)jj_loc[e] * HW;
     const int k = 4 * (blockIdx.x * kAccThreads + threadIdx.x);
     if (k >= HW) return;
-    const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + ebase + k);
-    const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + ebase + k);
-    const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + ebase + k + 2);
-    const float4 q4 = *reinterpret_cast<const float4*>(Q + ebase + k);
+    const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + k);
+    const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + k);
+    const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + k + 2);
+    const float4 q4 = *reinterpret_cast<const float4*>(Q + k);
     const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
     const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
     const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
@@ -610,11 +621,11 @@ void gn_accum_packed_kernel(
 
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
-                        const int64_t* idx, const uint8_t* valid, const float* Q,
-                        const AccParams& P, const int* sched, float* partials, const int* flags) {
+                        const EdgeSrc& es, const AccParams& P, const int* sched, float* partials,
+                        const int* flags) {
 #define M3S_ACC(MODE, V)                                                                    \
     hipLaunchKernelGGL((gn_accum_kernel<MODE, V>), grid, dim3(kAccThreads), 0, st, Twc, Xs, \
-                       Cs, ii_loc, jj_loc, idx, valid, Q, P, sched, partials, flags)
+                       Cs, ii_loc, jj_loc, es, P, sched, partials, flags)
     if (mode == GN_RAYS) {
         if (vec) M3S_ACC(GN_RAYS, true); else M3S_ACC(GN_RAYS, false);
     } else if (mode == GN_CALIB) {
@@ -627,13 +638,12 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
 }
 
 hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
-                       const int* ii_loc, const int* jj_loc, const int64_t* idx,
-                       const uint8_t* valid, const float* Q, const AccParams& P, int4* pack,
-                       float* Zs, const int* flags) {
+                       const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P,
+                       int4* pack, float* Zs, const int* flags) {
     if (E_local > 0) {
         const dim3 grid((unsigned)((P.HW / 4 + kAccThreads - 1) / kAccThreads), (unsigned)E_local);
-        hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, idx,
-                           valid, Q, P, pack, flags);
+        hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, es,
+                           P, pack, flags);
     }
     if (Zs) {
         const int64_t total = N * (int64_t)P.HW;

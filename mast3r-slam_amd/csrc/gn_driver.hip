@@ -713,6 +713,11 @@ int validate(const m3s_gn_args& a) {
     M3S_REQUIRE(a.Twc && a.Xs && a.Cs && a.dx, "gauss_newton: null pointer");
     if (a.E_total > 0) M3S_REQUIRE(a.ii && a.jj, "gauss_newton: null ii/jj");
     if (a.E_local > 0) M3S_REQUIRE(a.idx && a.valid && a.Q, "gauss_newton: null edge data");
+    if (a.idx_b || a.valid_b || a.Q_b) {
+        M3S_REQUIRE(a.idx_b && a.valid_b && a.Q_b, "gauss_newton: incomplete second edge half");
+        M3S_REQUIRE(a.E_a >= 0 && a.E_a <= a.E_local, "gauss_newton: bad edge split E_a = %lld",
+                    (long long)a.E_a);
+    }
     const size_t need = make_layout(a.mode, a.N, a.HW, a.E_total, a.E_local).total;
     M3S_REQUIRE(a.ws != nullptr && a.ws_bytes >= need,
                 "gauss_newton: workspace too small (%zu < %zu bytes)", a.ws_bytes, need);
@@ -728,6 +733,7 @@ struct Ctx {
     Plan plan;
     SparsePlan sp;
     AccParams P;
+    EdgeSrc es{};
     bool vec;
     char* ws;
     hipStream_t st = nullptr;
@@ -844,8 +850,16 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     P.nchunks = L.nchunks;
     P.nkf = (int)a.N;
     auto al16 = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
+    const bool two = a.idx_b != nullptr;
+    c.es.idx[0] = a.idx;
+    c.es.valid[0] = a.valid;
+    c.es.Q[0] = a.Q;
+    c.es.idx[1] = two ? a.idx_b : a.idx;
+    c.es.valid[1] = two ? a.valid_b : a.valid;
+    c.es.Q[1] = two ? a.Q_b : a.Q;
+    c.es.E_a = two ? (int)a.E_a : (int)a.E_local;
     c.vec = (a.HW % 4 == 0) && al16(a.Xs) && al16(a.Cs) && al16(a.idx) && al16(a.valid) &&
-            al16(a.Q);
+            al16(a.Q) && (!two || (al16(a.idx_b) && al16(a.valid_b) && al16(a.Q_b)));
     // M3S_GN_PACK: 0 never, 1 (default) when the call runs >= 3 iterations, 2 always
     const int pack_mode = env_int("M3S_GN_PACK", 1);
     c.packed = c.vec && a.E_local > 0 && (pack_mode == 2 || (pack_mode == 1 && a.max_iter >= 3));
@@ -877,7 +891,7 @@ int prepare_iterations(const m3s_gn_args& a, Ctx& c) {
     if (!c.packed) return M3S_OK;
     const Layout& L = c.L;
     M3S_HIP_CHECK(launch_pack(c.st, (int)a.E_local, a.Xs, a.N, a.Cs, c.at<int>(L.ii_loc),
-                              c.at<int>(L.jj_loc), a.idx, a.valid, a.Q, c.P, c.at<int4>(L.pack),
+                              c.at<int>(L.jj_loc), c.es, c.P, c.at<int4>(L.pack),
                               a.mode == M3S_GN_CALIB ? c.at<float>(L.zs) : nullptr,
                               c.at<int>(L.flags)));
     return M3S_OK;
@@ -894,7 +908,7 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
         M3S_REQUIRE(c.sp.enabled, "gauss_newton: the reference order needs the block-sparse solver");
         g_prof.mark(c.st, true);
         M3S_HIP_CHECK(launch_accum_ref(a.mode, (int)a.E_local, c.st, a.Twc, a.Xs, a.Cs,
-                                       c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), a.idx, a.valid, a.Q,
+                                       c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), c.es,
                                        c.R, c.at<float>(L.edgeblk), flags));
         g_prof.mark(c.st, true);
         SparsePlan& sp = c.sp;
@@ -920,8 +934,8 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
                                               c.at<float>(L.partials), flags));
         else
             M3S_HIP_CHECK(launch_accum(a.mode, c.vec, grid, c.st, a.Twc, a.Xs, a.Cs,
-                                       c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), a.idx, a.valid,
-                                       a.Q, c.P, c.at<int>(L.sched), c.at<float>(L.partials),
+                                       c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), c.es, c.P,
+                                       c.at<int>(L.sched), c.at<float>(L.partials),
                                        flags));
         g_prof.mark(c.st, true);
         M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
@@ -1184,7 +1198,7 @@ int ref_edge_records(const m3s_gn_args& a0, Ctx& c, std::vector<float>& rec) {
     if (a.E_local == 0) return M3S_OK;
     const Layout& L = c.L;
     M3S_HIP_CHECK(launch_accum_ref(a.mode, (int)a.E_local, c.st, a.Twc, a.Xs, a.Cs, c.at<int>(L.ii_loc),
-                                   c.at<int>(L.jj_loc), a.idx, a.valid, a.Q, c.R, c.at<float>(L.edgeblk),
+                                   c.at<int>(L.jj_loc), c.es, c.R, c.at<float>(L.edgeblk),
                                    c.at<int>(L.flags)));
     M3S_HIP_CHECK(hipMemcpyAsync(rec.data(), c.at<float>(L.edgeblk), sizeof(float) * rec.size(),
                                  hipMemcpyDeviceToHost, c.st));

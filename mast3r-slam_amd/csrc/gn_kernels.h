@@ -20,6 +20,26 @@ constexpr int kFlagFail = 1;   // set by the factorisation when a pivot <= 0
 constexpr int kFlagNotRay = 2; // calib: some Xs point is not its pixel's ray times its depth
 constexpr int kNumFlags = 16;
 
+// Where the per-point-edge inputs (idx, valid, Q) of local directed edge e live: edges
+// e < E_a in the first arrays (row e), the others in the second arrays (row e - E_a).  One
+// contiguous tensor (the reference's layout): both halves the same arrays and E_a = E_local.
+// Two halves: the forward and backward edge sets of a two-way edge store, passed without the
+// per-call concatenation of global_opt.py:104-110.
+struct EdgeSrc {
+    const int64_t* idx[2];
+    const uint8_t* valid[2];
+    const float* Q[2];
+    int E_a;
+    __device__ __forceinline__ void at(int e, int64_t HW, const int64_t*& i, const uint8_t*& v,
+                                       const float*& q) const {
+        const int h = e >= E_a;
+        const int64_t off = (int64_t)(h ? e - E_a : e) * HW;
+        i = idx[h] + off;
+        v = valid[h] + off;
+        q = Q[h] + off;
+    }
+};
+
 // Upper-triangle packing of a symmetric 7x7 block: index of (a,b), a <= b.
 __host__ __device__ constexpr int sym_idx(int a, int b) {
     return a * 7 - a * (a - 1) / 2 + (b - a);
@@ -58,21 +78,19 @@ constexpr int kRefVarLogRatio = 1;  // calib log depth as ln2 * log2(zj * rcp(zi
 constexpr int kRefVarRcp = 2;       // 1/x by v_rcp_f32 instead of the double division
 constexpr int kRefVarHuberMin = 4;  // Huber weight as min(1, 1.345 rcp|r|)
 hipError_t launch_accum_ref(int mode, int E_local, hipStream_t st, const float* Twc, const float* Xs,
-                            const float* Cs, const int* ii_loc, const int* jj_loc, const int64_t* idx,
-                            const uint8_t* valid, const float* Q, const RefParams& P, float* out,
-                            const int* flags);
+                            const float* Cs, const int* ii_loc, const int* jj_loc, const EdgeSrc& es,
+                            const RefParams& P, float* out, const int* flags);
 hipError_t launch_assemble_ref(hipStream_t st, const float* ref, const int* blk_ptr, const int* blk_ref,
                                const int* grad_ptr, const int* grad_ent, int nblk, int nblocks,
                                int npose, int bpad, double* out, const int* flags);
 
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
-                        const int64_t* idx, const uint8_t* valid, const float* Q,
-                        const AccParams& P, const int* sched, float* partials, const int* flags);
+                        const EdgeSrc& es, const AccParams& P, const int* sched, float* partials,
+                        const int* flags);
 hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
-                       const int* ii_loc, const int* jj_loc, const int64_t* idx,
-                       const uint8_t* valid, const float* Q, const AccParams& P, int4* pack,
-                       float* Zs, const int* flags);
+                       const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P,
+                       int4* pack, float* Zs, const int* flags);
 hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,

@@ -196,8 +196,7 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
 template <int MODE>
 __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
-    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int64_t* __restrict__ idx,
-    const uint8_t* __restrict__ valid, const float* __restrict__ Q, RefParams P,
+    const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, EdgeSrc es, RefParams P,
     float* __restrict__ out, const int* __restrict__ flags) {
     if (flags[kFlagDone]) return;
     const int e = blockIdx.x;
@@ -208,7 +207,13 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
     const Sim3f Tij = rel_sim3(Ti, Tj);
     const float si_inv = (float)(1.0 / (double)Ti.s);  // apply_Sim3_adj_inv's s_inv
     const int64_t HW = P.HW;
-    const int64_t ebase = (int64_t)e * HW;
+    const int64_t* idx_e;
+    const uint8_t* valid_e;
+    const float* Q_e;
+    es.at(e, HW, idx_e, valid_e, Q_e);
+    const int64_t* __restrict__ idx = idx_e;
+    const uint8_t* __restrict__ valid = valid_e;
+    const float* __restrict__ Q = Q_e;
     const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
     const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
     const float* __restrict__ Ci_b = Cs + (int64_t)ix * HW;
@@ -222,12 +227,12 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
         a.g[n] = 0.0f;
     }
     for (int64_t k = tid; k < HW; k += kAccThreads) {
-        const bool vm = valid[ebase + k] != 0;
-        int64_t ind = vm ? idx[ebase + k] : 0;
+        const bool vm = valid[k] != 0;
+        int64_t ind = vm ? idx[k] : 0;
         if ((uint64_t)ind >= (uint64_t)HW) ind = HW - 1;  // the reference reads out of bounds
         const float Xi[3] = {Xi_b[ind * 3], Xi_b[ind * 3 + 1], Xi_b[ind * 3 + 2]};
         const float Xj[3] = {Xj_b[k * 3], Xj_b[k * 3 + 1], Xj_b[k * 3 + 2]};
-        point_ref<MODE>(P, Ti, si_inv, Tij, Xi, Xj, Q[ebase + k], Ci_b[ind], Cj_b[k], vm, ind, a);
+        point_ref<MODE>(P, Ti, si_inv, Tij, Xi, Xj, Q[k], Ci_b[ind], Cj_b[k], vm, ind, a);
     }
 
     // blockReduce (gn_kernels.cu:36-55) of all 56 chains at once: level o adds s[t + o] into
@@ -303,13 +308,12 @@ __global__ __launch_bounds__(64) void gn_assemble_ref_kernel(
 }
 
 hipError_t launch_accum_ref(int mode, int E_local, hipStream_t st, const float* Twc, const float* Xs,
-                            const float* Cs, const int* ii_loc, const int* jj_loc, const int64_t* idx,
-                            const uint8_t* valid, const float* Q, const RefParams& P, float* out,
-                            const int* flags) {
+                            const float* Cs, const int* ii_loc, const int* jj_loc, const EdgeSrc& es,
+                            const RefParams& P, float* out, const int* flags) {
     if (E_local <= 0) return hipSuccess;
 #define M3S_REF(MODE)                                                                              \
     hipLaunchKernelGGL(gn_accum_ref_kernel<MODE>, dim3(E_local), dim3(kAccThreads), 0, st, Twc, Xs, \
-                       Cs, ii_loc, jj_loc, idx, valid, Q, P, out, flags)
+                       Cs, ii_loc, jj_loc, es, P, out, flags)
     if (mode == GN_RAYS) M3S_REF(GN_RAYS);
     else if (mode == GN_CALIB) M3S_REF(GN_CALIB);
     else M3S_REF(GN_POINTS);

@@ -92,11 +92,30 @@ class HostComm:
             self.handle = None
 
 
+def two_way_range(fwd, bwd, lo, hi):
+    """The rank's directed edges [lo, hi) of a two-way edge store -- forward edges 0..E-1, then
+    the same pairs backward (global_opt.py:104-110 order) -- as (first, second) halves of
+    (idx, valid, Q) views, without concatenating: ``fwd`` / ``bwd`` are (idx, valid, Q) of the
+    E forward / backward edges.  Returns (first, second_or_None)."""
+    E = fwd[0].shape[0]
+    a_lo, a_hi = min(lo, E), min(hi, E)
+    b_lo, b_hi = max(lo, E) - E, max(hi, E) - E
+    first = tuple(t[a_lo:a_hi] for t in fwd)
+    second = tuple(t[b_lo:b_hi] for t in bwd)
+    if a_hi == a_lo:
+        return second, None
+    if b_hi == b_lo:
+        return first, None
+    return first, second
+
+
 def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx_local, valid_local, Q_local, edge_offset,
-                         comm: RcclComm | HostComm | None, max_iter, delta_thresh, **p):
+                         comm: RcclComm | HostComm | None, max_iter, delta_thresh,
+                         second_half=None, **p):
     """Sharded variant of gauss_newton_{rays,calib,points}: ``ii``/``jj`` hold ALL directed
     edges, ``idx_local``/``valid_local``/``Q_local`` the rank's range starting at
-    ``edge_offset``.  Twc is updated in place identically on every rank."""
+    ``edge_offset`` (optionally continued by ``second_half``, see two_way_range).  Twc is
+    updated in place identically on every rank."""
     mode_id = {"points": mb.GN_POINTS, "rays": mb.GN_RAYS, "calib": mb.GN_CALIB}[mode]
     if mode == "rays":
         s0, s1 = p["sigma_ray"], p["sigma_dist"]
@@ -109,5 +128,5 @@ def gauss_newton_sharded(mode, Twc, Xs, Cs, ii, jj, idx_local, valid_local, Q_lo
         s0, s1, p.get("C_conf", 0.0), p.get("Q_conf", 1.5), K=p.get("K"),
         height=p.get("height", 0), width=p.get("width", 0), pixel_border=p.get("pixel_border", 0),
         z_eps=p.get("depth_eps", 0.0), comm=(comm.handle if comm is not None else None),
-        edge_offset=edge_offset,
+        edge_offset=edge_offset, edge_total=ii.shape[0], second_half=second_half,
     )

@@ -95,6 +95,10 @@ class GNArgs(ctypes.Structure):
         ("comm", _vp),
         ("stream", _vp),
         ("order", _i),
+        ("idx_b", _vp),
+        ("valid_b", _vp),
+        ("Q_b", _vp),
+        ("E_a", _c_int64),
     ]
 
 
@@ -274,9 +278,25 @@ def _gn_common_checks(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, edge_local
 
 def _run_gn(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter, delta_thresh,
             sigma0, sigma1, C_thresh, Q_thresh, K=None, height=0, width=0, pixel_border=0,
-            z_eps=0.0, comm=None, edge_offset=0, edge_total=None):
-    E_local = idx_ii2jj.shape[0]
-    dev, N, HW, E = _gn_common_checks(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, E_local)
+            z_eps=0.0, comm=None, edge_offset=0, edge_total=None, second_half=None):
+    """``second_half`` = (idx, valid, Q) of local directed edges E_a.. when the edges come as
+    two tensors (a two-way edge store: forward then backward), E_a = len(idx_ii2jj)."""
+    E_a = idx_ii2jj.shape[0]
+    E_local = E_a
+    if second_half is not None:
+        idx_b, valid_b, Q_b = second_half
+        _check(idx_b, "idx_ii2jj (second half)", torch.int64, 2)
+        _check(valid_b, "valid_match (second half)", torch.bool, 3)
+        _check(Q_b, "Q (second half)", torch.float32, 3)
+        _on_device(idx_a=idx_ii2jj, idx_b=idx_b, valid_b=valid_b, Q_b=Q_b)
+        E_b = idx_b.shape[0]
+        if idx_b.shape[1:] != idx_ii2jj.shape[1:] or valid_b.shape != (E_b,) + valid_match.shape[1:] \
+                or Q_b.shape != (E_b,) + Q.shape[1:]:
+            raise RuntimeError("gauss_newton: second edge half shapes differ from the first")
+        E_local = E_a + E_b
+    dev, N, HW, E = _gn_common_checks(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, E_a)
+    if E_local != E_a and edge_total is None and E_local != E:
+        raise RuntimeError("gauss_newton: the two edge halves must cover len(ii) directed edges")
     if edge_total is not None and edge_total != E:
         raise RuntimeError("gauss_newton: edge_total must equal len(ii)")
     if K is not None:
@@ -305,6 +325,9 @@ def _run_gn(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter, delt
     a.ws, a.ws_bytes = ws.data_ptr(), ws_bytes
     a.comm = comm
     a.order = _gn_order[0]
+    if second_half is not None:
+        a.idx_b, a.valid_b, a.Q_b = idx_b.data_ptr(), valid_b.data_ptr(), Q_b.data_ptr()
+        a.E_a = E_a
     with torch.cuda.device(dev):
         a.stream = torch.cuda.current_stream(dev).cuda_stream
         rc = lib.m3s_gauss_newton(ctypes.byref(a))

@@ -54,26 +54,38 @@ def _params(g, mode):
     return p
 
 
-def _worker(rank, world, port, mode, out_q):
+def _worker(rank, world, port, mode, layout, out_q):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "mast3r-slam_amd")]
     import torch.distributed as dist
 
-    from m3s.dist import HostComm, gauss_newton_sharded, shard_range
+    from m3s.dist import HostComm, gauss_newton_sharded, shard_range, two_way_range
 
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         g = _graph(mode)
         lo, hi = shard_range(g.ii.shape[0], world, rank)
+        if layout == "two_way":  # uneven split: rank 0's range spans both halves of the store
+            E = g.ii.shape[0] // 2
+            lo, hi = [(0, E + 5), (E + 5, 2 * E)][rank]
         c = lambda t: t.cuda().contiguous()
         Twc = c(g.Twc)
         comm = HostComm()
-        gauss_newton_sharded(mode, Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx[lo:hi]),
-                             c(g.valid[lo:hi]), c(g.Q[lo:hi]), lo, comm, ITERS, 0.0,
-                             **_params(g, mode))
+        if layout == "contiguous":
+            gauss_newton_sharded(mode, Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx[lo:hi]),
+                                 c(g.valid[lo:hi]), c(g.Q[lo:hi]), lo, comm, ITERS, 0.0,
+                                 **_params(g, mode))
+        else:
+            # a two-way edge store (forward, backward halves): the rank's directed range as views
+            E = g.ii.shape[0] // 2
+            fwd = (c(g.idx[:E]), c(g.valid[:E]), c(g.Q[:E]))
+            bwd = (c(g.idx[E:]), c(g.valid[E:]), c(g.Q[E:]))
+            first, second = two_way_range(fwd, bwd, lo, hi)
+            gauss_newton_sharded(mode, Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), *first, lo, comm,
+                                 ITERS, 0.0, second_half=second, **_params(g, mode))
         torch.cuda.synchronize()
         out_q.put((rank, Twc.cpu().numpy(), comm.calls, (lo, hi), None))
         comm.close()
@@ -83,13 +95,16 @@ def _worker(rank, world, port, mode, out_q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("mode", ["rays", "calib"])
-def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode):
+@pytest.mark.parametrize("mode,layout", [("rays", "contiguous"), ("calib", "contiguous"),
+                                         ("rays", "two_way")])
+def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout):
+    """layout "two_way": each rank passes its directed-edge range of a two-way edge store as
+    the op's two halves (m3s.dist.two_way_range) -- the owner-sharded store layout."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, layout, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:

@@ -78,3 +78,24 @@ def test_edge_confidence_full_size_bit_exact(backend):
     assert torch.equal(Qj, ref_Qj) and torch.equal(Qi, ref_Qi)
     assert torch.equal(counts[:, 0].long(), (vj & (ref_Qj > 1.5)).sum(dim=(1, 2)))
     assert torch.equal(counts[:, 1].long(), (vi & (ref_Qi > 1.5)).sum(dim=(1, 2)))
+
+
+def test_device_factor_graph_store_equals_reference_store():
+    """DeviceFactorGraph appends into its two-way EdgeStore (capacity doubling) instead of
+    concatenating: after every add_factors call its edge attributes are exactly the
+    reference-compatible FactorGraph's."""
+    from m3s.global_opt import DeviceFactorGraph, FactorGraph
+
+    fg = FactorGraph(None, None, device=DEV)
+    dg = DeviceFactorGraph(None, None, device=DEV)
+    for c in range(int(GOLD["ncalls"])):
+        m = [torch.from_numpy(GOLD[f"c{c}_{n}"]).to(DEV) for n in NAMES]
+        args = (GOLD[f"c{c}_ii"].tolist(), GOLD[f"c{c}_jj"].tolist(), *m, float(GOLD["min_match_frac"]))
+        r1 = fg.add_matched_factors(*args, is_reloc=bool(GOLD[f"c{c}_reloc"]))
+        r2 = dg.add_matched_factors(*args, is_reloc=bool(GOLD[f"c{c}_reloc"]))
+        assert r1 == r2
+        for n in ["ii", "jj", "idx_ii2jj", "idx_jj2ii", "valid_match_j", "valid_match_i", "Q_ii2jj", "Q_jj2ii"]:
+            assert torch.equal(getattr(fg, n), getattr(dg, n)), (c, n)
+        a, b = fg.prep_two_way_edges(), dg.prep_two_way_edges()
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+    assert dg.edges.capacity >= dg.edges.E

@@ -116,3 +116,48 @@ def test_factor_graph_solve_with_one_keyframe_is_a_noop():
     calls = {}
     fg.solve_GN_rays(backend=_proxy(calls))
     assert not calls and torch.equal(store.T_WC, before)
+
+
+def _device_setup(mode, ids):
+    from m3s.global_opt import DeviceFactorGraph
+
+    g = synth.make_graph(dict(N=len(ids), E=9), H=48, W=64, seed=23)
+    K = g.K.cuda()
+    stores = []
+    for _ in range(2):
+        st = KeyframeStore(16, g.H, g.W, device="cuda", K=K if mode == "calib" else None)
+        st.size = 16
+        for r, k in enumerate(ids):
+            st.set_keyframe(k, X=g.Xs[r].cuda(), C=(3.0 * g.Cs[r]).cuda(), T_WC=g.Twc[r].cuda(), n_obs=3.0)
+        stores.append(st)
+    fg = FactorGraph(None, stores[0], K=K if mode == "calib" else None, device="cuda", cfg=DEFAULT_CONFIG)
+    dg = DeviceFactorGraph(None, stores[1], K=K if mode == "calib" else None, device="cuda",
+                           cfg=DEFAULT_CONFIG)
+    to_g = torch.tensor(ids, device="cuda")
+    E = g.ii.shape[0] // 2
+    fg.ii, fg.jj = to_g[g.ii[:E].cuda()], to_g[g.jj[:E].cuda()]
+    fg.idx_ii2jj, fg.idx_jj2ii = g.idx[:E].cuda(), g.idx[E:].cuda()
+    fg.valid_match_j, fg.valid_match_i = g.valid[:E].cuda(), g.valid[E:].cuda()
+    fg.Q_ii2jj, fg.Q_jj2ii = g.Q[:E].cuda(), g.Q[E:].cuda()
+    # the device graph gets the same edges in two batches (the store grows in between)
+    h = E // 2
+    for sl in (slice(0, h), slice(h, E)):
+        dg.add_edges(fg.ii[sl], fg.jj[sl], fg.idx_ii2jj[sl], fg.idx_jj2ii[sl], fg.valid_match_j[sl],
+                     fg.valid_match_i[sl], fg.Q_ii2jj[sl], fg.Q_jj2ii[sl])
+    return fg, dg, stores
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+@pytest.mark.parametrize("ids", [[3, 4, 5, 6, 7, 8], [2, 3, 5, 8, 9, 13]], ids=["contiguous", "sparse"])
+def test_device_factor_graph_solve_is_bitwise_the_reference_path(mode, ids):
+    """DeviceFactorGraph's zero-copy solve (two-way edge halves into the op; store views for
+    contiguous keyframe ids, ray-constrained points and C / N kept by the store) gives bitwise
+    the poses of the reference-compatible FactorGraph (cat + stack + constrain per call)."""
+    fg, dg, (s_ref, s_dev) = _device_setup(mode, ids)
+    (fg.solve_GN_rays if mode == "rays" else fg.solve_GN_calib)()
+    (dg.solve_GN_rays if mode == "rays" else dg.solve_GN_calib)()
+    torch.cuda.synchronize()
+    assert torch.equal(s_ref.T_WC, s_dev.T_WC)
+    # the keyframes moved
+    g0 = synth.make_graph(dict(N=len(ids), E=9), H=48, W=64, seed=23)
+    assert not torch.equal(s_dev.T_WC[ids[1:], 0].cpu(), g0.Twc[1:])
