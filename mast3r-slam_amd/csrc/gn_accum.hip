@@ -81,27 +81,54 @@ struct PointsIn {
     V ut, vt;  // calib: pixel of the match, (ind % W, ind / W) as float
 };
 
-// T_ij * Xj with the reference's quaternion formula (act_so3 + scale + translation,
-// gn_kernels.cu:195-205, 252-272), on one point or a packed pair.
+// T_ij as the 3x4 affine map it applies to a point.  The reference's act_so3
+// (gn_kernels.cu:195-205) computes x + w uv + q x uv with uv = 2 q x x, which is linear in x:
+// M = I + 2w[q]x + 2[q]x^2 (exactly that map, unit quaternion or not); actSim3 then scales and
+// translates (gn_kernels.cu:252-272).  Formed once per workgroup, s M x + t costs 9 FMAs per
+// point instead of the 24 operations of the quaternion formula.  The two differ by float
+// rounding only; on the bench graphs the normal equations built this way are closer to the
+// exactly summed reference system than the quaternion form's, and
+// gn_refacc.hip keeps the reference's own formula for the parity mode.
+struct RelXf {
+    float m[9];  // s * M, row-major
+    float t[3];
+};
+
+__device__ __forceinline__ RelXf rel_xf(const Sim3f& T) {
+    const float x = T.q[0], y = T.q[1], z = T.q[2], w = T.q[3], s = T.s;
+    const float xx = x * x, yy = y * y, zz = z * z;
+    const float xy = x * y, xz = x * z, yz = y * z, wx = w * x, wy = w * y, wz = w * z;
+    RelXf R;
+    R.m[0] = s * (1.0f - 2.0f * (yy + zz));
+    R.m[1] = s * (2.0f * (xy - wz));
+    R.m[2] = s * (2.0f * (xz + wy));
+    R.m[3] = s * (2.0f * (xy + wz));
+    R.m[4] = s * (1.0f - 2.0f * (xx + zz));
+    R.m[5] = s * (2.0f * (yz - wx));
+    R.m[6] = s * (2.0f * (xz - wy));
+    R.m[7] = s * (2.0f * (yz + wx));
+    R.m[8] = s * (1.0f - 2.0f * (xx + yy));
+    R.t[0] = T.t[0];
+    R.t[1] = T.t[1];
+    R.t[2] = T.t[2];
+    // workgroup-uniform: keep the 12 coefficients in SGPRs (VALU operands), not VGPRs
+#pragma unroll
+    for (int k = 0; k < 9; k++) R.m[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(R.m[k])));
+#pragma unroll
+    for (int k = 0; k < 3; k++) R.t[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(R.t[k])));
+    return R;
+}
+
 template <typename V>
-__device__ __forceinline__ void apply_rel(const Sim3f& T, V x0, V x1, V x2, V& X0, V& X1, V& X2) {
-    const V q0 = vsplat(T.q[0], x0), q1 = vsplat(T.q[1], x0), q2 = vsplat(T.q[2], x0),
-            q3 = vsplat(T.q[3], x0), two = vsplat(2.0f, x0);
-    const V uv0 = two * (q1 * x2 - q2 * x1);
-    const V uv1 = two * (q2 * x0 - q0 * x2);
-    const V uv2 = two * (q0 * x1 - q1 * x0);
-    const V y0 = (x0 + q3 * uv0) + (q1 * uv2 - q2 * uv1);
-    const V y1 = (x1 + q3 * uv1) + (q2 * uv0 - q0 * uv2);
-    const V y2 = (x2 + q3 * uv2) + (q0 * uv1 - q1 * uv0);
-    const V s = vsplat(T.s, x0);
-    X0 = y0 * s + vsplat(T.t[0], x0);
-    X1 = y1 * s + vsplat(T.t[1], x0);
-    X2 = y2 * s + vsplat(T.t[2], x0);
+__device__ __forceinline__ void apply_rel(const RelXf& T, V x0, V x1, V x2, V& X0, V& X1, V& X2) {
+    X0 = vfma(vsplat(T.m[0], x0), x0, vfma(vsplat(T.m[1], x0), x1, vfma(vsplat(T.m[2], x0), x2, vsplat(T.t[0], x0))));
+    X1 = vfma(vsplat(T.m[3], x0), x0, vfma(vsplat(T.m[4], x0), x1, vfma(vsplat(T.m[5], x0), x2, vsplat(T.t[1], x0))));
+    X2 = vfma(vsplat(T.m[6], x0), x0, vfma(vsplat(T.m[7], x0), x1, vfma(vsplat(T.m[8], x0), x2, vsplat(T.t[2], x0))));
 }
 
 // One (pair of) point-edge(s): residuals, robust weights, raw rows -> acc.
 template <int MODE, typename V>
-__device__ __forceinline__ void point_body(const PointsIn<V>& p, const Sim3f& T, const AccParams& P,
+__device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T, const AccParams& P,
                                            V* __restrict__ acc) {
     V X0, X1, X2;
     apply_rel(T, p.xj0, p.xj1, p.xj2, X0, X1, X2);
@@ -233,15 +260,47 @@ __device__ __forceinline__ void pixel_of(int ind, const AccParams& P, float& ut,
     ut = (float)(ind - (int)q * P.width);
 }
 
-// Deterministic workgroup reduction of the 35 sums: wave butterfly, then the 4 waves in fixed
-// order; one 36-float partial per (edge, chunk).
+// Half exchanges of two registers (gfx950 v_permlane32_swap / v_permlane16_swap): afterwards
+// a + b holds, in the first half (row pair) of the lanes, a's partial sums and in the second
+// b's -- a reduce-scatter step that costs one swap + one add for two values.
+__device__ __forceinline__ float halfsum32(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float halfsum16(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// sum over the 16 lanes of each row (every lane of the row gets it): DPP row rotations
+template <int N>
+__device__ __forceinline__ float row_ror(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x120 + N, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    v += row_ror<2>(v);
+    v += row_ror<1>(v);
+    return v;
+}
+
+// Deterministic workgroup reduction of the 35 sums, one 36-float partial per (edge, chunk).
+// Per wave a reduce-scatter: 36 values -> 18 (32-lane halves) -> 9 (16-lane rows, row r of
+// register j holding value j + 9r), then a 16-lane row sum (126 lane ops instead of the
+// 35 x 6 shuffle-adds of a butterfly per value); then the 4 waves in fixed order.
 __device__ __forceinline__ void block_partial(const float* accs, float* __restrict__ out) {
-    __shared__ float red[kAccThreads / 64][kNacc];
+    __shared__ float red[kAccThreads / 64][kNaccPad];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    static_assert(kNaccPad == 36, "reduce-scatter is laid out for 36 values");
+    float w[18], x[9];
 #pragma unroll
-    for (int q = 0; q < kNacc; q++) {
-        const float s = wave_sum(accs[q]);
-        if (lane == 0) red[wave][q] = s;
+    for (int j = 0; j < 18; j++) w[j] = halfsum32(accs[j], j + 18 < kNacc ? accs[j + 18] : 0.0f);
+#pragma unroll
+    for (int j = 0; j < 9; j++) x[j] = row_sum16(halfsum16(w[j], w[j + 9]));
+    if ((lane & 15) == 0) {
+        const int r = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < 9; j++) red[wave][j + 9 * r] = x[j];
     }
     __syncthreads();
     if (tid < kNacc) {
@@ -297,7 +356,7 @@ struct AccStage {
 
     // the 4 points one at a time on scalar accumulators
     template <int M>
-    __device__ __forceinline__ void compute(const Sim3f& T, const AccParams& P, float* __restrict__ acc) const {
+    __device__ __forceinline__ void compute(const RelXf& T, const AccParams& P, float* __restrict__ acc) const {
         const int codes[4] = {ka.x, ka.z, kb.x, kb.z};
         const int sqb[4] = {ka.y, ka.w, kb.y, kb.w};
         float xj[12];
@@ -347,13 +406,11 @@ template <int MODE, bool VEC>
 __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, EdgeSrc es, AccParams P,
-    const int* __restrict__ sched, float* __restrict__ partials, const int* __restrict__ flags) {
+    const int4* __restrict__ sched, float* __restrict__ partials, const int* __restrict__ flags) {
+    const int4 tk = sched[blockIdx.x];  // {edge, chunk, ix, jx}, loaded together with the flag
     if (flags[kFlagDone]) return;
-    const int task = sched[blockIdx.x];
-    const int e = task / P.nchunks;
-    const int c = task - e * P.nchunks;
-    const int ix = ii_loc[e], jx = jj_loc[e];
-    const Sim3f T = rel_sim3(load_sim3(Twc + (int64_t)ix * 8), load_sim3(Twc + (int64_t)jx * 8));
+    const int e = tk.x, c = tk.y, ix = tk.z, jx = tk.w;
+    const RelXf T = rel_xf(rel_sim3(load_sim3(Twc + (int64_t)ix * 8), load_sim3(Twc + (int64_t)jx * 8)));
 
     const int HW = P.HW;
     const int64_t* idx_e;
@@ -510,7 +567,7 @@ __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__
 template <int MODE, bool RC>
 __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
                                             const float* __restrict__ Zi_b, const int4* __restrict__ pk_b,
-                                            int k0, int k1, const Sim3f& T, const AccParams& P,
+                                            int k0, int k1, const RelXf& T, const AccParams& P,
                                             const float* __restrict__ Zs, float* __restrict__ acc) {
     constexpr int S = 4 * kAccThreads;
     AccStage<MODE, RC> cur;
@@ -556,14 +613,12 @@ __global__ __launch_bounds__(kAccThreads) __attribute__((amdgpu_waves_per_eu(M3S
 void gn_accum_packed_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Zs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int4* __restrict__ pack,
-    AccParams P, const int* __restrict__ sched, float* __restrict__ partials,
+    AccParams P, const int4* __restrict__ sched, float* __restrict__ partials,
     const int* __restrict__ flags) {
+    const int4 tk = sched[blockIdx.x];  // {edge, chunk, ix, jx}, loaded together with the flag
     if (flags[kFlagDone]) return;
-    const int task = sched[blockIdx.x];
-    const int e = task / P.nchunks;
-    const int c = task - e * P.nchunks;
-    const int ix = ii_loc[e], jx = jj_loc[e];
-    const Sim3f T = rel_sim3(load_sim3(Twc + (int64_t)ix * 8), load_sim3(Twc + (int64_t)jx * 8));
+    const int e = tk.x, c = tk.y, ix = tk.z, jx = tk.w;
+    const RelXf T = rel_xf(rel_sim3(load_sim3(Twc + (int64_t)ix * 8), load_sim3(Twc + (int64_t)jx * 8)));
 
     const int HW = P.HW;
     const int64_t ebase = (int64_t)e * HW;
@@ -621,7 +676,7 @@ void gn_accum_packed_kernel(
 
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
-                        const EdgeSrc& es, const AccParams& P, const int* sched, float* partials,
+                        const EdgeSrc& es, const AccParams& P, const int4* sched, float* partials,
                         const int* flags) {
 #define M3S_ACC(MODE, V)                                                                    \
     hipLaunchKernelGGL((gn_accum_kernel<MODE, V>), grid, dim3(kAccThreads), 0, st, Twc, Xs, \
@@ -659,7 +714,7 @@ hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, 
 hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,
-                               const int* sched, float* partials, const int* flags) {
+                               const int4* sched, float* partials, const int* flags) {
     if (mode == GN_RAYS)
         hipLaunchKernelGGL(gn_accum_packed_kernel<GN_RAYS>, grid, dim3(kAccThreads), 0, st, Twc, Xs,
                            Zs, ii_loc, jj_loc, pack, P, sched, partials, flags);

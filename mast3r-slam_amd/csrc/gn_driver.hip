@@ -182,7 +182,7 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.blk_ref = take(sizeof(int) * (size_t)E_local * 4);  // reference-order assembly codes
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
-    L.sched = take(sizeof(int) * (size_t)E_local * L.nchunks);
+    L.sched = take(sizeof(int) * 4 * (size_t)E_local * L.nchunks);  // {edge, chunk, ix, jx} per task
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
     L.pack = take(8 * (size_t)E_local * (size_t)HW);
@@ -201,6 +201,7 @@ struct Plan {
     std::vector<int> grad_ptr, grad_ent;          // CSR: pose -> (edge<<1 | neg)
     std::vector<int> slotmap;                     // (npose x npose) -> slot or -1
     std::vector<int> sched;                       // accumulate task order: e * nchunks + c
+    std::vector<int> sched4;                      // the same as {e, c, ii_loc[e], jj_loc[e]} records
     std::vector<std::pair<int, int>> pairs;       // slot nblk0.. -> unordered pose pair (a<b)
     float K[4] = {0, 0, 0, 0};
 };
@@ -780,6 +781,18 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     if (rc) return rc;
     const auto s1 = std::chrono::steady_clock::now();
     build_schedule(c.plan.ii_loc, c.plan.jj_loc, c.L.nchunks, c.plan.sched);
+    {   // the accumulate's task records carry the edge's keyframes: one load, not three levels
+        Plan& pl = c.plan;
+        const int nc = c.L.nchunks;
+        pl.sched4.resize(4 * pl.sched.size());
+        for (size_t t = 0; t < pl.sched.size(); t++) {
+            const int e = pl.sched[t] / nc;
+            pl.sched4[4 * t] = e;
+            pl.sched4[4 * t + 1] = pl.sched[t] - e * nc;
+            pl.sched4[4 * t + 2] = pl.ii_loc[e];
+            pl.sched4[4 * t + 3] = pl.jj_loc[e];
+        }
+    }
     if (prof_host)
         fprintf(stderr, "gn host: build_plan %.0f us, schedule %.0f us\n",
                 std::chrono::duration<double, std::micro>(s1 - s0).count(),
@@ -789,7 +802,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     // the workspace's plan integers (flags .. sched, one contiguous span of the layout) as an
     // image in pinned memory, one asynchronous copy
     {
-        const size_t lo = L.flags, hi = L.sched + sizeof(int) * p.sched.size();
+        const size_t lo = L.flags, hi = L.sched + sizeof(int) * p.sched4.size();
         const size_t nslot = c.need_slotmap ? p.slotmap.size() : 0;
         if (c.need_slotmap) {
             rc = c.alloc_dense(L.npad, (int)std::max<int64_t>(a.N - 1, 0));
@@ -813,7 +826,7 @@ int setup(const m3s_gn_args& a, Ctx& c) {
         put(L.blk_ref, p.blk_ref);
         put(L.grad_ptr, p.grad_ptr);
         put(L.grad_ent, p.grad_ent);
-        put(L.sched, p.sched);
+        put(L.sched, p.sched4);
         M3S_HIP_CHECK(hipMemcpyAsync(c.ws + lo, h, hi - lo, hipMemcpyHostToDevice, c.st));
         if (nslot) {  // the dense (npose x npose) slot table
             std::memcpy(h + (hi - lo), p.slotmap.data(), sizeof(int) * nslot);
@@ -930,12 +943,12 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
         if (c.packed)
             M3S_HIP_CHECK(launch_accum_packed(a.mode, grid, c.st, a.Twc, a.Xs, c.at<float>(L.zs),
                                               c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
-                                              c.at<int4>(L.pack), c.P, c.at<int>(L.sched),
+                                              c.at<int4>(L.pack), c.P, c.at<int4>(L.sched),
                                               c.at<float>(L.partials), flags));
         else
             M3S_HIP_CHECK(launch_accum(a.mode, c.vec, grid, c.st, a.Twc, a.Xs, a.Cs,
                                        c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), c.es, c.P,
-                                       c.at<int>(L.sched), c.at<float>(L.partials),
+                                       c.at<int4>(L.sched), c.at<float>(L.partials),
                                        flags));
         g_prof.mark(c.st, true);
         M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,

@@ -86,7 +86,7 @@ hipError_t launch_assemble_ref(hipStream_t st, const float* ref, const int* blk_
 
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
                         const float* Xs, const float* Cs, const int* ii_loc, const int* jj_loc,
-                        const EdgeSrc& es, const AccParams& P, const int* sched, float* partials,
+                        const EdgeSrc& es, const AccParams& P, const int4* sched, float* partials,
                         const int* flags);
 hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
                        const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P,
@@ -94,7 +94,7 @@ hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, 
 hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,
-                               const int* sched, float* partials, const int* flags);
+                               const int4* sched, float* partials, const int* flags);
 hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
                               const float* Twc, const int* ii_loc, double* edgeblk,
                               const int* flags);

@@ -334,18 +334,29 @@ def test_cfg1_keyframe_pair_matches_oracle(backend, oracle, mode):
     assert np.abs(dx_g - dx_o).max() < 1e-5 * max(np.abs(T_o).max(), 1.0)
 
 
-@pytest.mark.timeout(400)
-def test_cfg4_full_size_one_iteration_and_ten_iteration_properties(backend, oracle):
+@pytest.mark.timeout(600)
+def test_cfg4_full_size_one_and_ten_iterations(backend, oracle):
     """BASELINE config 4 at full size on one GPU (256 keyframes, 1024 pairs = 2048 directed
-    edges, 512x384, gauss_newton_rays): one iteration against the oracle at 1e-5, then the
-    timed 10-iteration call's properties -- finite, deterministic (two runs bitwise equal),
-    converging (the last update far below the first)."""
+    edges, 512x384, gauss_newton_rays).  One iteration: at this size the first pose update is
+    only determined to the fp32 rounding of its ~4e8 summed terms (sigma = the distance between
+    the oracle's reference order and the same float terms summed in double: 4e-6 on this graph,
+    2.5e-5 on bench.py's), and per-point rounding differences (the op's affine-map form of
+    T_ij x, gn_accum.hip) move it by the same amount -- so the op must agree with both within
+    max(1e-5, 4 sigma).  The formula itself is pinned at 1e-5 by the reference-order mode
+    (test_gpu_gn_reference_order.py).  Ten iterations (the timed call): within the north-star
+    1e-5 of the oracle, finite, deterministic (two runs bitwise equal), converging."""
     g = synth.make_graph("cfg4")
-    T1, _ = _run_gpu(backend, g, "rays", 1)
+    T1, dx1 = _run_gpu(backend, g, "rays", 1)
     T_o, _, _ = _run_oracle(oracle, g, "rays", 1)
-    assert _rel(T1, T_o) < 1e-5, _rel(T1, T_o)
+    with oracle.exact_sums():
+        T_exact, _, _ = _run_oracle(oracle, g, "rays", 1)
+    bound = max(1e-5, 4 * _rel(T_o, T_exact))
+    assert _rel(T1, T_o) < bound, (_rel(T1, T_o), bound)
+    assert _rel(T1, T_exact) < bound, (_rel(T1, T_exact), bound)
     Ta, dxa = _run_gpu(backend, g, "rays", 10)
     Tb, dxb = _run_gpu(backend, g, "rays", 10)
     assert np.isfinite(Ta).all() and np.array_equal(Ta, Tb) and np.array_equal(dxa, dxb)
-    _, dx1 = _run_gpu(backend, g, "rays", 1)
     assert np.abs(dxa).max() < 1e-2 * np.abs(dx1).max()
+    T10, _, it = _run_oracle(oracle, g, "rays", 10)
+    assert it == 10
+    assert _rel(Ta, T10) < 1e-5, _rel(Ta, T10)

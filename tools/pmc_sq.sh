@@ -10,7 +10,7 @@ CFG="${CFG:-cfg3}"
 run_pass() {  # $1 = pass name, rest = counters
     local name=$1; shift
     timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- \
-        python bench.py --config $CFG --steps 1 --warmup 0 --iters 3 --no-cpu-baseline \
+        python bench.py --config $CFG --steps 1 --warmup 0 --iters 3 --no-cpu-baseline --no-matching \
         > $OUT/$name.log 2>&1
     local rc=$?; echo "pmc $name rc=$rc"; return $rc
 }
