@@ -217,7 +217,8 @@ def main():
 def matching_bench(dev, reps=10):
     """Matching ops (SURVEY.md §8(d) 'matching pairs/s, B=1 and B=8'): iter_proj + refine_matches
     at 512x384 (inputs resident, base.yaml matching parameters), kernel time from events on the
-    current stream; plus the whole match_iterative_proj glue call.  Bytes per pixel as SURVEY
+    current stream; plus the whole match_iterative_proj call (the fused pipeline op, and the torch
+    glue around the two ops for comparison).  Bytes per pixel as SURVEY
     §8(d): iter_proj 65 B, refine 128 B (+ the candidate gathers, served from L2/MALL)."""
     import mast3r_slam_backends as mb
     from m3s import synth
@@ -257,14 +258,18 @@ def matching_bench(dev, reps=10):
             if r >= 2:
                 t_gather += ev[1].elapsed_time(ev[2]) / reps
         del os.environ["M3S_REFINE_LDS"]
-        for _ in range(2):
-            match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init)
-        torch.cuda.synchronize()
-        t_glue = (time.perf_counter() - t0) / reps * 1e3
+        def wall_ms(fused):
+            for _ in range(2):
+                match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=fused)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=fused)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps * 1e3
+
+        t_glue = wall_ms(True)        # the fused pipeline op (csrc/match_glue.hip)
+        t_torch_glue = wall_ms(False)  # the reference's torch glue around the two ops
         npx = B * h * w
         res[f"B{B}"] = {
             "pairs_per_s_kernels": B / ((t_ip + t_rf) * 1e-3),
@@ -273,6 +278,7 @@ def matching_bench(dev, reps=10):
             "refine_ms": t_rf,
             "refine_lds_tile_kernel_ms": t_gather,
             "match_iterative_proj_ms": t_glue,
+            "match_iterative_proj_torch_glue_ms": t_torch_glue,
             "iter_proj_GBps": 65 * npx / (t_ip * 1e-3) / 1e9,
             "refine_GBps": 128 * npx / (t_rf * 1e-3) / 1e9,
             "refine_candidate_GBps": 245 * 48 * npx / (t_rf * 1e-3) / 1e9,

@@ -72,6 +72,22 @@ int m3s_refine_matches_f64(const double* D11, const double* D21,
                            int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
                            int radius, int dilation_max, void* stream);
 
+/*
+ * match_iterative_proj -- the whole matching pipeline of the reference's Python caller
+ * (matching.py:52-90: prep_for_iter_proj, iter_proj, p.long(), the occlusion test, refine on
+ * .half() descriptors, pixel_to_lin) in five launches.
+ *   X11, X21  [B,H,W,3] f32      D11, D21 [B,H,W,F] f32
+ *   idx_init  [B,H*W]   i64 or NULL (identity start)
+ *   idx_out   [B,H*W]   i64 out  (u + W v)      valid_out [B,H*W] u8 out (bool)
+ *   ws        device workspace of >= m3s_match_workspace_bytes(B, H, W, F) bytes
+ */
+size_t m3s_match_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t F);
+int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D11, const float* D21,
+                             const int64_t* idx_init, int64_t B, int64_t H, int64_t W, int64_t F,
+                             int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
+                             int radius, int dilation_max, int64_t* idx_out, uint8_t* valid_out,
+                             void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------- Gauss-Newton ---------------- */
 
 enum { M3S_GN_POINTS = 0, M3S_GN_RAYS = 1, M3S_GN_CALIB = 2 };

@@ -151,6 +151,18 @@ __device__ __forceinline__ bool inside_image(int64_t u, int64_t v, int W, int H)
 
 typedef _Float16 half_t;
 
+// The refined match as (u, v), or (fused matching pipeline) as the linear index u + W v the
+// caller forms next (matching.py:13-15, 87).
+__device__ __forceinline__ void store_match(int64_t* __restrict__ p1_new, int64_t* __restrict__ lin,
+                                            int64_t g, int W, int64_t u, int64_t v) {
+    if (lin) {
+        lin[g] = u + (int64_t)W * v;
+    } else {
+        p1_new[g * 2 + 0] = u;
+        p1_new[g * 2 + 1] = v;
+    }
+}
+
 // F = 24 fp16 fast path: the query descriptor lives in registers (3 x 16 B loads),
 // each candidate row is 48 B = 3 x dwordx4.  Sequential fp16 accumulation exactly as
 // c10::Half: round after every * and after every +=.
@@ -234,8 +246,8 @@ __device__ __forceinline__ void score_f16_multi(const half2_t (&q2)[F / 2], cons
 template <int F, int R>
 __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
     const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21,
-    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int H, int W, int64_t N,
-    int64_t B, TileMap tm, int radius_rt, int dilation_max) {
+    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int64_t* __restrict__ lin, int H,
+    int W, int64_t N, int64_t B, TileMap tm, int radius_rt, int dilation_max) {
     static_assert(F % 8 == 0, "vector path needs F % 8 == 0");
     int64_t g;
     if (!tile_pixel(tm, B, W, H, g)) return;
@@ -307,8 +319,7 @@ __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
         u0 = u_new;
         v0 = v_new;
     }
-    p1_new[g * 2 + 0] = u_new;
-    p1_new[g * 2 + 1] = v_new;
+    store_match(p1_new, lin, g, W, u_new, v_new);
 }
 
 // ---------------------------------------------------------------------------------
@@ -364,8 +375,8 @@ __device__ __forceinline__ void block_minmax4(int (&v)[4], int* red /* [8 waves]
 template <int F, int R>
 __global__ __launch_bounds__(kLdsThreads) void refine_lds_kernel(
     const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21,
-    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int H, int W, int64_t B,
-    LdsTileMap tm, int dilation_max, int* __restrict__ stats) {
+    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int64_t* __restrict__ lin, int H,
+    int W, int64_t B, LdsTileMap tm, int dilation_max, int* __restrict__ stats) {
     static_assert(F == 24, "LDS tile path is for 24-d fp16 descriptors (48-B rows)");
     constexpr int SC = 2 * R + 1;
     constexpr int RU4 = F / 8;  // uint4 per descriptor row
@@ -520,10 +531,7 @@ __global__ __launch_bounds__(kLdsThreads) void refine_lds_kernel(
         v0 = v_new;
         if (use_lds) __syncthreads();  // the next level's staging overwrites the tile
     }
-    if (active) {
-        p1_new[g * 2 + 0] = u_new;
-        p1_new[g * 2 + 1] = v_new;
-    }
+    if (active) store_match(p1_new, lin, g, W, u_new, v_new);
     if (stats && threadIdx.x == 0 && n_global_levels)
         atomicAdd(stats, n_global_levels);  // diagnostics: levels that did not fit the LDS tile
 }
@@ -542,8 +550,8 @@ __device__ __forceinline__ double zero_score<double>() { return 0.0; }
 template <typename T>
 __global__ __launch_bounds__(kBlock) void refine_generic_kernel(
     const T* __restrict__ D11, const T* __restrict__ D21, const int64_t* __restrict__ p1,
-    int64_t* __restrict__ p1_new, int H, int W, int64_t N, int64_t F, int64_t total, int radius,
-    int dilation_max, T max_init) {
+    int64_t* __restrict__ p1_new, int64_t* __restrict__ lin, int H, int W, int64_t N, int64_t F,
+    int64_t total, int radius, int dilation_max, T max_init) {
     const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (g >= total) return;
     const int64_t b = g / N;
@@ -578,8 +586,7 @@ __global__ __launch_bounds__(kBlock) void refine_generic_kernel(
         u0 = u_new;
         v0 = v_new;
     }
-    p1_new[g * 2 + 0] = u_new;
-    p1_new[g * 2 + 1] = v_new;
+    store_match(p1_new, lin, g, W, u_new, v_new);
 }
 
 inline unsigned grid_for(int64_t total) { return (unsigned)((total + kBlock - 1) / kBlock); }
@@ -614,10 +621,12 @@ static int refine_checks(const void* D11, const void* D21, const void* p1, void*
     return M3S_OK;
 }
 
-extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
-                                      int64_t* p1_new, int64_t B, int64_t H, int64_t W, int64_t N,
-                                      int64_t F, int radius, int dilation_max, void* stream) {
-    int rc = refine_checks(D11, D21, p1, p1_new, B, H, W, N, F, radius, dilation_max);
+namespace m3s {
+// refine_matches on fp16 descriptors; lin != nullptr writes u + W v per pixel instead of (u, v)
+int refine_f16_launch(const uint16_t* D11, const uint16_t* D21, const int64_t* p1, int64_t* p1_new,
+                      int64_t* lin, int64_t B, int64_t H, int64_t W, int64_t N, int64_t F, int radius,
+                      int dilation_max, hipStream_t st) {
+    int rc = refine_checks(D11, D21, p1, lin ? (void*)lin : (void*)p1_new, B, H, W, N, F, radius, dilation_max);
     if (rc) return rc;
     const int64_t total = B * N;
     if (total == 0) return M3S_OK;
@@ -632,9 +641,8 @@ extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, 
         tm.ntiles = tm.tiles_x * tm.tiles_y;
         const int64_t nblk = (int64_t)tm.ntiles * B;
         const int64_t grid = (nblk + 7) / 8 * 8;
-        hipLaunchKernelGGL((refine_lds_kernel<24, 3>), dim3((unsigned)grid), dim3(kLdsThreads), 0,
-                           (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, B, tm,
-                           dilation_max, (int*)nullptr);
+        hipLaunchKernelGGL((refine_lds_kernel<24, 3>), dim3((unsigned)grid), dim3(kLdsThreads), 0, st, D11,
+                           D21, p1, p1_new, lin, (int)H, (int)W, B, tm, dilation_max, (int*)nullptr);
     } else if (F == 24 && aligned && N == H * W) {
         TileMap tm;
         tm.tiles_x = (int)((W + kTile - 1) / kTile);
@@ -643,21 +651,27 @@ extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, 
         const int64_t nblk = (int64_t)tm.ntiles * B;
         const int64_t grid = (nblk + 7) / 8 * 8;  // whole rounds of the 8 XCDs
         if (radius == 3)  // base.yaml:13
-            hipLaunchKernelGGL((refine_f16_kernel<24, 3>), dim3((unsigned)grid), dim3(kBlock), 0,
-                               (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, B, tm,
-                               radius, dilation_max);
+            hipLaunchKernelGGL((refine_f16_kernel<24, 3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21,
+                               p1, p1_new, lin, (int)H, (int)W, N, B, tm, radius, dilation_max);
         else
-            hipLaunchKernelGGL((refine_f16_kernel<24, -1>), dim3((unsigned)grid), dim3(kBlock), 0,
-                               (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, B, tm,
-                               radius, dilation_max);
+            hipLaunchKernelGGL((refine_f16_kernel<24, -1>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21,
+                               p1, p1_new, lin, (int)H, (int)W, N, B, tm, radius, dilation_max);
     } else {
-        hipLaunchKernelGGL(refine_generic_kernel<half_t>, dim3(grid_for(total)), dim3(kBlock), 0,
-                           (hipStream_t)stream, reinterpret_cast<const half_t*>(D11),
-                           reinterpret_cast<const half_t*>(D21), p1, p1_new, (int)H, (int)W, N, F,
-                           total, radius, dilation_max, (half_t)kRefineHalfMaxInit);
+        hipLaunchKernelGGL(refine_generic_kernel<half_t>, dim3(grid_for(total)), dim3(kBlock), 0, st,
+                           reinterpret_cast<const half_t*>(D11), reinterpret_cast<const half_t*>(D21), p1,
+                           p1_new, lin, (int)H, (int)W, N, F, total, radius, dilation_max,
+                           (half_t)kRefineHalfMaxInit);
     }
     M3S_LAUNCH_CHECK();
     return M3S_OK;
+}
+}  // namespace m3s
+
+extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
+                                      int64_t* p1_new, int64_t B, int64_t H, int64_t W, int64_t N,
+                                      int64_t F, int radius, int dilation_max, void* stream) {
+    return m3s::refine_f16_launch(D11, D21, p1, p1_new, nullptr, B, H, W, N, F, radius, dilation_max,
+                                  (hipStream_t)stream);
 }
 
 extern "C" int m3s_refine_matches_f32(const float* D11, const float* D21, const int64_t* p1,
@@ -668,7 +682,7 @@ extern "C" int m3s_refine_matches_f32(const float* D11, const float* D21, const 
     const int64_t total = B * N;
     if (total == 0) return M3S_OK;
     hipLaunchKernelGGL(refine_generic_kernel<float>, dim3(grid_for(total)), dim3(kBlock), 0,
-                       (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, F, total,
+                       (hipStream_t)stream, D11, D21, p1, p1_new, nullptr, (int)H, (int)W, N, F, total,
                        radius, dilation_max, kRefineFloatMaxInit);
     M3S_LAUNCH_CHECK();
     return M3S_OK;
@@ -682,7 +696,7 @@ extern "C" int m3s_refine_matches_f64(const double* D11, const double* D21, cons
     const int64_t total = B * N;
     if (total == 0) return M3S_OK;
     hipLaunchKernelGGL(refine_generic_kernel<double>, dim3(grid_for(total)), dim3(kBlock), 0,
-                       (hipStream_t)stream, D11, D21, p1, p1_new, (int)H, (int)W, N, F, total,
+                       (hipStream_t)stream, D11, D21, p1, p1_new, nullptr, (int)H, (int)W, N, F, total,
                        radius, dilation_max, kRefineDoubleMaxInit);
     M3S_LAUNCH_CHECK();
     return M3S_OK;

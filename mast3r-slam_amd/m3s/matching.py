@@ -8,7 +8,10 @@ Mirror of mast3r_slam/matching.py:8-90 (same function names, arguments and outpu
   the PRE-refine pixels -> refine_matches on fp16 descriptors -> linear index
   (matching.py:52-90).
 
-The heavy lifting runs in the gfx950 kernels of ``mast3r_slam_backends``.
+On HIP tensors ``match_iterative_proj`` runs as ONE op (``mast3r_slam_backends.match_iterative_proj``:
+prep, iter_proj, occlusion, refine and the linear index in four launches, the glue's float ops in
+the reference's host arithmetic); ``fused=False`` runs the torch glue below around the two
+reference ops instead (its normalize / conv2d round as torch's GPU kernels do).
 """
 from __future__ import annotations
 
@@ -49,10 +52,20 @@ def prep_for_iter_proj(X11, X21, idx_1_to_2_init):
     return rays_with_grad, pts3d_norm, p_init
 
 
-def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None):
+def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, fused=None):
     cfg = (cfg if cfg is not None else _global_config)["matching"]
     b, h, w = X21.shape[:3]
     device = X11.device
+    if fused is None:
+        fused = device.type == "cuda" and hasattr(mast3r_slam_backends, "match_iterative_proj")
+    if fused:
+        idx_1_to_2, valid = mast3r_slam_backends.match_iterative_proj(
+            X11.contiguous(), X21.contiguous(), D11.contiguous(), D21.contiguous(),
+            None if idx_1_to_2_init is None else idx_1_to_2_init.contiguous(),
+            cfg["max_iter"], cfg["lambda_init"], cfg["convergence_thresh"], cfg["dist_thresh"],
+            cfg["radius"], cfg["dilation_max"],
+        )
+        return idx_1_to_2, valid
 
     rays_with_grad, pts3d_norm, p_init = prep_for_iter_proj(X11, X21, idx_1_to_2_init)
     p1, valid_proj2 = mast3r_slam_backends.iter_proj(

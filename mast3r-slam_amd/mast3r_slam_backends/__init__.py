@@ -56,6 +56,10 @@ lib.m3s_iter_proj.argtypes = [_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _vp]
 lib.m3s_refine_matches_f16.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_refine_matches_f32.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_refine_matches_f64.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
+lib.m3s_match_workspace_bytes.argtypes = [_c_int64] * 4
+lib.m3s_match_workspace_bytes.restype = ctypes.c_size_t
+lib.m3s_match_iterative_proj.argtypes = ([_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _f, _i, _i]
+                                         + [_vp, _vp, _vp, ctypes.c_size_t, _vp])
 lib.m3s_gn_workspace_bytes.restype = ctypes.c_size_t
 lib.m3s_gn_workspace_bytes.argtypes = [_i, _c_int64, _c_int64, _c_int64, _c_int64]
 
@@ -244,6 +248,40 @@ def refine_matches(D11, D21, p1, window_size, dilation_max):
         )
     _raise(rc, "refine_matches")
     return [p1_new]
+
+
+def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init, max_iter, lambda_init, cost_thresh,
+                         dist_thresh, radius, dilation_max):
+    """The whole Python matching caller (matching.py:52-90) as one op: prep_for_iter_proj,
+    iter_proj, ``p.long()``, the occlusion test on the pre-refine pixels, refine_matches on the
+    ``.half()`` descriptors and ``pixel_to_lin`` -> [idx i64[B,H*W], valid bool[B,H*W,1]].
+    Extension op (not in the reference's module); the glue's float ops follow the reference's
+    host arithmetic (csrc/match_glue.hip)."""
+    _check(X11, "X11", torch.float32, 4)
+    _check(X21, "X21", torch.float32, 4)
+    _check(D11, "D11", torch.float32, 4)
+    _check(D21, "D21", torch.float32, 4)
+    if idx_1_to_2_init is not None:
+        _check(idx_1_to_2_init, "idx_1_to_2_init", torch.int64, 2)
+    dev = _on_device(X11=X11, X21=X21, D11=D11, D21=D21, idx_1_to_2_init=idx_1_to_2_init)
+    B, H, W, _ = X11.shape
+    F = D11.shape[3]
+    if X11.shape[3] != 3 or X21.shape != X11.shape or D21.shape != D11.shape or D11.shape[:3] != (B, H, W):
+        raise RuntimeError("match_iterative_proj: expected X11, X21 [B,H,W,3] and D11, D21 [B,H,W,F]")
+    if idx_1_to_2_init is not None and tuple(idx_1_to_2_init.shape) != (B, H * W):
+        raise RuntimeError("match_iterative_proj: idx_1_to_2_init must be [B,H*W]")
+    idx = torch.empty((B, H * W), dtype=torch.int64, device=dev)
+    valid = torch.empty((B, H * W, 1), dtype=torch.bool, device=dev)
+    nbytes = int(lib.m3s_match_workspace_bytes(B, H, W, F))
+    ws = torch.empty((max(nbytes, 1),), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.m3s_match_iterative_proj(
+            _ptr(X11), _ptr(X21), _ptr(D11), _ptr(D21), _ptr(idx_1_to_2_init), B, H, W, F,
+            int(max_iter), float(lambda_init), float(cost_thresh), float(dist_thresh), int(radius),
+            int(dilation_max), _ptr(idx), _ptr(valid), _ptr(ws), nbytes, _stream(dev),
+        )
+    _raise(rc, "match_iterative_proj")
+    return [idx, valid]
 
 
 # ---------------------------------------------------------------------------------

@@ -194,6 +194,79 @@ void oracle_iter_proj(const float* rays, const float* pts, const float* p_init,
  * 0.0 (SURVEY.md §7.3 hard part 1).  Only strictly positive scores can move a match. */
 #define REFINE_MAX_SCORE_INIT 0.0f
 
+/* ---------------- matching glue (reference matching.py:25-90, image.py:5-38) ----------------
+ * The reference's Python glue with the float arithmetic torch uses on the host (pinned by the
+ * reference-generated tests/golden/glue_golden.npz):
+ *   F.normalize / linalg.norm: sqrt(fma(x2, x2, fma(x1, x1, x0 * x0))), x / max(n, 1e-12)
+ *   img_gradient: reflect pad 1, depthwise 3x3 conv as acc = fma(w, x, acc) over the taps in
+ *   row-major order from 0, w = (1/32) * [[-3,0,3],[-10,0,10],[-3,0,3]] and its transpose.   */
+static inline void normalize3_ref(const float* x, float* y) {
+    const float n = fmaxf(sqrtf(fmaf(x[2], x[2], fmaf(x[1], x[1], x[0] * x[0]))), 1e-12f);
+    y[0] = x[0] / n;
+    y[1] = x[1] / n;
+    y[2] = x[2] / n;
+}
+
+static inline int64_t reflect1_ref(int64_t i, int64_t n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
+
+void oracle_match_prep(const float* X11, const float* X21, const int64_t* idx_init, int64_t B, int64_t H,
+                       int64_t W, float* rays9, float* pts, float* p_init) {
+    static const float wx[9] = {-3.0f / 32, 0.0f, 3.0f / 32, -10.0f / 32, 0.0f, 10.0f / 32, -3.0f / 32, 0.0f, 3.0f / 32};
+    static const float wy[9] = {-3.0f / 32, -10.0f / 32, -3.0f / 32, 0.0f, 0.0f, 0.0f, 3.0f / 32, 10.0f / 32, 3.0f / 32};
+    const int64_t HW = H * W;
+#pragma omp parallel for schedule(static)
+    for (int64_t n = 0; n < B * HW; n++) {
+        const int64_t b = n / HW, k = n % HW, y = k / W, x = k % W;
+        float r[9][3];
+        for (int t = 0; t < 9; t++) {
+            const int64_t yy = reflect1_ref(y + t / 3 - 1, H), xx = reflect1_ref(x + t % 3 - 1, W);
+            normalize3_ref(X11 + ((b * HW) + yy * W + xx) * 3, r[t]);
+        }
+        float* o = rays9 + n * 9;
+        for (int c = 0; c < 3; c++) {
+            float gx = 0.0f, gy = 0.0f;
+            for (int t = 0; t < 9; t++) {
+                gx = fmaf(wx[t], r[t][c], gx);
+                gy = fmaf(wy[t], r[t][c], gy);
+            }
+            o[c] = r[4][c];
+            o[3 + c] = gx;
+            o[6 + c] = gy;
+        }
+        normalize3_ref(X21 + n * 3, pts + n * 3);
+        int64_t u = x, v = y;
+        if (idx_init) { /* lin_to_pixel (matching.py:18-22): Python floor // and % */
+            const int64_t id = idx_init[n];
+            v = id / W;
+            u = id - v * W;
+            if (u < 0) {
+                u += W;
+                v -= 1;
+            }
+        }
+        p_init[n * 2] = (float)u;
+        p_init[n * 2 + 1] = (float)v;
+    }
+}
+
+/* p.long(), occlusion test ||X11[p1] - X21|| < dist_thresh, valid = converged & that
+ * (matching.py:66-76) */
+void oracle_match_post(const float* X11, const float* X21, const float* p_new, const uint8_t* conv,
+                       int64_t B, int64_t H, int64_t W, float dist_thresh, int64_t* p1, uint8_t* valid) {
+    const int64_t HW = H * W;
+    for (int64_t n = 0; n < B * HW; n++) {
+        const int64_t b = n / HW;
+        const int64_t u = (int64_t)p_new[n * 2], v = (int64_t)p_new[n * 2 + 1];
+        const float* a = X11 + (b * HW + v * W + u) * 3;
+        const float* q = X21 + n * 3;
+        const float d0 = a[0] - q[0], d1 = a[1] - q[1], d2 = a[2] - q[2];
+        const float dist = sqrtf(fmaf(d2, d2, fmaf(d1, d1, d0 * d0)));
+        valid[n] = conv[n] && dist < dist_thresh;
+        p1[n * 2] = u;
+        p1[n * 2 + 1] = v;
+    }
+}
+
 static inline int inside_image(int64_t u, int64_t v, int64_t W, int64_t H) {
     return v >= 0 && v < H && u >= 0 && u < W; /* matching_kernels.cu:17-19 */
 }

@@ -34,6 +34,11 @@ extern "C" {
 #endif
 
 /* matching_kernels.cu:119-275 (iter_proj_kernel) + :279-316 (launcher) */
+/* matching glue of the reference's Python caller (matching.py:25-90), host arithmetic */
+void oracle_match_prep(const float* X11, const float* X21, const int64_t* idx_init, int64_t B, int64_t H,
+                       int64_t W, float* rays9, float* pts, float* p_init);
+void oracle_match_post(const float* X11, const float* X21, const float* p_new, const uint8_t* conv,
+                       int64_t B, int64_t H, int64_t W, float dist_thresh, int64_t* p1, uint8_t* valid);
 void oracle_iter_proj(const float* rays, const float* pts, const float* p_init,
                       float* p_new, uint8_t* converged,
                       int64_t B, int64_t H, int64_t W, int64_t N,

@@ -36,6 +36,8 @@ _lib.oracle_f16_to_f32.restype = _f
 _lib.oracle_f16_to_f32.argtypes = [ctypes.c_uint16]
 _lib.oracle_num_threads.restype = _i
 _lib.oracle_set_exact_sums.argtypes = [_i]
+_lib.oracle_match_prep.argtypes = [_vp] * 3 + [_i64] * 3 + [_vp] * 3
+_lib.oracle_match_post.argtypes = [_vp] * 4 + [_i64] * 3 + [_f, _vp, _vp]
 
 
 class GNParams(ctypes.Structure):
@@ -117,6 +119,42 @@ def iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh):
     _lib.oracle_iter_proj(_p(rays), _p(pts), _p(p_init), _p(p_new), _p(conv), B, H, W, N,
                           int(max_iter), float(lambda_init), float(cost_thresh))
     return p_new, conv.astype(bool)
+
+
+def match_prep(X11, X21, idx_init=None):
+    """prep_for_iter_proj (matching.py:25-49) with the reference's host arithmetic
+    -> rays_with_grad [B,H,W,9], pts3d_norm [B,HW,3], p_init [B,HW,2]."""
+    X11 = _c(X11, np.float32)
+    X21 = _c(X21, np.float32)
+    B, H, W, _ = X11.shape
+    rays = np.zeros((B, H, W, 9), np.float32)
+    pts = np.zeros((B, H * W, 3), np.float32)
+    p_init = np.zeros((B, H * W, 2), np.float32)
+    ii = None if idx_init is None else _c(idx_init, np.int64)
+    _lib.oracle_match_prep(_p(X11), _p(X21), _p(ii) if ii is not None else None, B, H, W, _p(rays), _p(pts),
+                           _p(p_init))
+    return rays, pts, p_init
+
+
+def match_iterative_proj(X11, X21, D11, D21, idx_init, max_iter, lambda_init, cost_thresh, dist_thresh,
+                         radius, dilation_max):
+    """The reference's match_iterative_proj (matching.py:52-90): glue with the host arithmetic,
+    the oracle's iter_proj / refine_matches -> idx [B,HW] i64, valid [B,HW,1] bool."""
+    X11 = _c(X11, np.float32)
+    X21 = _c(X21, np.float32)
+    B, H, W, _ = X11.shape
+    rays, pts, p_init = match_prep(X11, X21, idx_init)
+    p_new, conv = iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh)
+    p1 = np.zeros((B, H * W, 2), np.int64)
+    valid = np.zeros((B, H * W), np.uint8)
+    conv8 = np.ascontiguousarray(conv.astype(np.uint8))
+    _lib.oracle_match_post(_p(X11), _p(X21), _p(p_new), _p(conv8), B, H, W, float(dist_thresh), _p(p1),
+                           _p(valid))
+    if radius > 0:
+        d11 = np.asarray(D11, np.float32).astype(np.float16)
+        d21 = np.asarray(D21, np.float32).reshape(B, H * W, -1).astype(np.float16)
+        p1 = refine_matches(d11, d21, p1, radius, dilation_max)
+    return p1[..., 0] + W * p1[..., 1], valid.astype(bool)[..., None]
 
 
 def refine_matches(D11, D21, p1, radius, dilation_max):

@@ -123,3 +123,26 @@ def test_factor_graph_hands_the_op_the_reference_arguments(name):
     # Twc is a view into the stacked pose tensor that is written back for ids[pin:]
     np.testing.assert_array_equal(store.T_WC[torch.tensor(kf_ids[1:])].numpy(), GOLD[f"fg_{name}_upd_T"])
     assert GOLD[f"fg_{name}_upd_idx"].tolist() == kf_ids[1:]
+
+
+def test_oracle_match_glue_restatement_matches_reference(oracle):
+    """The oracle's C restatement of the matching glue (oracle_match_prep / _post: the reference's
+    host arithmetic -- fma-chain normalize, row-major fma conv taps, Python floor // and %) is
+    bitwise the reference's prep_for_iter_proj output, and its whole pipeline (with the oracle's
+    kernels) reproduces the reference's match_iterative_proj indices and flags.  This pins the
+    checker of the fused HIP pipeline (test_gpu_matching.py)."""
+    from m3s.config import config as cfg0
+
+    rays, pts, p_init = oracle.match_prep(GOLD["X11"], GOLD["X21"], None)
+    np.testing.assert_array_equal(rays, GOLD["prep_rays"])
+    np.testing.assert_array_equal(pts, GOLD["prep_pts"])
+    np.testing.assert_array_equal(p_init, GOLD["prep_pinit"])
+    _, _, p_w = oracle.match_prep(GOLD["X11"], GOLD["X21"], GOLD["idx_init"])
+    np.testing.assert_array_equal(p_w, GOLD["prep_pinit_warm"])
+    c = cfg0["matching"]
+    for tag, init in (("id", None), ("warm", GOLD["idx_init"])):
+        idx, valid = oracle.match_iterative_proj(GOLD["X11"], GOLD["X21"], GOLD["D11"], GOLD["D21"], init,
+                                                 c["max_iter"], c["lambda_init"], c["convergence_thresh"],
+                                                 c["dist_thresh"], c["radius"], c["dilation_max"])
+        np.testing.assert_array_equal(idx, GOLD[f"match_{tag}_idx"])
+        np.testing.assert_array_equal(valid, GOLD[f"match_{tag}_valid"])

@@ -163,14 +163,56 @@ def test_match_pipeline_against_golden(backend, oracle):
 
     ob.iter_proj, ob.refine_matches = o_iter_proj, o_refine
     for tag, init in (("id", None), ("warm", t("idx_init"))):
-        idx, valid = mm.match_iterative_proj(t("X11"), t("X21"), t("D11"), t("D21"), init)
+        idx, valid = mm.match_iterative_proj(t("X11"), t("X21"), t("D11"), t("D21"), init, fused=False)
         real = mm.mast3r_slam_backends
         try:
             mm.mast3r_slam_backends = ob
-            idx_o, valid_o = mm.match_iterative_proj(t("X11"), t("X21"), t("D11"), t("D21"), init)
+            idx_o, valid_o = mm.match_iterative_proj(t("X11"), t("X21"), t("D11"), t("D21"), init,
+                                                     fused=False)
         finally:
             mm.mast3r_slam_backends = real
         assert torch.equal(idx, idx_o) and torch.equal(valid, valid_o), tag
         agree = (idx.cpu().numpy() == gold[f"match_{tag}_idx"]).mean()
         vagree = (valid.cpu().numpy() == gold[f"match_{tag}_valid"]).mean()
         assert agree > 0.999 and vagree > 0.999, (tag, agree, vagree)
+
+
+def test_fused_pipeline_bitwise_equals_reference_fixture(backend):
+    """The fused op (csrc/match_glue.hip: prep + iter_proj + occlusion + refine + linear index)
+    against the fixture made by running the REFERENCE's matching.py glue (on the host, with the
+    oracle as its two kernels): identical indices and valid flags for the identity and the
+    warm start, and the torch-glue path on the same GPU differs from it only where torch's GPU
+    normalize / conv2d round differently."""
+    import os
+
+    import m3s.matching as mm
+
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "glue_golden.npz"))
+    t = lambda k: torch.from_numpy(gold[k]).cuda()
+    for tag, init in (("id", None), ("warm", t("idx_init"))):
+        idx, valid = mm.match_iterative_proj(t("X11"), t("X21"), t("D11"), t("D21"), init)
+        assert idx.dtype == torch.int64 and valid.dtype == torch.bool and valid.shape[-1] == 1
+        assert np.array_equal(idx.cpu().numpy(), gold[f"match_{tag}_idx"]), (
+            tag, (idx.cpu().numpy() != gold[f"match_{tag}_idx"]).sum())
+        assert np.array_equal(valid.cpu().numpy(), gold[f"match_{tag}_valid"]), tag
+
+
+@pytest.mark.parametrize("B,H,W,radius", [(1, 384, 512, 3), (2, 37, 53, 3), (1, 24, 32, 0), (2, 16, 16, 2)])
+def test_fused_pipeline_matches_oracle_pipeline(backend, oracle, B, H, W, radius):
+    """On synthetic pairs (full size, ragged tiles, radius 0 = no refine): the fused op equals
+    the oracle's whole pipeline (its C restatement of the glue, pinned to the reference's glue
+    by test_glue_golden.py, plus the oracle kernels), identity and warm start."""
+    import m3s.matching as mm
+    from m3s.config import config as cfg0
+
+    mp = synth.make_match_pair(B=B, H=H, W=W, seed=5 + H)
+    c = dict(cfg0["matching"], radius=radius)
+    for init in (None, mp.idx_init):
+        idx, valid = mm.match_iterative_proj(mp.X11.cuda(), mp.X21.cuda(), mp.D11.cuda(), mp.D21.cuda(),
+                                             None if init is None else init.cuda(), cfg={"matching": c})
+        idx_o, valid_o = oracle.match_iterative_proj(
+            mp.X11.numpy(), mp.X21.numpy(), mp.D11.numpy(), mp.D21.numpy(),
+            None if init is None else init.numpy(), c["max_iter"], c["lambda_init"],
+            c["convergence_thresh"], c["dist_thresh"], c["radius"], c["dilation_max"])
+        assert np.array_equal(idx.cpu().numpy(), idx_o), (idx.cpu().numpy() != idx_o).sum()
+        assert np.array_equal(valid.cpu().numpy(), valid_o)
