@@ -258,6 +258,21 @@ def matching_bench(dev, reps=10):
             if r >= 2:
                 t_gather += ev[1].elapsed_time(ev[2]) / reps
         del os.environ["M3S_REFINE_LDS"]
+        # A/B: the MFMA correlation path (M3S_REFINE_MFMA=1, opt-in): approximate scores on
+        # v_mfma_f32_16x16x32_f16 + exact re-scoring of the candidates within the error bound
+        os.environ["M3S_REFINE_MFMA"] = "1"
+        t_mfma = 0.0
+        for r in range(reps + 2):
+            ev[1].record()
+            mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r >= 2:
+                t_mfma += ev[1].elapsed_time(ev[2]) / reps
+        mb.refine_mfma_stats(True)
+        mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
+        resc, cand = mb.refine_mfma_stats(False)
+        del os.environ["M3S_REFINE_MFMA"]
         def wall_ms(fused):
             for _ in range(2):
                 match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=fused)
@@ -277,6 +292,16 @@ def matching_bench(dev, reps=10):
             "iter_proj_ms": t_ip,
             "refine_ms": t_rf,
             "refine_lds_tile_kernel_ms": t_gather,
+            "refine_mfma": {
+                "ms": t_mfma,
+                "rescored_fraction": resc / max(cand, 1),
+                # one 16x16x32 f16 MFMA per 16 (pixel, candidate) pairs (the diagonal), 245 pairs
+                # per pixel; useful = the 245 x 24 MACs of the reference's correlation
+                "mfma_issued_TFLOPs": 245 * 16384 / 16 * npx / (t_mfma * 1e-3) / 1e12,
+                "useful_TFLOPs": 245 * 48 * npx / (t_mfma * 1e-3) / 1e12,
+                "mfma_util_vs_2500TF": 245 * 16384 / 16 * npx / (t_mfma * 1e-3) / 2.5e15,
+                "useful_util_vs_2500TF": 245 * 48 * npx / (t_mfma * 1e-3) / 2.5e15,
+            },
             "match_iterative_proj_ms": t_glue,
             "match_iterative_proj_torch_glue_ms": t_torch_glue,
             "iter_proj_GBps": 65 * npx / (t_ip * 1e-3) / 1e9,

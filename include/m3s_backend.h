@@ -88,6 +88,13 @@ int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D1
                              int radius, int dilation_max, int64_t* idx_out, uint8_t* valid_out,
                              void* ws, size_t ws_bytes, void* stream);
 
+/*
+ * Diagnostics of the MFMA refine path (env M3S_REFINE_MFMA=1): out2 = {candidates re-scored
+ * exactly, in-image candidates} accumulated since the previous call; enable != 0 turns the
+ * counting on for later calls (it synchronises the stream after each refine), 0 off.
+ */
+void m3s_refine_mfma_stats(int enable, unsigned long long* out2);
+
 /* ---------------- Gauss-Newton ---------------- */
 
 enum { M3S_GN_POINTS = 0, M3S_GN_RAYS = 1, M3S_GN_CALIB = 2 };

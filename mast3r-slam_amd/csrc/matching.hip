@@ -14,6 +14,7 @@
 // so the bilinear / window gathers of a wave hit the same L1/L2 lines.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 #include <cstdlib>
@@ -323,6 +324,190 @@ __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// refine_matches with the correlation on MFMA (opt-in M3S_REFINE_MFMA=1; SURVEY §8(d) prices the
+// correlation against the fp16 matrix peak).  Exact by construction:
+//
+//  1. approximate scores: per dilation level, candidate c (of 49) of 16 pixels at once as one
+//     v_mfma_f32_16x16x32_f16: A = the 16 pixels' descriptors (K = 24, zero-padded to 32), B = the
+//     16 pixels' candidate-c descriptors, gathered (out-of-image / padding lanes: zeros); the
+//     16 wanted dot products are the diagonal of the 16x16 product (fp16 products are exact in
+//     fp32, the sum rounds in fp32).  The windows of neighbouring pixels are on different
+//     dilation lattices, so no candidate row is shared by two pixels -- the MFMA does 16x the
+//     needed MACs and the gathers are the same as the VALU kernel's.
+//  2. bound: |s_half - s_mfma| <= E = 0.0126 * ||q|| * Hmax + 4e-6, where s_half is the
+//     c10::Half score (24 roundings of products, 24 of the running sum, each <= 2^-11 relative
+//     via fp32: 25 * (2^-11 + 2^-23) * 1.015 < 0.0126 of sum |q_k h_k| <= ||q|| ||h||, plus the
+//     fp16 subnormal half-spacing 2^-25 per rounding and the MFMA's own fp32 error), Hmax = the
+//     largest ||h|| in the image (refine_hmax_kernel).  Non-finite or huge bounds: every
+//     candidate is re-scored.
+//  3. exact re-scoring: with L = max (s_mfma - E) over the pixel's in-image candidates, only
+//     candidates with s_mfma + E >= L (every possible argmax, ties included) and s_mfma + E >
+//     max_score (so it could pass the strict '>') get the exact fp16 chain, in the reference's
+//     candidate order -> the same winner and the same persisted max_score as scoring all 49.
+// ---------------------------------------------------------------------------------
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+constexpr float kRefineBoundRel = 0.0126f;
+constexpr float kRefineBoundAbs = 4e-6f;
+constexpr float kRefineBoundMax = 3.0e4f;  // sum |q h| beyond: fp16 overflow possible, score all
+
+// per image: max over pixels of sum_k h_k^2 (float bits; +inf if any value is not finite)
+__global__ __launch_bounds__(kBlock) void refine_hmax_kernel(const uint16_t* __restrict__ D11, int64_t HW,
+                                                             unsigned* __restrict__ hmax2) {
+    const int64_t b = blockIdx.y;
+    float m = 0.0f;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < HW; p += (int64_t)gridDim.x * kBlock) {
+        const uint4* src = reinterpret_cast<const uint4*>(D11 + (b * HW + p) * 24);
+        float s = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            uint4 w = src[c];
+            const half_t* h = reinterpret_cast<const half_t*>(&w);
+#pragma unroll
+            for (int k = 0; k < 8; k++) s = fmaf((float)h[k], (float)h[k], s);
+        }
+        m = (s == s && s <= 3.0e38f) ? fmaxf(m, s) : __int_as_float(0x7f800000);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(hmax2 + b, __float_as_uint(m));
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void refine_mfma_kernel(
+    const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21, const int64_t* __restrict__ p1,
+    int64_t* __restrict__ p1_new, int64_t* __restrict__ lin, int H, int W, int64_t N, int64_t B, TileMap tm,
+    int dilation_max, const unsigned* __restrict__ hmax2, unsigned long long* __restrict__ stats) {
+    constexpr int F = 24;
+    constexpr int S = 2 * R + 1;
+    constexpr int NC = S * S;
+    static_assert(NC <= 64, "candidate mask is 64 bits");
+    __shared__ float sc[kBlock / 64][NC][64];  // approximate scores, per wave: [candidate][pixel]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t g = 0;
+    const bool active = tile_pixel(tm, B, W, H, g);  // every lane stays for the MFMAs
+    const int64_t b = active ? g / N : 0;
+    const uint16_t* __restrict__ img = D11 + b * (int64_t)H * W * F;
+
+    half2_t q2[F / 2];
+    float qn2 = 0.0f;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(D21 + (active ? g : 0) * F);
+#pragma unroll
+        for (int c = 0; c < F / 8; c++) {
+            uint4 w = src[c];
+            const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                q2[c * 4 + k] = hp[k];
+                qn2 = fmaf((float)hp[k].x, (float)hp[k].x, fmaf((float)hp[k].y, (float)hp[k].y, qn2));
+            }
+        }
+    }
+    // A fragments of the wave's 4 row groups: lane l holds pixel (16 r + (l & 15))'s descriptor
+    // elements 8 (l >> 4) .. + 7 (zeros for the K padding 24..31)
+    const int kc = lane >> 4, col = lane & 15;
+    half8_t A[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int64_t gp = __shfl(g, 16 * r + col, 64);
+        const bool ap = __shfl((int)active, 16 * r + col, 64) != 0;
+        uint4 w = make_uint4(0, 0, 0, 0);
+        if (kc < 3 && ap) w = reinterpret_cast<const uint4*>(D21 + gp * F)[kc];
+        A[r] = __builtin_bit_cast(half8_t, w);
+    }
+    // the diagonal of a 16x16 tile: lane l holds C[4 (l >> 4) + q][l & 15]; it is (col, col)
+    // for the 16 lanes with (col >> 2) == kc, at q = col & 3
+    const bool diag = (col >> 2) == kc;
+    const int dq = col & 3;
+    const float hmax = sqrtf(__uint_as_float(hmax2[b])) * 1.00001f;
+    const float pbound = (sqrtf(qn2) * 1.00001f) * hmax;  // >= sum_k |q_k h_k| for every candidate
+    const float E = kRefineBoundRel * pbound + kRefineBoundAbs;
+    const bool score_all = !(pbound <= kRefineBoundMax);  // NaN / inf / fp16 overflow possible
+
+    int64_t u0 = active ? p1[g * 2 + 0] : 0;
+    int64_t v0 = active ? p1[g * 2 + 1] : 0;
+    half_t max_score = (half_t)kRefineHalfMaxInit;
+    int64_t u_new = u0, v_new = v0;
+    unsigned nresc = 0, ntotal = 0;
+    for (int d = dilation_max; d > 0; d--) {
+        const int64_t rd = (int64_t)R * d;
+        // 1. approximate scores of the 4 row groups' candidates
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int64_t uc = __shfl(u0, 16 * r + col, 64), vc = __shfl(v0, 16 * r + col, 64);
+#pragma unroll
+            for (int i = 0; i < S; i++) {
+                const int64_t u = uc - rd + (int64_t)i * d;
+#pragma unroll
+                for (int j = 0; j < S; j++) {
+                    const int64_t v = vc - rd + (int64_t)j * d;
+                    uint4 w = make_uint4(0, 0, 0, 0);
+                    if (kc < 3 && inside_image(u, v, W, H))
+                        w = reinterpret_cast<const uint4*>(img + (v * W + u) * F)[kc];
+                    float4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[r], __builtin_bit_cast(half8_t, w), acc, 0, 0, 0);
+                    const float dv = dq == 0 ? acc[0] : dq == 1 ? acc[1] : dq == 2 ? acc[2] : acc[3];
+                    if (diag) sc[wave][i * S + j][16 * r + col] = dv;
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's score writes landed
+        __builtin_amdgcn_wave_barrier();
+        // 2. shortlist: every candidate that can be the level's first argmax and beat max_score
+        uint64_t mask = 0;
+        float lo = -__int_as_float(0x7f800000);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int64_t u = u0 - rd + (int64_t)(c / S) * d, v = v0 - rd + (int64_t)(c % S) * d;
+            if (inside_image(u, v, W, H)) lo = fmaxf(lo, sc[wave][c][lane] - E);
+        }
+        const float beat = (float)max_score;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int64_t u = u0 - rd + (int64_t)(c / S) * d, v = v0 - rd + (int64_t)(c % S) * d;
+            const float hi = sc[wave][c][lane] + E;
+            const bool in = inside_image(u, v, W, H);
+            ntotal += in;
+            if (in && (score_all || (hi >= lo && hi > beat))) mask |= 1ull << c;
+        }
+        if (!active) mask = 0;
+        nresc += __builtin_popcountll(mask);
+        // 3. exact c10::Half scores of the shortlist, in candidate order
+        while (mask) {
+            const int c = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const int64_t u = u0 - rd + (int64_t)(c / S) * d, v = v0 - rd + (int64_t)(c % S) * d;
+            uint4 row[F / 8];
+            const uint4* src = reinterpret_cast<const uint4*>(img + (v * W + u) * F);
+#pragma unroll
+            for (int k = 0; k < F / 8; k++) row[k] = src[k];
+            const half_t score = score_f16<F>(q2, row);
+            if (score > max_score) {
+                max_score = score;
+                u_new = u;
+                v_new = v;
+            }
+        }
+        u0 = u_new;
+        v0 = v_new;
+        __builtin_amdgcn_wave_barrier();  // the next level overwrites this wave's scores
+    }
+    if (active) store_match(p1_new, lin, g, W, u_new, v_new);
+    if (stats) {  // diagnostics: candidates re-scored exactly / in-image candidates
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            nresc += __shfl_xor(nresc, off, 64);
+            ntotal += __shfl_xor(ntotal, off, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(stats, (unsigned long long)nresc);
+            atomicAdd(stats + 1, (unsigned long long)ntotal);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // refine_matches, LDS-tiled (F = 24 fp16, radius 3): opt-in (M3S_REFINE_LDS=1), measured slower.
 //
 // The gather kernel above reads every candidate row (48 B) through the vector L1 / texture path:
@@ -621,6 +806,19 @@ static int refine_checks(const void* D11, const void* D21, const void* p1, void*
     return M3S_OK;
 }
 
+// M3S_REFINE_MFMA diagnostics (m3s_refine_mfma_stats): exactly re-scored / in-image candidates
+static bool g_refine_stats_enabled = false;
+static unsigned long long g_refine_stats[2] = {0, 0};
+
+extern "C" void m3s_refine_mfma_stats(int enable, unsigned long long* out2) {
+    if (out2) {
+        out2[0] = g_refine_stats[0];
+        out2[1] = g_refine_stats[1];
+    }
+    g_refine_stats_enabled = enable != 0;
+    g_refine_stats[0] = g_refine_stats[1] = 0;
+}
+
 namespace m3s {
 // refine_matches on fp16 descriptors; lin != nullptr writes u + W v per pixel instead of (u, v)
 int refine_f16_launch(const uint16_t* D11, const uint16_t* D21, const int64_t* p1, int64_t* p1_new,
@@ -634,7 +832,38 @@ int refine_f16_launch(const uint16_t* D11, const uint16_t* D21, const int64_t* p
     // M3S_REFINE_LDS=1 selects the LDS-tiled kernel (A/B; slower on the bench data, see above)
     const char* lds_env = getenv("M3S_REFINE_LDS");
     const bool lds_ok = lds_env && atoi(lds_env) != 0;
-    if (F == 24 && aligned && N == H * W && radius == 3 && lds_ok) {
+    const char* mf_env = getenv("M3S_REFINE_MFMA");
+    const bool mfma_ok = mf_env && atoi(mf_env) != 0;
+    if (F == 24 && aligned && N == H * W && radius == 3 && mfma_ok) {
+        TileMap tm;
+        tm.tiles_x = (int)((W + kTile - 1) / kTile);
+        tm.tiles_y = (int)((H + kTile - 1) / kTile);
+        tm.ntiles = tm.tiles_x * tm.tiles_y;
+        const int64_t nblk = (int64_t)tm.ntiles * B;
+        const int64_t grid = (nblk + 7) / 8 * 8;
+        // per-image max ||h||^2 (+ the optional re-score counters), stream-ordered scratch
+        unsigned* scratch = nullptr;
+        const size_t sbytes = sizeof(unsigned) * (size_t)B + 2 * sizeof(unsigned long long) + 16;
+        M3S_HIP_CHECK(hipMallocAsync((void**)&scratch, sbytes, st));
+        M3S_HIP_CHECK(hipMemsetAsync(scratch, 0, sbytes, st));
+        unsigned long long* stats = reinterpret_cast<unsigned long long*>(
+            reinterpret_cast<char*>(scratch) + ((sizeof(unsigned) * (size_t)B + 15) / 16 * 16));
+        const int64_t HW = H * W;
+        const unsigned hb = (unsigned)std::min<int64_t>((HW + kBlock - 1) / kBlock, 1024);
+        hipLaunchKernelGGL(refine_hmax_kernel, dim3(hb, (unsigned)B), dim3(kBlock), 0, st, D11, HW, scratch);
+        hipLaunchKernelGGL((refine_mfma_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
+                           p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, scratch,
+                           g_refine_stats_enabled ? stats : nullptr);
+        M3S_LAUNCH_CHECK();
+        if (g_refine_stats_enabled) {
+            unsigned long long h[2];
+            M3S_HIP_CHECK(hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st));
+            M3S_HIP_CHECK(hipStreamSynchronize(st));
+            g_refine_stats[0] += h[0];
+            g_refine_stats[1] += h[1];
+        }
+        M3S_HIP_CHECK(hipFreeAsync(scratch, st));
+    } else if (F == 24 && aligned && N == H * W && radius == 3 && lds_ok) {
         LdsTileMap tm;
         tm.tiles_x = (int)((W + kLdsTx - 1) / kLdsTx);
         tm.tiles_y = (int)((H + kLdsTy - 1) / kLdsTy);

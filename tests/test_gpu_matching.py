@@ -216,3 +216,45 @@ def test_fused_pipeline_matches_oracle_pipeline(backend, oracle, B, H, W, radius
             c["convergence_thresh"], c["dist_thresh"], c["radius"], c["dilation_max"])
         assert np.array_equal(idx.cpu().numpy(), idx_o), (idx.cpu().numpy() != idx_o).sum()
         assert np.array_equal(valid.cpu().numpy(), valid_o)
+
+
+@pytest.mark.parametrize("warm", [False, True])
+def test_refine_mfma_path_bit_exact(backend, oracle, monkeypatch, warm):
+    """The MFMA correlation path (M3S_REFINE_MFMA=1: approximate scores on
+    v_mfma_f32_16x16x32_f16, exact c10::Half re-scoring of every candidate within the error
+    bound of the best) gives the oracle's indices bit for bit at 512x384, and re-scores only a
+    fraction of the candidates."""
+    mp = synth.make_match_pair(B=1, H=384, W=512, seed=21)
+    rays, pts, p_init = prep_for_iter_proj(mp.X11, mp.X21, mp.idx_init if warm else None)
+    p, _ = oracle.iter_proj(rays.numpy(), pts.numpy(), p_init.numpy(), 10, 1e-8, 1e-6)
+    p1 = torch.from_numpy(p).long()
+    D11 = mp.D11.half()
+    D21 = mp.D21.view(1, -1, 24).half()
+    monkeypatch.setenv("M3S_REFINE_MFMA", "1")
+    backend.refine_mfma_stats(True)
+    out_g, out_o = _refine_both(backend, oracle, D11, D21, p1, 3, 5)
+    resc, total = backend.refine_mfma_stats(False)
+    assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
+    assert 0 < resc < total, (resc, total)
+
+
+def test_refine_mfma_path_edge_cases(backend, oracle, monkeypatch):
+    """Ties everywhere, all-negative scores, out-of-image starts, huge values (bound beyond fp16
+    range: every candidate re-scored) and NaN descriptors, all bit-exact on the MFMA path."""
+    monkeypatch.setenv("M3S_REFINE_MFMA", "1")
+    g = torch.Generator().manual_seed(4)
+    B, H, W, F = 1, 40, 36, 24
+    p1 = torch.stack((torch.randint(-5, W + 5, (B, H * W), generator=g),
+                      torch.randint(-5, H + 5, (B, H * W), generator=g)), -1)
+    cases = {
+        "ties": (torch.full((B, H, W, F), 0.25), torch.full((B, H * W, F), 0.25)),
+        "negative": (torch.full((B, H, W, F), 0.25), torch.full((B, H * W, F), -0.25)),
+        "random": (torch.randn((B, H, W, F), generator=g), torch.randn((B, H * W, F), generator=g)),
+        "huge": (torch.randn((B, H, W, F), generator=g) * 200, torch.randn((B, H * W, F), generator=g) * 200),
+    }
+    nan11 = torch.randn((B, H, W, F), generator=g)
+    nan11[0, 7, 9, 3] = float("nan")
+    cases["nan"] = (nan11, torch.randn((B, H * W, F), generator=g))
+    for name, (D11, D21) in cases.items():
+        out_g, out_o = _refine_both(backend, oracle, D11.half(), D21.half(), p1, 3, 5)
+        assert np.array_equal(out_g, out_o), name
