@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 
 #include "gn_kernels.h"
@@ -530,6 +531,126 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
     dst[1] = int4{code[2], sqb[2], code[3], sqb[3]};
 }
 
+// ---------------------------------------------------------------------------
+// Compacted packed stream (opt-in M3S_GN_COMPACT=1; default: the positional one above).  A point
+// whose pose-independent validity fails (match, q, ci, cj) contributes w = 0 every iteration,
+// and 0 * (finite Jacobian / residual) = 0 exactly: such a point is "dead" when its own point
+// and the matched point it gathers are finite (the reference's NaN poisoning through an invalid
+// point needs a non-finite input, and those points are kept).  Per (edge, chunk) the live points
+// are written contiguously, in point order (a fixed-order workgroup scan: deterministic), as
+// the 8-B record {code, sqrt q} plus a copy of Xj (12 B, iteration-invariant), padded to a
+// multiple of 4 with copies of a dead point (exact zeros); the count goes to pcnt.  Every
+// iteration then runs the point math only on live points, reading contiguous streams.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool finite3(const float* p) {
+    return isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
+    const float* __restrict__ Xs, const float* __restrict__ Cs, const int* __restrict__ ii_loc,
+    const int* __restrict__ jj_loc, EdgeSrc es, AccParams P, int2* __restrict__ pk, float* __restrict__ px,
+    int* __restrict__ pcnt, const int* __restrict__ flags) {
+    __shared__ int s_wsum[kAccThreads / 64];
+    __shared__ int s_dead;
+    if (flags[kFlagDone]) return;
+    const int e = blockIdx.y, c = blockIdx.x;
+    const int HW = P.HW;
+    const int k0 = c * P.chunk, k1 = min(k0 + P.chunk, HW);
+    const int64_t obase = ((int64_t)e * P.nchunks + c) * P.chunk;
+    const int64_t* idx_e;
+    const uint8_t* valid_e;
+    const float* Q_e;
+    es.at(e, HW, idx_e, valid_e, Q_e);
+    const int ix = ii_loc[e], jx = jj_loc[e];
+    const float* __restrict__ Ci_b = Cs + (int64_t)ix * HW;
+    const float* __restrict__ Cj_b = Cs + (int64_t)jx * HW;
+    const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
+    const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_dead = INT_MAX;
+    __syncthreads();
+    int running = 0;
+    for (int base = k0; base < k1; base += 4 * kAccThreads) {
+        const int k = base + 4 * tid;
+        int code[4], sqb[4];
+        bool live[4] = {false, false, false, false};
+        float xj[12];
+        if (k < k1) {
+            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid_e + k);
+            const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx_e + k);
+            const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx_e + k + 2);
+            const float4 q4 = *reinterpret_cast<const float4*>(Q_e + k);
+            const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
+            const float4 xa = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
+            const float4 xb = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
+            const float4 xc = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
+            const float t[12] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w, xc.x, xc.y, xc.z, xc.w};
+#pragma unroll
+            for (int q = 0; q < 12; q++) xj[q] = t[q];
+            const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
+            const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
+            const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
+            const float cjs[4] = {cj4.x, cj4.y, cj4.z, cj4.w};
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int ind = match_index(ids[s], vm[s], HW);
+                const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (cjs[s] > P.C_thresh);
+                code[s] = ok ? ind : (int)((unsigned)ind | 0x80000000u);
+                sqb[s] = __float_as_int(vsqrt(qs[s]));
+                const float* xi = Xi_b + (int64_t)ind * 3;
+                const bool fin = finite3(&xj[3 * s]) &&
+                                 (MODE == GN_CALIB ? (bool)isfinite(xi[2]) : finite3(xi));
+                live[s] = ok || !fin;
+                if (!live[s]) atomicMin(&s_dead, k + s);
+            }
+        }
+        const int n = (int)live[0] + (int)live[1] + (int)live[2] + (int)live[3];
+        // exclusive scan of n over the workgroup in thread order
+        int incl = n;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        int wbase = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kAccThreads / 64; w++) {
+            wbase += w < wave ? s_wsum[w] : 0;
+            total += s_wsum[w];
+        }
+        int pos = running + wbase + incl - n;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            if (live[s]) {
+                pk[obase + pos] = make_int2(code[s], sqb[s]);
+                float* o = px + (obase + pos) * 3;
+                o[0] = xj[3 * s];
+                o[1] = xj[3 * s + 1];
+                o[2] = xj[3 * s + 2];
+                pos++;
+            }
+        }
+        running += total;
+        __syncthreads();  // s_wsum is reused by the next step
+    }
+    // pad to a multiple of 4 with copies of the first dead point (its contribution is exactly 0)
+    const int pad = (4 - (running & 3)) & 3;
+    if (tid < pad) {
+        const int kd = s_dead;  // pad > 0 implies a dead point exists (chunks are multiples of 4)
+        const int64_t id = idx_e[kd];
+        const int ind = match_index(id, valid_e[kd] != 0, HW);
+        pk[obase + running + tid] = make_int2((int)((unsigned)ind | 0x80000000u), __float_as_int(vsqrt(Q_e[kd])));
+        float* o = px + (obase + running + tid) * 3;
+        o[0] = Xj_b[(int64_t)kd * 3];
+        o[1] = Xj_b[(int64_t)kd * 3 + 1];
+        o[2] = Xj_b[(int64_t)kd * 3 + 2];
+    }
+    if (tid == 0) pcnt[(int64_t)e * P.nchunks + c] = running + pad;
+}
+
 // Zs[n, k] = Xs[n, k, 2]: the only coordinate of the matched point calib mode reads, as a
 // dense 4-B array so the per-iteration gather touches 4 B per point instead of a 12-B stride.
 // Also the ray tables tu[u] = (u - cx) / fx, tv[v] = (v - cy) / fy (after Zs), and a check that
@@ -608,13 +729,13 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
 #ifndef M3S_ACC_WAVES
 #define M3S_ACC_WAVES 1
 #endif
-template <int MODE>
+template <int MODE, bool COMPACT>
 __global__ __launch_bounds__(kAccThreads) __attribute__((amdgpu_waves_per_eu(M3S_ACC_WAVES)))
 void gn_accum_packed_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Zs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int4* __restrict__ pack,
     AccParams P, const int4* __restrict__ sched, float* __restrict__ partials,
-    const int* __restrict__ flags) {
+    const int* __restrict__ flags, const float* __restrict__ px, const int* __restrict__ pcnt) {
     const int4 tk = sched[blockIdx.x];  // {edge, chunk, ix, jx}, loaded together with the flag
     if (flags[kFlagDone]) return;
     const int e = tk.x, c = tk.y, ix = tk.z, jx = tk.w;
@@ -665,8 +786,13 @@ void gn_accum_packed_kernel(
         nxt.kb = pb2;
     }
 #else
-    // calib with ray-constrained keyframe points (gn_depth_kernel's check): Xj from its depth
-    if (MODE == GN_CALIB && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
+    if constexpr (COMPACT) {
+        // compacted stream: the chunk's live points, Xj copied alongside the records
+        const int64_t cb = ((int64_t)e * P.nchunks + c) * P.chunk;
+        accum_steps<MODE, false>(px + cb * 3, Xi_b, Zi_b, pack + cb / 2, 0, pcnt[(int64_t)e * P.nchunks + c], T, P,
+                                 Zs, acc);
+    } else if (MODE == GN_CALIB && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
+        // calib with ray-constrained keyframe points (gn_depth_kernel's check): Xj from its depth
         accum_steps<MODE, true>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
     else
         accum_steps<MODE, false>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
@@ -692,10 +818,22 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
     return hipGetLastError();
 }
 
-hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
+hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
                        const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P,
-                       int4* pack, float* Zs, const int* flags) {
-    if (E_local > 0) {
+                       int4* pack, float* px, int* pcnt, float* Zs, const int* flags) {
+    if (E_local > 0 && px) {
+        const dim3 grid((unsigned)P.nchunks, (unsigned)E_local);
+        int2* pk = reinterpret_cast<int2*>(pack);
+        if (mode == GN_RAYS)
+            hipLaunchKernelGGL(gn_pack_compact_kernel<GN_RAYS>, grid, dim3(kAccThreads), 0, st, Xs, Cs, ii_loc,
+                               jj_loc, es, P, pk, px, pcnt, flags);
+        else if (mode == GN_CALIB)
+            hipLaunchKernelGGL(gn_pack_compact_kernel<GN_CALIB>, grid, dim3(kAccThreads), 0, st, Xs, Cs, ii_loc,
+                               jj_loc, es, P, pk, px, pcnt, flags);
+        else
+            hipLaunchKernelGGL(gn_pack_compact_kernel<GN_POINTS>, grid, dim3(kAccThreads), 0, st, Xs, Cs, ii_loc,
+                               jj_loc, es, P, pk, px, pcnt, flags);
+    } else if (E_local > 0) {
         const dim3 grid((unsigned)((P.HW / 4 + kAccThreads - 1) / kAccThreads), (unsigned)E_local);
         hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, es,
                            P, pack, flags);
@@ -714,16 +852,20 @@ hipError_t launch_pack(hipStream_t st, int E_local, const float* Xs, int64_t N, 
 hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,
-                               const int4* sched, float* partials, const int* flags) {
-    if (mode == GN_RAYS)
-        hipLaunchKernelGGL(gn_accum_packed_kernel<GN_RAYS>, grid, dim3(kAccThreads), 0, st, Twc, Xs,
-                           Zs, ii_loc, jj_loc, pack, P, sched, partials, flags);
-    else if (mode == GN_CALIB)
-        hipLaunchKernelGGL(gn_accum_packed_kernel<GN_CALIB>, grid, dim3(kAccThreads), 0, st, Twc, Xs,
-                           Zs, ii_loc, jj_loc, pack, P, sched, partials, flags);
-    else
-        hipLaunchKernelGGL(gn_accum_packed_kernel<GN_POINTS>, grid, dim3(kAccThreads), 0, st, Twc, Xs,
-                           Zs, ii_loc, jj_loc, pack, P, sched, partials, flags);
+                               const int4* sched, float* partials, const int* flags, const float* px,
+                               const int* pcnt) {
+#define M3S_ACCP(MODE, CP)                                                                       \
+    hipLaunchKernelGGL((gn_accum_packed_kernel<MODE, CP>), grid, dim3(kAccThreads), 0, st, Twc, Xs, Zs, \
+                       ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt)
+    const bool cp = px != nullptr;
+    if (mode == GN_RAYS) {
+        if (cp) M3S_ACCP(GN_RAYS, true); else M3S_ACCP(GN_RAYS, false);
+    } else if (mode == GN_CALIB) {
+        if (cp) M3S_ACCP(GN_CALIB, true); else M3S_ACCP(GN_CALIB, false);
+    } else {
+        if (cp) M3S_ACCP(GN_POINTS, true); else M3S_ACCP(GN_POINTS, false);
+    }
+#undef M3S_ACCP
     return hipGetLastError();
 }
 

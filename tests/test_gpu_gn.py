@@ -241,8 +241,47 @@ def test_packed_stream_gives_identical_system(backend, monkeypatch, mode):
     monkeypatch.setenv("M3S_GN_PACK", "0")
     H0, b0 = build_system_gpu(g, mode, LOCAL)
     monkeypatch.setenv("M3S_GN_PACK", "2")
+    monkeypatch.setenv("M3S_GN_COMPACT", "0")  # the positional stream: same points, same order
     H2, b2 = build_system_gpu(g, mode, LOCAL)
     assert np.array_equal(H0, H2) and np.array_equal(b0, b2)
+    # the compacted stream (M3S_GN_COMPACT=1): dead points dropped, so only the summation
+    # grouping moves
+    monkeypatch.setenv("M3S_GN_COMPACT", "1")
+    H3, b3 = build_system_gpu(g, mode, LOCAL)
+    assert np.abs(H3 - H0).max() <= 1e-6 * np.abs(H0).max()
+    assert np.abs(b3 - b0).max() <= 1e-6 * np.abs(b0).max()
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib", "points"])
+def test_compacted_stream_keeps_nan_poisoning_and_empty_edges(backend, oracle, monkeypatch, mode):
+    """Dead-point compaction (gn_pack_compact_kernel) drops a point only when its validity fails
+    AND its own and its matched point are finite (then its contribution is exactly 0): a NaN
+    in an invalid point must still poison the system as in the reference; an edge with no live
+    point contributes nothing; and the iterated result equals the positional stream's to
+    rounding and the oracle to 1e-5."""
+    from m3s.debug import build_system_gpu
+
+    monkeypatch.setenv("M3S_GN_PACK", "2")
+    monkeypatch.setenv("M3S_GN_COMPACT", "1")
+    g = _graph(mode, N=5, E=6)
+    g.valid[2, :] = False        # one directed edge with no live point at all
+    T_c, _ = _run_gpu(backend, g, mode, 3)
+    monkeypatch.setenv("M3S_GN_COMPACT", "0")
+    T_p, _ = _run_gpu(backend, g, mode, 3)
+    monkeypatch.setenv("M3S_GN_COMPACT", "1")
+    T_o, _, _ = _run_oracle(oracle, g, mode, 3)
+    assert np.isfinite(T_c).all()
+    assert _rel(T_c, T_p) < 1e-6 and _rel(T_c, T_o) < 1e-5
+    # an invalid point with a NaN coordinate, read by no valid point: kept, and it poisons like
+    # the reference's 0 * NaN
+    j = int(g.jj[3])
+    g.valid[g.jj == j, 5] = False                          # every edge that reads it as Xj
+    g.valid[(g.ii == j)[:, None] & (g.idx == 5)] = False   # no valid point gathers it as Xi
+    g.Xs[j, 5, 0] = float("nan")
+    H, b = build_system_gpu(g, mode, LOCAL)
+    monkeypatch.setenv("M3S_GN_COMPACT", "0")
+    H_p, b_p = build_system_gpu(g, mode, LOCAL)
+    assert np.isnan(H).any() and np.array_equal(np.isnan(H), np.isnan(H_p))
 
 
 def test_full_size_cfg3_calib_within_1e5_of_exactly_summed_system(backend, oracle):
