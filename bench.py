@@ -273,6 +273,20 @@ def matching_bench(dev, reps=10):
         mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
         resc, cand = mb.refine_mfma_stats(False)
         del os.environ["M3S_REFINE_MFMA"]
+        # A/B: bound-and-rescore with dot2 approximations (M3S_REFINE_DOT2=1, opt-in)
+        os.environ["M3S_REFINE_DOT2"] = "1"
+        mb.refine_mfma_stats(True)
+        mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
+        resc_d, cand_d = mb.refine_mfma_stats(False)
+        t_exact = 0.0
+        for r in range(reps + 2):
+            ev[1].record()
+            mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r >= 2:
+                t_exact += ev[1].elapsed_time(ev[2]) / reps
+        del os.environ["M3S_REFINE_DOT2"]
         def wall_ms(fused):
             for _ in range(2):
                 match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=fused)
@@ -291,6 +305,7 @@ def matching_bench(dev, reps=10):
             "pairs_per_s_glue": B / (t_glue * 1e-3),
             "iter_proj_ms": t_ip,
             "refine_ms": t_rf,
+            "refine_dot2_rescore": {"ms": t_exact, "rescored_fraction": resc_d / max(cand_d, 1)},
             "refine_lds_tile_kernel_ms": t_gather,
             "refine_mfma": {
                 "ms": t_mfma,

@@ -151,6 +151,8 @@ struct Layout {
     int nchunks, npad, nblk_max;
 };
 
+int env_int(const char* name, int dflt);
+
 Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_local) {
     Layout L{};
     const int64_t npose = std::max<int64_t>(N - 1, 0);
@@ -185,11 +187,15 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.sched = take(sizeof(int) * 4 * (size_t)E_local * L.nchunks);  // {edge, chunk, ix, jx} per task
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
-    {   // compacted stream capacity: every (edge, chunk) region holds a whole chunk
+    if (env_int("M3S_GN_COMPACT", 0) != 0) {
+        // compacted stream (opt-in): every (edge, chunk) region holds a whole chunk
         const size_t cap = (size_t)E_local * (size_t)L.nchunks * (size_t)chunk_points(HW, L.nchunks);
         L.pack = take(8 * std::max(cap, (size_t)E_local * (size_t)HW));
         L.packx = take(12 * cap);
         L.pcnt = take(sizeof(int) * (size_t)E_local * L.nchunks);
+    } else {
+        L.pack = take(8 * (size_t)E_local * (size_t)HW);
+        L.packx = L.pcnt = L.pack;  // unused
     }
     // + the ray tables tu[W], tv[H] (gn_depth_kernel); HW floats is an upper bound for W + H
     L.zs = take(mode == M3S_GN_CALIB ? sizeof(float) * ((size_t)N + 1) * (size_t)HW + 64 : 0);

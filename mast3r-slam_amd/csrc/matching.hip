@@ -508,6 +508,152 @@ __global__ __launch_bounds__(kBlock) void refine_mfma_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// refine_matches, bound-and-rescore on the VALU (opt-in M3S_REFINE_DOT2=1).  The same
+// exactness argument as refine_mfma_kernel, with the approximate scores from v_dot2c_f32_f16
+// (12 per candidate: fp16 products exact in fp32, fp32 sums) instead of 48 half-precision ops:
+//   1. per window column, the 7 candidates' rows are loaded together (as refine_f16_kernel) and
+//      their approximate scores computed as 7 interleaved dot2 chains; the best lower bound
+//      L = max (s - E) over the in-image candidates is tracked;
+//   2. the exact c10::Half chain runs only for candidates with s + E >= L and s + E > max_score,
+//      in the reference's candidate order -> the same winner and persisted max_score.
+// E = 0.0126 ||q|| Hmax (the fp16 chain's rounding, see refine_mfma_kernel) + 24 * 2^-14 *
+// max(||q||, Hmax) (the terms an fp16-denormal flush inside dot2 could drop: a subnormal
+// factor is < 2^-14 and the other <= the norm bound) + 4e-6.
+// ---------------------------------------------------------------------------------
+constexpr float kRefineFlushRel = 24.0f / 16384.0f;
+
+#ifndef M3S_REFINE_DOT2_WAVES
+#define M3S_REFINE_DOT2_WAVES 1
+#endif
+template <int R>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M3S_REFINE_DOT2_WAVES))) void refine_dot2_kernel(
+    const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21, const int64_t* __restrict__ p1,
+    int64_t* __restrict__ p1_new, int64_t* __restrict__ lin, int H, int W, int64_t N, int64_t B, TileMap tm,
+    int dilation_max, const unsigned* __restrict__ hmax2, unsigned long long* __restrict__ stats) {
+    constexpr int F = 24;
+    constexpr int S = 2 * R + 1;
+    constexpr int NC = S * S;
+    static_assert(NC <= 64, "candidate mask is 64 bits");
+    int64_t g;
+    unsigned nresc = 0, ntotal = 0;
+    const bool active = tile_pixel(tm, B, W, H, g);
+    if (active) {
+        const int64_t b = g / N;
+        const uint16_t* __restrict__ img = D11 + b * (int64_t)H * W * F;
+        half2_t q2[F / 2];
+        float qn2 = 0.0f;
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
+#pragma unroll
+            for (int c = 0; c < F / 8; c++) {
+                uint4 w = src[c];
+                const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    q2[c * 4 + k] = hp[k];
+                    qn2 = fmaf((float)hp[k].x, (float)hp[k].x, fmaf((float)hp[k].y, (float)hp[k].y, qn2));
+                }
+            }
+        }
+        const float hmax = sqrtf(__uint_as_float(hmax2[b])) * 1.00001f;
+        const float qn = sqrtf(qn2) * 1.00001f;
+        const float pbound = qn * hmax;
+        const float E = kRefineBoundRel * pbound + kRefineFlushRel * fmaxf(qn, hmax) + kRefineBoundAbs;
+        const bool score_all = !(pbound <= kRefineBoundMax) || !(E <= kRefineBoundMax);
+
+        int64_t u0 = p1[g * 2 + 0];
+        int64_t v0 = p1[g * 2 + 1];
+        half_t max_score = (half_t)kRefineHalfMaxInit;
+        int64_t u_new = u0, v_new = v0;
+        for (int d = dilation_max; d > 0; d--) {
+            const int64_t rd = (int64_t)R * d;
+            float sa[NC];
+            float lo = -__int_as_float(0x7f800000);
+            uint64_t inimg = 0;
+#pragma unroll
+            for (int i = 0; i < S; i++) {  // u offset outer (matching_kernels.cu:54)
+                const int64_t u = u0 - rd + (int64_t)i * d;
+                uint4 rows[S][F / 8];
+#pragma unroll
+                for (int j = 0; j < S; j++) {
+                    const int64_t v = v0 - rd + (int64_t)j * d;
+                    const bool ok = inside_image(u, v, W, H);
+                    inimg |= (uint64_t)ok << (i * S + j);
+                    const uint4* src = reinterpret_cast<const uint4*>(img + (ok ? (v * W + u) * F : 0));
+#pragma unroll
+                    for (int c = 0; c < F / 8; c++) rows[j][c] = src[c];
+                }
+                float acc[S];
+#pragma unroll
+                for (int j = 0; j < S; j++) acc[j] = 0.0f;
+#pragma unroll
+                for (int c = 0; c < F / 8; c++) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+#pragma unroll
+                        for (int j = 0; j < S; j++)
+                            acc[j] = __builtin_amdgcn_fdot2(q2[c * 4 + k],
+                                                            reinterpret_cast<const half2_t*>(&rows[j][c])[k],
+                                                            acc[j], false);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < S; j++) {
+                    sa[i * S + j] = acc[j];
+                    if ((inimg >> (i * S + j)) & 1) lo = fmaxf(lo, acc[j] - E);
+                }
+                // one window column's rows in flight at a time: pin this column's scores here (the
+                // compiler would otherwise sink all 49 dot2 chains below the level's 147 row loads,
+                // keeping every row live, and spill)
+#pragma unroll
+                for (int j = 0; j < S; j++) asm volatile("" : "+v"(sa[i * S + j]));
+                asm volatile("" : "+v"(lo));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const float beat = (float)max_score;
+            uint64_t mask = 0;
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const float hi = sa[c] + E;
+                if (score_all || (hi >= lo && hi > beat)) mask |= 1ull << c;
+            }
+            mask &= inimg;
+            nresc += __builtin_popcountll(mask);
+            ntotal += __builtin_popcountll(inimg);
+            while (mask) {  // exact c10::Half scores of the shortlist, in candidate order
+                const int c = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const int64_t u = u0 - rd + (int64_t)(c / S) * d, v = v0 - rd + (int64_t)(c % S) * d;
+                uint4 row[F / 8];
+                const uint4* src = reinterpret_cast<const uint4*>(img + (v * W + u) * F);
+#pragma unroll
+                for (int k = 0; k < F / 8; k++) row[k] = src[k];
+                const half_t score = score_f16<F>(q2, row);
+                if (score > max_score) {
+                    max_score = score;
+                    u_new = u;
+                    v_new = v;
+                }
+            }
+            u0 = u_new;
+            v0 = v_new;
+        }
+        store_match(p1_new, lin, g, W, u_new, v_new);
+    }
+    if (stats) {  // diagnostics: candidates re-scored exactly / in-image candidates
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            nresc += __shfl_xor(nresc, off, 64);
+            ntotal += __shfl_xor(ntotal, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(stats, (unsigned long long)nresc);
+            atomicAdd(stats + 1, (unsigned long long)ntotal);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // refine_matches, LDS-tiled (F = 24 fp16, radius 3): opt-in (M3S_REFINE_LDS=1), measured slower.
 //
 // The gather kernel above reads every candidate row (48 B) through the vector L1 / texture path:
@@ -806,7 +952,8 @@ static int refine_checks(const void* D11, const void* D21, const void* p1, void*
     return M3S_OK;
 }
 
-// M3S_REFINE_MFMA diagnostics (m3s_refine_mfma_stats): exactly re-scored / in-image candidates
+// bound-and-rescore diagnostics (m3s_refine_mfma_stats; the MFMA and dot2 paths): exactly
+// re-scored / in-image candidates
 static bool g_refine_stats_enabled = false;
 static unsigned long long g_refine_stats[2] = {0, 0};
 
@@ -834,7 +981,11 @@ int refine_f16_launch(const uint16_t* D11, const uint16_t* D21, const int64_t* p
     const bool lds_ok = lds_env && atoi(lds_env) != 0;
     const char* mf_env = getenv("M3S_REFINE_MFMA");
     const bool mfma_ok = mf_env && atoi(mf_env) != 0;
-    if (F == 24 && aligned && N == H * W && radius == 3 && mfma_ok) {
+    // M3S_REFINE_DOT2=1: bound-and-rescore with dot2 approximations (measured slower than
+    // scoring every candidate with the fp16 chain, the default: DESIGN.md §4)
+    const char* d2_env = getenv("M3S_REFINE_DOT2");
+    const bool dot2_ok = d2_env && atoi(d2_env) != 0;
+    if (F == 24 && aligned && N == H * W && radius == 3 && (mfma_ok || dot2_ok)) {
         TileMap tm;
         tm.tiles_x = (int)((W + kTile - 1) / kTile);
         tm.tiles_y = (int)((H + kTile - 1) / kTile);
@@ -848,12 +999,16 @@ int refine_f16_launch(const uint16_t* D11, const uint16_t* D21, const int64_t* p
         M3S_HIP_CHECK(hipMemsetAsync(scratch, 0, sbytes, st));
         unsigned long long* stats = reinterpret_cast<unsigned long long*>(
             reinterpret_cast<char*>(scratch) + ((sizeof(unsigned) * (size_t)B + 15) / 16 * 16));
+        unsigned long long* st_arg = g_refine_stats_enabled ? stats : nullptr;
         const int64_t HW = H * W;
         const unsigned hb = (unsigned)std::min<int64_t>((HW + kBlock - 1) / kBlock, 1024);
         hipLaunchKernelGGL(refine_hmax_kernel, dim3(hb, (unsigned)B), dim3(kBlock), 0, st, D11, HW, scratch);
-        hipLaunchKernelGGL((refine_mfma_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
-                           p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, scratch,
-                           g_refine_stats_enabled ? stats : nullptr);
+        if (mfma_ok)
+            hipLaunchKernelGGL((refine_mfma_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
+                               p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, scratch, st_arg);
+        else
+            hipLaunchKernelGGL((refine_dot2_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
+                               p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, scratch, st_arg);
         M3S_LAUNCH_CHECK();
         if (g_refine_stats_enabled) {
             unsigned long long h[2];

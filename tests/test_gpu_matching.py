@@ -68,8 +68,12 @@ def _refine_both(backend, oracle, D11, D21, p1, radius=3, dmax=5):
     return out_g.cpu().numpy(), out_o
 
 
+@pytest.mark.parametrize("dot2", ["0", "1"])
 @pytest.mark.parametrize("B,H,W", [(1, 384, 512), (2, 24, 32)])
-def test_refine_matches_f16_bit_exact(backend, oracle, B, H, W):
+def test_refine_matches_f16_bit_exact(backend, oracle, monkeypatch, B, H, W, dot2):
+    """Default fp16 path (every candidate's fp16 chain) and M3S_REFINE_DOT2=1 (bound-and-rescore:
+    dot2 approximations, exact fp16 chains for the shortlist): both bit-exact."""
+    monkeypatch.setenv("M3S_REFINE_DOT2", dot2)
     mp = synth.make_match_pair(B=B, H=H, W=W, seed=11)
     p1 = torch.stack((mp.idx_init % W, mp.idx_init // W), -1).long()
     D11 = mp.D11.half()
@@ -238,10 +242,12 @@ def test_refine_mfma_path_bit_exact(backend, oracle, monkeypatch, warm):
     assert 0 < resc < total, (resc, total)
 
 
-def test_refine_mfma_path_edge_cases(backend, oracle, monkeypatch):
+@pytest.mark.parametrize("path", ["M3S_REFINE_MFMA", "M3S_REFINE_DOT2"])
+def test_refine_mfma_path_edge_cases(backend, oracle, monkeypatch, path):
     """Ties everywhere, all-negative scores, out-of-image starts, huge values (bound beyond fp16
-    range: every candidate re-scored) and NaN descriptors, all bit-exact on the MFMA path."""
-    monkeypatch.setenv("M3S_REFINE_MFMA", "1")
+    range: every candidate re-scored) and NaN descriptors, all bit-exact on the MFMA and the dot2
+    bound-and-rescore paths."""
+    monkeypatch.setenv(path, "1")
     g = torch.Generator().manual_seed(4)
     B, H, W, F = 1, 40, 36, 24
     p1 = torch.stack((torch.randint(-5, W + 5, (B, H * W), generator=g),
