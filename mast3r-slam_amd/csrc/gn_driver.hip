@@ -1087,17 +1087,49 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     double* Ls = S.Lstore;
     double* W = S.W;
     double* x = S.x;
-    for (const SpRound& R : sp.rounds)
-        M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_tg), sp.iptr(sp.i_tc3), R.tbeg, R.nbt,
-                                      sp.iptr(sp.i_rtg), sp.iptr(sp.i_rc4), R.rbeg, R.nrt, A, b, Ls,
-                                      W, y, flags));
+    // M3S_SOLVE_COOP: 0 (default) = one launch per round; 1 = all rounds (+ the hybrid core's
+    // fill) in one launch with an own grid barrier and agent-coherent block accesses
+    // (gn_sparse.hip); 2 = the same as a cooperative launch with cooperative-groups grid sync.
+    // Measured (cfg3 solve per iteration): 0.24 ms per-round launches, 0.32 ms own barrier,
+    // 0.43 ms cooperative groups -- in-kernel a round's chain is ~4 us, but coherent (MALL)
+    // block traffic + write-through + the barrier cost as much as the ~5 us launch overhead saved
+    static const int coop_mode = env_int("M3S_SOLVE_COOP", 0);
+    const bool coop = coop_mode != 0;
+    if (coop) {
+        SpCoopArgs ca{};
+        ca.tg = sp.iptr(sp.i_tg);
+        ca.tc3 = sp.iptr(sp.i_tc3);
+        ca.rtg = sp.iptr(sp.i_rtg);
+        ca.rc4 = sp.iptr(sp.i_rc4);
+        ca.rounds = sp.iptr(sp.i_rounds);
+        ca.tmap = sp.iptr(sp.i_tmap);
+        ca.tail = sp.iptr(sp.i_tail);
+        ca.A = A;
+        ca.b = b;
+        ca.Lstore = Ls;
+        ca.W = W;
+        ca.y = y;
+        ca.Hd = sp.hybrid && sp.ntail > 0 ? sp.dptr<double>(sp.o_dense) : nullptr;
+        ca.flags = flags;
+        ca.nrounds = (int)sp.rounds.size();
+        ca.ntail = sp.hybrid ? sp.ntail : 0;
+        ca.npad = sp.npad_tail;
+        ca.coop = coop_mode == 2;
+        M3S_HIP_CHECK(launch_sp_rounds_coop(c.st, ca));
+    } else {
+        for (const SpRound& R : sp.rounds)
+            M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_tg), sp.iptr(sp.i_tc3), R.tbeg, R.nbt,
+                                          sp.iptr(sp.i_rtg), sp.iptr(sp.i_rc4), R.rbeg, R.nrt, A, b, Ls,
+                                          W, y, flags));
+    }
     if (sp.hybrid) {
         // the <= 27-pose core in registers, the back-substitution through the rounds and the
         // retraction: one single-workgroup launch (gn_solve.hip) reading the plan prefix; the
         // core is first laid out densely by a many-workgroup fill (one CU gathering it block by
-        // block took ~28 us)
-        M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail),
-                                          sp.ntail, sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
+        // block took ~28 us) -- inside the cooperative launch, or its own launch
+        if (!coop)
+            M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail),
+                                              sp.ntail, sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
         S.Hd = sp.ntail > 0 ? sp.dptr<double>(sp.o_dense) : nullptr;
         S.npad_h = sp.npad_tail;
         S.nmeta = (int)sp.nints_back;

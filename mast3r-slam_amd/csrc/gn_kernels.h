@@ -18,6 +18,8 @@ constexpr int kCholTile = 64;  // dense Cholesky tile
 constexpr int kFlagDone = 0;   // set once ||dx|| < delta_thresh (skips later iterations)
 constexpr int kFlagFail = 1;   // set by the factorisation when a pivot <= 0
 constexpr int kFlagNotRay = 2; // calib: some Xs point is not its pixel's ray times its depth
+constexpr int kFlagBarCount = 4;  // grid barrier of the all-rounds launch: arrivals
+constexpr int kFlagBarGen = 5;    // ... and its generation
 constexpr int kNumFlags = 16;
 
 // Where the per-point-edge inputs (idx, valid, Q) of local directed edge e live: edges
@@ -114,6 +116,15 @@ constexpr int kMaxNpad = 8192;  // dense solve limit: N <= 1171 keyframes
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
                                      double* x, int* flags);
 // multi-launch block-sparse elimination (gn_sparse.hip): one launch per round
+// every elimination round (+ optionally the hybrid core's dense fill) in one cooperative launch
+struct SpCoopArgs {
+    const int *tg, *tc3, *rtg, *rc4, *rounds, *tmap, *tail;
+    double *A, *b, *Lstore, *W, *y, *Hd;
+    int* flags;
+    int nrounds, ntail, npad;
+    int coop;  // 1: hipLaunchCooperativeKernel + cooperative-groups grid sync; 0: own barrier
+};
+hipError_t launch_sp_rounds_coop(hipStream_t st, const SpCoopArgs& args);
 hipError_t launch_sp_round(hipStream_t st, const int* tg, const int* tc3, int tbeg, int nbt,
                            const int* rtg, const int* rc4, int rbeg, int nrt, double* A, double* b,
                            double* Lstore, double* W, double* y, int* flags);

@@ -21,6 +21,7 @@
 // integers, then the blocks): a dependent global round trip is the unit of cost here.
 // Failure semantics follow SimplicialLLT (reference gn_kernels.cu:142-150): a pivot <= 0 sets
 // the failure flag and the update becomes zero.
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -39,25 +40,37 @@ constexpr int kLd = 8;      // LDS row stride (doubles) of a staged 7x7 block
 // rtg = (pose r | -1, begin, end) with rc4 = (v, code_r, W id | -1, owner node | -1), where
 // code = block * 2 + transposed (the block holds the rows of the other pose).  r = -1 collects
 // the poses without fronts: only their L and y are stored.
-__global__ __launch_bounds__(64) void sp_round_kernel(
-    const int* __restrict__ tg, const int* __restrict__ tc3, int tbeg, int nbt,
+// COH: the all-rounds launch reads, in round r + 1, blocks other workgroups (other XCDs) wrote
+// in round r.  The per-XCD L2s are not coherent, so those A / b accesses are agent-coherent
+// (relaxed agent-scope atomics: sc1 loads and write-through stores) and the grid barrier needs
+// no L2 write-back or invalidation.
+template <bool COH>
+__device__ __forceinline__ double ldA(const double* p) {
+    if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void stA(double* p, double v) {
+    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+template <bool COH>
+__device__ __forceinline__ void sp_round_target(
+    int gi, const int* __restrict__ tg, const int* __restrict__ tc3, int tbeg, int nbt,
     const int* __restrict__ rtg, const int* __restrict__ rc4, int rbeg, double* __restrict__ A,
     double* __restrict__ b, double* __restrict__ Lstore, double* __restrict__ W,
-    double* __restrict__ y, int* __restrict__ flags) {
-    __shared__ double sR[kGroups][7 * kLd];  // rows of W_rv, per contribution of the batch
-    __shared__ double sS[kGroups][7 * kLd];  // block target: rows of W_sv; RHS target: y_v
-    const int done = flags[kFlagDone];
-    const int gi = blockIdx.x, lane = threadIdx.x;
+    double* __restrict__ y, int* __restrict__ flags, double (*sR)[7 * kLd], double (*sS)[7 * kLd]) {
+    const int lane = threadIdx.x;
     const bool blk = gi < nbt;
     const int* T_ = blk ? tg + 3 * (tbeg + gi) : rtg + 3 * (rbeg + gi - nbt);
     const int tgt = T_[0], c0 = T_[1], c1 = T_[2];
-    if (done) return;
     const int g = lane / 7, ra = lane - 7 * g;
     // this lane's output: entry (er, ec) of the block, or row er of the RHS
     const int nact = tgt < 0 ? 0 : (blk ? 49 : 7);
     const int er = blk ? lane / 7 : lane, ec = lane % 7;
     double* dst = blk ? A + (int64_t)tgt * 49 + lane : b + (int64_t)tgt * 7 + lane;
-    const double d0 = lane < nact ? *dst : 0.0;
+    const double d0 = lane < nact ? ldA<COH>(dst) : 0.0;
     double acc = 0.0;
     bool bad = false;
     for (int base = c0; base < c1; base += kGroups) {
@@ -79,17 +92,17 @@ __global__ __launch_bounds__(64) void sp_round_kernel(
 #pragma unroll
             for (int i = 0; i < 7; i++)
 #pragma unroll
-                for (int j = 0; j <= i; j++) L[b7::pk(i, j)] = Av[i * 7 + j];
+                for (int j = 0; j <= i; j++) L[b7::pk(i, j)] = ldA<COH>(Av + i * 7 + j);
             const double* Ar = A + (int64_t)(cr >> 1) * 49;
 #pragma unroll
-            for (int m = 0; m < 7; m++) rr[m] = (cr & 1) ? Ar[m * 7 + ra] : Ar[ra * 7 + m];
+            for (int m = 0; m < 7; m++) rr[m] = ldA<COH>(Ar + ((cr & 1) ? m * 7 + ra : ra * 7 + m));
             if (blk) {
                 const double* As = A + (int64_t)(cs >> 1) * 49;
 #pragma unroll
-                for (int m = 0; m < 7; m++) rs[m] = (cs & 1) ? As[m * 7 + ra] : As[ra * 7 + m];
+                for (int m = 0; m < 7; m++) rs[m] = ldA<COH>(As + ((cs & 1) ? m * 7 + ra : ra * 7 + m));
             } else {
 #pragma unroll
-                for (int m = 0; m < 7; m++) rs[m] = b[(int64_t)v * 7 + m];
+                for (int m = 0; m < 7; m++) rs[m] = ldA<COH>(b + (int64_t)v * 7 + m);
             }
             b7::chol7(L, inv, bad);
             double wr[7], ws[7];
@@ -129,8 +142,20 @@ __global__ __launch_bounds__(64) void sp_round_kernel(
         }
         __syncthreads();
     }
-    if (lane < nact) *dst = d0 - acc;
+    if (lane < nact) stA<COH>(dst, d0 - acc);
     if (bad) flags[kFlagFail] = 1;  // benign race: every writer stores 1
+}
+
+// One round per launch: workgroup = target (the flag is loaded beside the target record).
+__global__ __launch_bounds__(64) void sp_round_kernel(
+    const int* __restrict__ tg, const int* __restrict__ tc3, int tbeg, int nbt,
+    const int* __restrict__ rtg, const int* __restrict__ rc4, int rbeg, double* __restrict__ A,
+    double* __restrict__ b, double* __restrict__ Lstore, double* __restrict__ W,
+    double* __restrict__ y, int* __restrict__ flags) {
+    __shared__ double sR[kGroups][7 * kLd];  // rows of W_rv, per contribution of the batch
+    __shared__ double sS[kGroups][7 * kLd];  // block target: rows of W_sv; RHS target: y_v
+    if (flags[kFlagDone]) return;
+    sp_round_target<false>(blockIdx.x, tg, tc3, tbeg, nbt, rtg, rc4, rbeg, A, b, Lstore, W, y, flags, sR, sS);
 }
 
 // x_v = L_v^-T (y_v - sum_r W_rv^T x_r), one workgroup per pose of the round; 7-lane group g
@@ -181,14 +206,10 @@ __global__ __launch_bounds__(64) void sp_back_kernel(
 
 // Dense core: Hd [npad + 64, npad] from the blocks of the ntail remaining poses (tmap:
 // ntail x ntail -> 2*block + transposed, or -1), RHS border row from b.
-__global__ __launch_bounds__(256) void sp_tail_fill_kernel(const double* __restrict__ A,
-                                                           const double* __restrict__ b,
-                                                           const int* __restrict__ tmap,
-                                                           const int* __restrict__ tail,
-                                                           int ntail, int npad,
-                                                           double* __restrict__ Hd,
-                                                           const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+template <bool COH>
+__device__ __forceinline__ void sp_tail_fill(const double* __restrict__ A, const double* __restrict__ b,
+                                             const int* __restrict__ tmap, const int* __restrict__ tail,
+                                             int ntail, int npad, double* __restrict__ Hd) {
     const int n = ntail * 7;
     const int64_t total = (int64_t)(npad + kCholTile) * npad;
     for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
@@ -198,20 +219,89 @@ __global__ __launch_bounds__(256) void sp_tail_fill_kernel(const double* __restr
         if (r > npad) {
             val = 0.0;
         } else if (r == npad) {
-            val = c < n ? b[(int64_t)tail[c / 7] * 7 + c % 7] : 0.0;
+            val = c < n ? ldA<COH>(b + (int64_t)tail[c / 7] * 7 + c % 7) : 0.0;
         } else if (r < n && c < n) {
             const int code = tmap[(r / 7) * ntail + c / 7];
             if (code < 0) {
                 val = 0.0;
             } else {
                 const double* Ab = A + (int64_t)(code >> 1) * 49;
-                val = (code & 1) ? Ab[(c % 7) * 7 + r % 7] : Ab[(r % 7) * 7 + c % 7];
+                val = ldA<COH>(Ab + ((code & 1) ? (c % 7) * 7 + r % 7 : (r % 7) * 7 + c % 7));
             }
         } else {
             val = (r == c) ? 1.0 : 0.0;
         }
         Hd[id] = val;
     }
+}
+
+__global__ __launch_bounds__(256) void sp_tail_fill_kernel(const double* __restrict__ A,
+                                                           const double* __restrict__ b,
+                                                           const int* __restrict__ tmap,
+                                                           const int* __restrict__ tail,
+                                                           int ntail, int npad,
+                                                           double* __restrict__ Hd,
+                                                           const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    sp_tail_fill<false>(A, b, tmap, tail, ntail, npad, Hd);
+}
+
+// All elimination rounds (and the hybrid's core fill) in ONE cooperative launch: a round costs
+// ~4 us of dependent work per workgroup (target record ~1, block loads ~1.4, 7x7 factor + W rows
+// ~1, Schur sums + store ~0.4, measured in-kernel) but ~9 us as its own launch, the rest being
+// the dependent launch's dispatch and drain.  Here a grid-wide barrier (cooperative groups,
+// co-residency guaranteed by hipLaunchCooperativeKernel) separates the rounds; workgroup w takes
+// the round's targets w, w + G, ...  The flag is read once: it was written by the previous
+// iteration's kernels, so every workgroup sees the same value and all leave or none.
+// Grid-wide barrier over the launch's workgroups (all resident: <= one 64-thread workgroup per
+// CU): arrival counter + generation word in the flags area.  Release = the arrival atomic
+// (writes back this XCD's L2), acquire = a fence after the generation moved (invalidates L1/L2),
+// so blocks written in one round are read fresh in the next on any XCD.  The spin is bounded
+// (~0.1 s): a workgroup that never arrives fails the solve instead of hanging the GPU.
+template <bool FENCED>
+__device__ __forceinline__ void grid_barrier(int* __restrict__ flags, unsigned nwg) {
+    if constexpr (!FENCED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my write-through stores landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned* cnt = reinterpret_cast<unsigned*>(flags + kFlagBarCount);
+        unsigned* gen = reinterpret_cast<unsigned*>(flags + kFlagBarGen);
+        const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned old = FENCED ? __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
+                                    : __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nwg - 1) {
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            int spins = 0;
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1 << 22)) {
+                    flags[kFlagFail] = 1;
+                    break;
+                }
+            }
+        }
+        if constexpr (FENCED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void sp_rounds_coop_kernel(SpCoopArgs a) {
+    __shared__ double sR[kGroups][7 * kLd];
+    __shared__ double sS[kGroups][7 * kLd];
+    if (a.flags[kFlagDone]) return;
+    for (int rd = 0; rd < a.nrounds; rd++) {
+        const int* R = a.rounds + 8 * rd;  // node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount
+        const int tbeg = R[2], nbt = R[3], rbeg = R[4], nrt = R[5];
+        for (int t = blockIdx.x; t < nbt + nrt; t += gridDim.x)
+            sp_round_target<true>(t, a.tg, a.tc3, tbeg, nbt, a.rtg, a.rc4, rbeg, a.A, a.b, a.Lstore, a.W, a.y,
+                                  a.flags, sR, sS);
+        if (a.coop)
+            cooperative_groups::this_grid().sync();
+        else
+            grid_barrier<false>(a.flags, gridDim.x);
+    }
+    if (a.ntail > 0 && a.Hd) sp_tail_fill<true>(a.A, a.b, a.tmap, a.tail, a.ntail, a.npad, a.Hd);
 }
 
 __global__ __launch_bounds__(256) void sp_tail_scatter_kernel(const double* __restrict__ xd,
@@ -231,6 +321,27 @@ hipError_t launch_sp_round(hipStream_t st, const int* tg, const int* tc3, int tb
     if (nbt + nrt <= 0) return hipSuccess;
     hipLaunchKernelGGL(sp_round_kernel, dim3(nbt + nrt), dim3(64), 0, st, tg, tc3, tbeg, nbt, rtg,
                        rc4, rbeg, A, b, Lstore, W, y, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_sp_rounds_coop(hipStream_t st, const SpCoopArgs& args) {
+    if (args.nrounds <= 0 && (args.ntail <= 0 || !args.Hd)) return hipSuccess;
+    static int grid = 0;
+    if (grid == 0) {
+        int dev = 0, ncu = 0, per = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)sp_rounds_coop_kernel, 64, 0);
+        if (e != hipSuccess) return e;
+        grid = std::max(1, std::min(ncu * std::max(per, 1), 256));  // <= one workgroup per CU
+    }
+    SpCoopArgs a = args;
+    if (a.coop) {
+        void* kargs[] = {&a};
+        return hipLaunchCooperativeKernel((const void*)sp_rounds_coop_kernel, dim3(grid), dim3(64), kargs, 0, st);
+    }
+    hipLaunchKernelGGL(sp_rounds_coop_kernel, dim3(grid), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 
