@@ -148,3 +148,64 @@ def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout):
     T_o, _, _ = oracle.gauss_newton(P, g.Twc.numpy(), g.Xs.numpy(), g.Cs.numpy(), g.ii.numpy(),
                                     g.jj.numpy(), g.idx.numpy(), g.valid.numpy(), g.Q.numpy())
     assert rel(T0, T_o) < 1e-5, rel(T0, T_o)
+
+
+def _rccl_worker(port, mode, out_q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mast3r-slam_amd")]
+    import torch.distributed as dist
+
+    import mast3r_slam_backends as mb
+    from m3s.dist import RcclComm, gauss_newton_sharded
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        torch.cuda.set_device(0)
+        g = _graph(mode)
+        c = lambda t: t.cuda().contiguous()
+        comm = RcclComm(0, 1, device=torch.device("cuda", 0))
+        Twc = c(g.Twc)
+        gauss_newton_sharded(mode, Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx), c(g.valid), c(g.Q), 0,
+                             comm, ITERS, 0.0, **_params(g, mode))
+        Twc_ref = c(g.Twc)
+        if mode == "rays":
+            mb.gauss_newton_rays(Twc_ref, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx), c(g.valid), c(g.Q),
+                                 LOCAL["sigma_ray"], LOCAL["sigma_dist"], LOCAL["C_conf"], LOCAL["Q_conf"],
+                                 ITERS, 0.0)
+        else:
+            mb.gauss_newton_calib(Twc_ref, c(g.Xs), c(g.Cs), c(g.K), c(g.ii), c(g.jj), c(g.idx), c(g.valid),
+                                  c(g.Q), g.H, g.W, LOCAL["pixel_border"], LOCAL["depth_eps"],
+                                  LOCAL["sigma_pixel"], LOCAL["sigma_depth"], LOCAL["C_conf"],
+                                  LOCAL["Q_conf"], ITERS, 0.0)
+        torch.cuda.synchronize()
+        out_q.put((Twc.cpu().numpy(), Twc_ref.cpu().numpy(), None))
+        comm.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        out_q.put((None, None, repr(e)))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_rccl_communicator_in_the_op(backend, mode):
+    """The production exchange: the library's RCCL communicator (m3s_comm_get_unique_id /
+    m3s_comm_init, librccl resolved at run time) and the in-stream ncclAllReduce of the block
+    system inside the op, with one rank on the box's one GPU (RCCL needs a GPU per rank, so more
+    ranks are the driver's multi-GPU bench).  A one-rank sum leaves the system unchanged: the
+    poses must equal the unsharded op's bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), mode, q))
+    p.start()
+    try:
+        T, T_ref, err = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert err is None, err
+    assert p.exitcode == 0
+    assert np.array_equal(T, T_ref)
