@@ -108,7 +108,9 @@ def main():
     torch.cuda.synchronize()
     # the timed region carries HIP events around each accumulate launch only (the roofline
     # kernel); the other phases are timed in one extra untimed step below
-    mb.lib.m3s_prof_begin_accum()
+    acc_events = os.environ.get("M3S_BENCH_ACC_EVENTS", "1") != "0"
+    if acc_events:
+        mb.lib.m3s_prof_begin_accum()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -135,7 +137,7 @@ def main():
     pair_iters = E_und * iters * args.steps
     value = pair_iters / elapsed
     n_it = max(nprof.value, 1)
-    acc_ms = prof[0] / n_it
+    acc_ms = prof[0] / n_it if acc_events else ph[0] / n_ph
     packed = iters >= 3 and os.environ.get("M3S_GN_PACK", "1") != "0"
     bpe = PACKED_BYTES_PER_POINT_EDGE[mode] if packed else REF_BYTES_PER_POINT_EDGE
     bytes_launch = bpe * g.HW * (hi - lo)

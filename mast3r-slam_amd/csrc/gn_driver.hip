@@ -81,6 +81,7 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // asynchronous; the next call waits for them (an event) before overwriting the buffer.
 struct Staging {
     char* buf = nullptr;
+    char* dev = nullptr;  // buf's device address (the stage-copy kernel reads it directly)
     size_t cap = 0;
     hipEvent_t done = nullptr;
     bool pending = false;
@@ -101,9 +102,22 @@ struct Staging {
             if (hipHostMalloc((void**)&buf, cap, hipHostMallocDefault) != hipSuccess) {
                 buf = nullptr;
                 cap = 0;
+            } else if (hipHostGetDevicePointer((void**)&dev, buf, 0) != hipSuccess) {
+                dev = nullptr;
             }
         }
         return buf;
+    }
+    // H2D of [h, h + bytes) (inside buf) to dst, stream-ordered: by a kernel reading the pinned
+    // buffer (default), or by hipMemcpyAsync (M3S_STAGE_DMA=1, or no device address)
+    hipError_t upload(void* dst, const char* h, size_t bytes, hipStream_t st) {
+        static const bool dma = [] {
+            const char* e = getenv("M3S_STAGE_DMA");
+            return e && atoi(e) != 0;
+        }();
+        if (!dma && dev && (bytes & 3) == 0 && ((uintptr_t)dst & 15) == 0 && ((h - buf) & 15) == 0)
+            return launch_stage_copy(st, dst, dev + (h - buf), bytes);
+        return hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st);
     }
     hipError_t mark(hipStream_t st) {
         if (!done) {
@@ -211,9 +225,7 @@ struct Plan {
     std::vector<int> blk_ref;                     // the same entries as (edge<<3 | type), gn_refacc.hip
     std::vector<int> grad_ptr, grad_ent;          // CSR: pose -> (edge<<1 | neg)
     std::vector<int> slotmap;                     // (npose x npose) -> slot or -1
-    std::vector<int> sched;                       // accumulate task order: e * nchunks + c
-    std::vector<int> sched4;                      // the same as {e, c, ii_loc[e], jj_loc[e]} records
-    std::vector<std::pair<int, int>> pairs;       // slot nblk0.. -> unordered pose pair (a<b)
+    std::vector<std::pair<int, int>> pairs;      // slot nblk0.. -> unordered pose pair (a<b)
     float K[4] = {0, 0, 0, 0};
 };
 
@@ -222,18 +234,26 @@ struct Plan {
 // groups, one per XCD (blocks b, b+8, ... share an XCD under round-robin dispatch); inside a
 // group tasks run chunk-major, so the few keyframes of a group stay L2-resident while all
 // of their edges stream the same point range.
+// Written straight into the upload image as the accumulate's task records {e, c, ii, jj}:
+// group g's list is chunk-major (element k: edge order[lo_g + k % n_g], chunk k / n_g) and the
+// groups are interleaved round-robin.
 void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_loc, int nchunks,
-                    std::vector<int>& sched) {
+                    int* rec) {
     const int E = (int)ii_loc.size();
-    sched.clear();
-    sched.reserve((size_t)E * nchunks);
+    auto put = [&](int e, int c) {
+        rec[0] = e;
+        rec[1] = c;
+        rec[2] = ii_loc[e];
+        rec[3] = jj_loc[e];
+        rec += 4;
+    };
     static const bool off = [] {
         const char* e = getenv("M3S_ACC_SCHED");
         return e && atoi(e) == 0;
     }();
     if (off) {
         for (int e = 0; e < E; e++)
-            for (int c = 0; c < nchunks; c++) sched.push_back(e * nchunks + c);
+            for (int c = 0; c < nchunks; c++) put(e, c);
         return;
     }
     std::vector<int> order(E);
@@ -241,23 +261,17 @@ void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_l
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
         return jj_loc[a] != jj_loc[b] ? jj_loc[a] < jj_loc[b] : ii_loc[a] < ii_loc[b];
     });
-    const int G = 8;
-    std::vector<std::vector<int>> lists(G);
+    constexpr int G = 8;
+    int lo[G], n[G];
+    int64_t len_max = 0;
     for (int g = 0; g < G; g++) {
-        const int lo = (int)((int64_t)E * g / G), hi = (int)((int64_t)E * (g + 1) / G);
-        for (int c = 0; c < nchunks; c++)
-            for (int q = lo; q < hi; q++) lists[g].push_back(order[q] * nchunks + c);
+        lo[g] = (int)((int64_t)E * g / G);
+        n[g] = (int)((int64_t)E * (g + 1) / G) - lo[g];
+        len_max = std::max(len_max, (int64_t)n[g] * nchunks);
     }
-    std::vector<size_t> pos(G, 0);
-    for (bool any = true; any;) {
-        any = false;
-        for (int g = 0; g < G; g++) {
-            if (pos[g] < lists[g].size()) {
-                sched.push_back(lists[g][pos[g]++]);
-                any = true;
-            }
-        }
-    }
+    for (int64_t k = 0; k < len_max; k++)
+        for (int g = 0; g < G; g++)
+            if (k < (int64_t)n[g] * nchunks) put(order[lo[g] + (int)(k % n[g])], (int)(k / n[g]));
 }
 
 int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
@@ -686,7 +700,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
             std::memcpy(hr, v, sizeof(v));
             hr += 8;
         }
-        M3S_HIP_CHECK(hipMemcpyAsync(sp.dbuf + sp.o_int, h, sizeof(int) * n, hipMemcpyHostToDevice, st));
+        M3S_HIP_CHECK(g_stage_out.upload(sp.dbuf + sp.o_int, reinterpret_cast<const char*>(h), sizeof(int) * n, st));
         M3S_HIP_CHECK(g_stage_out.mark(st));  // no host sync: the staging buffer outlives the copy
     }
     return M3S_OK;
@@ -741,6 +755,7 @@ struct Ctx {
     bool packed = false;  // per-call packed stream (gn_pack_kernel) feeds the accumulate
     bool compact = false;  // ... holding only the live points (gn_pack_compact_kernel)
     bool ref_order = false;  // M3S_GN_ORDER_REFERENCE: gn_refacc.hip accumulate + assembly
+    bool pack_issued = false;  // prepare_iterations already enqueued (setup's early pack)
     RefParams R;
     Layout L;
     Plan plan;
@@ -781,7 +796,11 @@ struct Ctx {
     }
 };
 
-int setup(const m3s_gn_args& a, Ctx& c) {
+int prepare_iterations(const m3s_gn_args& a, Ctx& c);
+
+// early_pack: launch the packed stream (prepare_iterations) as soon as the edge lists are on
+// the device, before the host builds the accumulate schedule
+int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     int rc = validate(a);
     if (rc) return rc;
     c.st = (hipStream_t)a.stream;
@@ -792,62 +811,8 @@ int setup(const m3s_gn_args& a, Ctx& c) {
     rc = build_plan(a, c.st, c.plan);
     if (rc) return rc;
     const auto s1 = std::chrono::steady_clock::now();
-    build_schedule(c.plan.ii_loc, c.plan.jj_loc, c.L.nchunks, c.plan.sched);
-    {   // the accumulate's task records carry the edge's keyframes: one load, not three levels
-        Plan& pl = c.plan;
-        const int nc = c.L.nchunks;
-        pl.sched4.resize(4 * pl.sched.size());
-        for (size_t t = 0; t < pl.sched.size(); t++) {
-            const int e = pl.sched[t] / nc;
-            pl.sched4[4 * t] = e;
-            pl.sched4[4 * t + 1] = pl.sched[t] - e * nc;
-            pl.sched4[4 * t + 2] = pl.ii_loc[e];
-            pl.sched4[4 * t + 3] = pl.jj_loc[e];
-        }
-    }
-    if (prof_host)
-        fprintf(stderr, "gn host: build_plan %.0f us, schedule %.0f us\n",
-                std::chrono::duration<double, std::micro>(s1 - s0).count(),
-                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - s1).count());
     const Layout& L = c.L;
     const Plan& p = c.plan;
-    // the workspace's plan integers (flags .. sched, one contiguous span of the layout) as an
-    // image in pinned memory, one asynchronous copy
-    {
-        const size_t lo = L.flags, hi = L.sched + sizeof(int) * p.sched4.size();
-        const size_t nslot = c.need_slotmap ? p.slotmap.size() : 0;
-        if (c.need_slotmap) {
-            rc = c.alloc_dense(L.npad, (int)std::max<int64_t>(a.N - 1, 0));
-            if (rc) return rc;
-        }
-        char* h = g_stage_ws.get(hi - lo + sizeof(int) * nslot);
-        M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
-        std::memset(h, 0, L.ii_loc - lo);  // flags
-        // M3S_GN_RAYCHECK=1: let the packed calib accumulate take the ray-constrained path
-        // (Xj read as its depth, 16 instead of 24 B per point-edge) when every point passes the
-        // check.  Off by default: bitwise the same result, but only ~3 % faster on cfg3 -- the
-        // kernel is latency-bound, not HBM-bound.
-        if (env_int("M3S_GN_RAYCHECK", 0) == 0) reinterpret_cast<int*>(h)[kFlagNotRay] = 1;
-        auto put = [&](size_t off, const std::vector<int>& v) {
-            if (!v.empty()) std::memcpy(h + (off - lo), v.data(), sizeof(int) * v.size());
-        };
-        put(L.ii_loc, p.ii_loc);
-        put(L.jj_loc, p.jj_loc);
-        put(L.blk_ptr, p.blk_ptr);
-        put(L.blk_ent, p.blk_ent);
-        put(L.blk_ref, p.blk_ref);
-        put(L.grad_ptr, p.grad_ptr);
-        put(L.grad_ent, p.grad_ent);
-        put(L.sched, p.sched4);
-        M3S_HIP_CHECK(hipMemcpyAsync(c.ws + lo, h, hi - lo, hipMemcpyHostToDevice, c.st));
-        if (nslot) {  // the dense (npose x npose) slot table
-            std::memcpy(h + (hi - lo), p.slotmap.data(), sizeof(int) * nslot);
-            M3S_HIP_CHECK(hipMemcpyAsync(c.dyn + c.o_slot, h + (hi - lo), sizeof(int) * nslot,
-                                         hipMemcpyHostToDevice, c.st));
-        }
-        M3S_HIP_CHECK(g_stage_ws.mark(c.st));
-    }
-
     AccParams& P = c.P;
     P.s0_inv = 1.0f / a.sigma0;
     P.s1_inv = (a.mode == M3S_GN_POINTS) ? 0.0f : 1.0f / a.sigma1;
@@ -912,6 +877,58 @@ int setup(const m3s_gn_args& a, Ctx& c) {
         R.pixel_border = a.pixel_border;
         R.HW = a.HW;
         R.variant = env_int("M3S_GN_REF_VARIANT", 0);  // diagnostics
+    }
+    // the workspace's plan integers (flags .. sched, one contiguous span of the layout) as an
+    // image in pinned memory: the edge lists / CSR lists first (what the pack reads), then the
+    // accumulate's task records (built while the GPU packs)
+    const size_t ntask = (size_t)a.E_local * L.nchunks;
+    const size_t lo = L.flags, hi = L.sched + sizeof(int) * 4 * ntask;
+    const size_t nslot = c.need_slotmap ? p.slotmap.size() : 0;
+    if (c.need_slotmap) {
+        rc = c.alloc_dense(L.npad, (int)std::max<int64_t>(a.N - 1, 0));
+        if (rc) return rc;
+    }
+    char* h = g_stage_ws.get(hi - lo + sizeof(int) * nslot);
+    M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
+    std::memset(h, 0, L.ii_loc - lo);  // flags
+    // M3S_GN_RAYCHECK=1: let the packed calib accumulate take the ray-constrained path
+    // (Xj read as its depth, 16 instead of 24 B per point-edge) when every point passes the
+    // check.  Off by default: bitwise the same result, but only ~3 % faster on cfg3 -- the
+    // kernel is latency-bound, not HBM-bound.
+    if (env_int("M3S_GN_RAYCHECK", 0) == 0) reinterpret_cast<int*>(h)[kFlagNotRay] = 1;
+    auto put = [&](size_t off, const std::vector<int>& v) {
+        if (!v.empty()) std::memcpy(h + (off - lo), v.data(), sizeof(int) * v.size());
+    };
+    put(L.ii_loc, p.ii_loc);
+    put(L.jj_loc, p.jj_loc);
+    put(L.blk_ptr, p.blk_ptr);
+    put(L.blk_ent, p.blk_ent);
+    put(L.blk_ref, p.blk_ref);
+    put(L.grad_ptr, p.grad_ptr);
+    put(L.grad_ent, p.grad_ent);
+    M3S_HIP_CHECK(g_stage_ws.upload(c.ws + lo, h, L.sched - lo, c.st));
+    if (early_pack) {
+        rc = prepare_iterations(a, c);
+        if (rc) return rc;
+        c.pack_issued = true;
+    }
+    const auto s2 = std::chrono::steady_clock::now();
+    // the accumulate's task records carry the edge's keyframes: one load, not three levels
+    build_schedule(p.ii_loc, p.jj_loc, L.nchunks, reinterpret_cast<int*>(h + (L.sched - lo)));
+    if (ntask > 0)
+        M3S_HIP_CHECK(g_stage_ws.upload(c.ws + L.sched, h + (L.sched - lo), hi - L.sched, c.st));
+    if (nslot) {  // the dense (npose x npose) slot table
+        std::memcpy(h + (hi - lo), p.slotmap.data(), sizeof(int) * nslot);
+        M3S_HIP_CHECK(hipMemcpyAsync(c.dyn + c.o_slot, h + (hi - lo), sizeof(int) * nslot,
+                                     hipMemcpyHostToDevice, c.st));
+    }
+    M3S_HIP_CHECK(g_stage_ws.mark(c.st));
+    if (prof_host) {
+        auto us = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+            return std::chrono::duration<double, std::micro>(y - x).count();
+        };
+        fprintf(stderr, "gn host: build_plan %.0f us, params+lists+pack %.0f us, schedule %.0f us\n",
+                us(s0, s1), us(s1, s2), us(s2, std::chrono::steady_clock::now()));
     }
     return M3S_OK;
 }
@@ -1158,22 +1175,22 @@ int run(const m3s_gn_args& a) {
     const auto t0 = now();
     Ctx c;
     c.need_slotmap = env_int("M3S_SOLVER_DENSE", 0) != 0;
-    int rc = setup(a, c);
+    // the packed stream is launched inside setup as soon as its inputs are on the device: the
+    // GPU builds it while the host plans the accumulate schedule and the elimination
+    int rc = setup(a, c, a.N > 1);
     if (rc) return rc;
     const auto t1 = now();
     const int npose = (int)(a.N - 1);
     if (npose <= 0) return M3S_OK;  // nothing to optimise (all poses pinned)
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
-    // the packed stream first: the GPU builds it while the host plans the elimination
-    rc = prepare_iterations(a, c);
-    if (rc) return rc;
-    std::chrono::steady_clock::time_point t2 = now(), t3 = t2;
+    std::chrono::steady_clock::time_point t2 = t1, t2a = t1, t3 = t1;
     if (env_int("M3S_SOLVER_DENSE", 0) == 0 || c.ref_order) {
         // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
         // single-workgroup solve when its plan needs few rounds, else multi-launch
         const int choice = env_int("M3S_SOLVER", 0);
         build_sparse_plan(c.plan, npose, fused_policy(), c.sp);
+        t2a = now();
         const bool meta_fits = solve_lds_bytes((int)c.sp.nints) <= (size_t)kSolveMaxLds;
         const bool fused_ok = c.sp.fused && meta_fits && npose <= solve_max_poses() &&
                               (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <=
@@ -1200,10 +1217,9 @@ int run(const m3s_gn_args& a) {
         if (rc) return rc;
         t3 = now();
     }
-    const auto t4 = now();
     if (prof_host)
-        fprintf(stderr, "gn host: setup %.0f us, pack launch %.0f us, sparse plan %.0f us, upload %.0f us\n",
-                us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4));
+        fprintf(stderr, "gn host: setup %.0f us, fused plan %.0f us, other plan %.0f us, upload %.0f us\n",
+                us(t0, t1), us(t1, t2a), us(t2a, t2), us(t2, t3));
     for (int itr = 0; itr < a.max_iter; itr++) {
         g_prof.mark(c.st);
         rc = enqueue_system(a, c);

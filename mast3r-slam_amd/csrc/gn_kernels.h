@@ -171,6 +171,9 @@ struct SolveArgs {
 size_t solve_lds_bytes(int nmeta_lds);
 int solve_max_poses();  // x stays in LDS: the single-workgroup solve takes at most this many poses
 hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
+// copy `bytes` (a multiple of 4; both addresses 16-B aligned) from pinned host memory (its
+// device address) to device memory, stream-ordered, by a kernel
+hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes);
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
                           float delta_thresh, int* flags);
 

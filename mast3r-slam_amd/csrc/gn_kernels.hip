@@ -568,9 +568,35 @@ __global__ __launch_bounds__(256) void gn_retract_kernel(float* __restrict__ Twc
     }
 }
 
+// Per-call plan upload: the device reads the pinned host image itself (16 B per lane, 4 B
+// for a ragged end).  A hipMemcpyAsync H2D is carried out by a DMA engine, whose handshake with
+// the kernel queue left the GPU idle ~100 us around every mid-stream plan upload (rocprofv3
+// kernel trace).
+__global__ __launch_bounds__(256) void stage_copy_kernel(const uint32_t* __restrict__ src,
+                                                         uint32_t* __restrict__ dst, int64_t n4) {
+    const int64_t n16 = n4 >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint4* s16 = reinterpret_cast<const uint4*>(src);
+    uint4* d16 = reinterpret_cast<uint4*>(dst);
+    for (int64_t i = t0; i < n16; i += stride) d16[i] = s16[i];
+    for (int64_t i = 4 * n16 + t0; i < n4; i += stride) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------------------
 // launchers (host)
 // ---------------------------------------------------------------------------
+
+hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    if ((bytes & 3) || ((uintptr_t)dst & 15) || ((uintptr_t)src_dev & 15)) return hipErrorInvalidValue;
+    const int64_t n4 = (int64_t)(bytes >> 2);
+    const int64_t want = ((n4 >> 2) + 255) / 256;
+    const int blocks = (int)(want < 1 ? 1 : (want > 256 ? 256 : want));
+    hipLaunchKernelGGL(stage_copy_kernel, dim3(blocks), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t*>(src_dev), reinterpret_cast<uint32_t*>(dst), n4);
+    return hipGetLastError();
+}
 
 hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
                               const float* Twc, const int* ii_loc, double* edgeblk,
