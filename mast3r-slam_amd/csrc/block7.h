@@ -61,14 +61,5 @@ __device__ __forceinline__ void bwd7(const double (&L)[28], const double (&inv)[
     }
 }
 
-// v[k] for a runtime k without dynamic register indexing
-template <int N>
-__device__ __forceinline__ double pick(const double (&v)[N], int k) {
-    double r = v[0];
-#pragma unroll
-    for (int m = 1; m < N; m++) r = (m == k) ? v[m] : r;
-    return r;
-}
-
 }  // namespace b7
 }  // namespace m3s

@@ -202,8 +202,26 @@ __device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T,
         const V w0 = huber(swp * e0) * wcp;
         const V w1 = huber(swp * e1) * wcp;
         const V w2 = huber(swd * e2) * wcd;
-        const V fx = vsplat(P.fx, x), fy = vsplat(P.fy, x), one = vsplat(1.0f, x);
+        const V one = vsplat(1.0f, x);
         const V xz = x * zj_inv, yz = y * zj_inv, xy = x * y;
+#ifndef M3S_CALIB_FOLD_F
+#define M3S_CALIB_FOLD_F 1
+#endif
+#if M3S_CALIB_FOLD_F
+        // the pixel rows are f * r' (r' = the normalised-plane row): w r r^T = (w f^2) r' r'^T and
+        // w r e = (w f^2) r' (e / f), so the focal lengths fold into the weight and the residual
+        // (2 multiplies per row instead of 5)
+        const float fx2 = P.fx * P.fx, fy2 = P.fy * P.fy, fx_inv = 1.0f / P.fx, fy_inv = 1.0f / P.fy;
+        {
+            const V r[7] = {zj_inv, zero, -xz, -xy, vfma(x, x, one), -y, zero};
+            acc_row<0b0111101>(acc, r, w0 * vsplat(fx2, x), e0 * vsplat(fx_inv, x));
+        }
+        {
+            const V r[7] = {zero, zj_inv, -yz, -vfma(y, y, one), xy, x, zero};
+            acc_row<0b0111110>(acc, r, w1 * vsplat(fy2, x), e1 * vsplat(fy_inv, x));
+        }
+#else
+        const V fx = vsplat(P.fx, x), fy = vsplat(P.fy, x);
         {
             const V r[7] = {fx * zj_inv, zero, -fx * xz, -fx * xy, fx * vfma(x, x, one), -fx * y, zero};
             acc_row<0b0111101>(acc, r, w0, e0);
@@ -212,6 +230,7 @@ __device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T,
             const V r[7] = {zero, fy * zj_inv, -fy * yz, -fy * vfma(y, y, one), fy * xy, fy * x, zero};
             acc_row<0b0111110>(acc, r, w1, e1);
         }
+#endif
         {
             const V r[7] = {zero, zero, zj_inv, y, -x, zero, one};
             acc_row<0b1011100>(acc, r, w2, e2);

@@ -402,6 +402,7 @@ struct SparsePlan {
     // multi-launch rounds (sp_round_kernel), per contribution: (v, code_r, code_s) for block
     // targets, (v, code_r, W id, owner node | -1) for RHS targets; code = block * 2 + transposed
     std::vector<int> tc3, rc4;
+    std::vector<int> inl;  // multi-launch rounds: one kSpRec record per target (gn_kernels.h)
     // device (one stream-ordered allocation per call)
     char* dbuf = nullptr;
     size_t o_dense = 0, o_linv = 0;  // the dense core (npad_tail + 64) x npad_tail and its tile inverses
@@ -412,7 +413,7 @@ struct SparsePlan {
     // core + back-substitution launch stages in LDS) [tg tc rtg rc] (nints: the whole plan of
     // the single-workgroup solve) [tc3 rc4] (multi-launch rounds only)
     size_t i_nodes = 0, i_fptr = 0, i_fronts = 0, i_tg = 0, i_tc = 0, i_rtg = 0, i_rc = 0,
-           i_tail = 0, i_tmap = 0, i_rounds = 0, i_tc3 = 0, i_rc4 = 0, nints = 0, nints_back = 0;
+           i_tail = 0, i_tmap = 0, i_rounds = 0, i_tc3 = 0, i_rc4 = 0, i_inl = 0, nints = 0, nints_back = 0;
     template <typename T>
     T* dptr(size_t off) const { return reinterpret_cast<T*>(dbuf + off); }
     const int* iptr(size_t i) const { return reinterpret_cast<const int*>(dbuf + o_int) + i; }
@@ -613,6 +614,21 @@ void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparseP
             k = e;
         }
         R.nrt = (int)sp.rtg.size() / 3 - R.rbeg;
+        if (!pol.fused) {
+            // the round's target records (block targets, then RHS targets), the first kSpInline
+            // contributions inline
+            auto record = [&](const int* T_, const std::vector<int>& lst, int w) {
+                const size_t o = sp.inl.size();
+                sp.inl.resize(o + kSpRec, 0);
+                sp.inl[o] = T_[0];
+                sp.inl[o + 1] = T_[1];
+                sp.inl[o + 2] = T_[2];
+                for (int k = 0; k < kSpInline && T_[1] + k < T_[2]; k++)
+                    for (int f = 0; f < w; f++) sp.inl[o + 4 + 4 * k + f] = lst[(size_t)w * (T_[1] + k) + f];
+            };
+            for (int t = 0; t < R.nbt; t++) record(&sp.tg[3 * (R.tbeg + t)], sp.tc3, 3);
+            for (int t = 0; t < R.nrt; t++) record(&sp.rtg[3 * (R.rbeg + t)], sp.rc4, 4);
+        }
         R.wcount = sp.nW - R.wbeg;
         sp.rounds.push_back(R);
         // eliminate: drop the poses, connect each front into a clique (fill)
@@ -675,15 +691,16 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     // the plan integers in one array (layout: SparsePlan), the rounds after tmap
     std::vector<const std::vector<int>*> parts = {&sp.nodes, &sp.fptr, &sp.fronts, &sp.tail,
                                                   &sp.tmap, &sp.tg, &sp.tc, &sp.rtg, &sp.rc,
-                                                  &sp.tc3, &sp.rc4};
+                                                  &sp.tc3, &sp.rc4, &sp.inl};
     size_t* offs[] = {&sp.i_nodes, &sp.i_fptr, &sp.i_fronts, &sp.i_tail, &sp.i_tmap, &sp.i_tg,
-                      &sp.i_tc, &sp.i_rtg, &sp.i_rc, &sp.i_tc3, &sp.i_rc4};
+                      &sp.i_tc, &sp.i_rtg, &sp.i_rc, &sp.i_tc3, &sp.i_rc4, &sp.i_inl};
     size_t n = 0;
     for (size_t k = 0; k < parts.size(); k++) {
         if (k == 5) {
             sp.i_rounds = n;
             n += 8 * sp.rounds.size();
         }
+        if (parts[k] == &sp.inl) n = align_up(n, 4);  // 16-B records (int4 loads)
         *offs[k] = n;
         n += parts[k]->size();
     }
@@ -1114,9 +1131,8 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     const bool coop = coop_mode != 0;
     if (coop) {
         SpCoopArgs ca{};
-        ca.tg = sp.iptr(sp.i_tg);
+        ca.inl = sp.iptr(sp.i_inl);
         ca.tc3 = sp.iptr(sp.i_tc3);
-        ca.rtg = sp.iptr(sp.i_rtg);
         ca.rc4 = sp.iptr(sp.i_rc4);
         ca.rounds = sp.iptr(sp.i_rounds);
         ca.tmap = sp.iptr(sp.i_tmap);
@@ -1135,9 +1151,8 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         M3S_HIP_CHECK(launch_sp_rounds_coop(c.st, ca));
     } else {
         for (const SpRound& R : sp.rounds)
-            M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_tg), sp.iptr(sp.i_tc3), R.tbeg, R.nbt,
-                                          sp.iptr(sp.i_rtg), sp.iptr(sp.i_rc4), R.rbeg, R.nrt, A, b, Ls,
-                                          W, y, flags));
+            M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_inl), R.tbeg + R.rbeg, R.nbt, R.nrt,
+                                          sp.iptr(sp.i_tc3), sp.iptr(sp.i_rc4), A, b, Ls, W, y, flags));
     }
     if (sp.hybrid) {
         // the <= 27-pose core in registers, the back-substitution through the rounds and the

@@ -117,17 +117,23 @@ hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, doubl
                                      double* x, int* flags);
 // multi-launch block-sparse elimination (gn_sparse.hip): one launch per round
 // every elimination round (+ optionally the hybrid core's dense fill) in one cooperative launch
+// Per round target, one record of kSpRec ints: {target, c0, c1, 0} then the first kSpInline
+// contributions {v, code_r, code_s | W id, 0 | owner} inline (the rest from tc3 / rc4), so a
+// workgroup's plan arrives in ONE load round trip with the flag.  Round rd's records start at
+// tbeg + rbeg (its block targets, then its RHS targets).
+constexpr int kSpInline = 9;
+constexpr int kSpRec = 4 + 4 * kSpInline;
 struct SpCoopArgs {
-    const int *tg, *tc3, *rtg, *rc4, *rounds, *tmap, *tail;
+    const int *inl, *tc3, *rc4, *rounds, *tmap, *tail;
     double *A, *b, *Lstore, *W, *y, *Hd;
     int* flags;
     int nrounds, ntail, npad;
     int coop;  // 1: hipLaunchCooperativeKernel + cooperative-groups grid sync; 0: own barrier
 };
 hipError_t launch_sp_rounds_coop(hipStream_t st, const SpCoopArgs& args);
-hipError_t launch_sp_round(hipStream_t st, const int* tg, const int* tc3, int tbeg, int nbt,
-                           const int* rtg, const int* rc4, int rbeg, int nrt, double* A, double* b,
-                           double* Lstore, double* W, double* y, int* flags);
+hipError_t launch_sp_round(hipStream_t st, const int* inl, int ibeg, int nbt, int nrt, const int* tc3,
+                           const int* rc4, double* A, double* b, double* Lstore, double* W, double* y,
+                           int* flags);
 hipError_t launch_sp_back(hipStream_t st, int nnodes, const int* nodes, const int* fptr,
                           const int* fronts, int node_begin, const double* Lstore, const double* W,
                           const double* y, double* x, const int* flags);

@@ -168,14 +168,6 @@ __device__ __forceinline__ void inv7(const double (&L)[28], const double (&inv)[
     }
 }
 
-// v[k] for a runtime k in [0, 7) without dynamic register indexing
-__device__ __forceinline__ double pick7(const double (&v)[7], int k) {
-    double r = v[0];
-#pragma unroll
-    for (int m = 1; m < 7; m++) r = (m == k) ? v[m] : r;
-    return r;
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------------
@@ -289,13 +281,14 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
                 for (int m = 0; m <= c; m++) s2 = fma(Li[pk(c, m)], z[m], s2);
                 y[c] = s2;
             }
-            if (lane < 28) {
-                double v = Li[0];
+            // every lane holds the same values: lane 0 stores them (no per-lane select chains
+            // on the critical path)
+            if (lane == 0) {
 #pragma unroll
-                for (int k = 1; k < 28; k++) v = (k == lane) ? Li[k] : v;
-                sL[K * kLRec + lane] = v;
+                for (int k = 0; k < 28; k++) sL[K * kLRec + k] = Li[k];
+#pragma unroll
+                for (int c = 0; c < 7; c++) sZ[c0 + c] = y[c];
             }
-            if (lane < 7) sZ[c0 + lane] = pick7(y, lane);
         }
         if (K >= 3 && K < 5) tick(7);
         lds_barrier();
@@ -434,7 +427,11 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
             for (int i = c; i < 7; i++) s2 = fma(Li[pk(i, c)], z[i], s2);
             xk[c] = s2;
         }
-        if (W == 0 && lane < 7) sX[Mtail[K] * 7 + lane] = pick7(xk, lane);
+        if (W == 0 && lane == 0) {
+            const int xo = Mtail[K] * 7;
+#pragma unroll
+            for (int c = 0; c < 7; c++) sX[xo + c] = xk[c];
+        }
         if (tid < c0) {
             double s2 = sZ[tid];
 #pragma unroll
@@ -486,6 +483,7 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
     int* __restrict__ M = reinterpret_cast<int*>(smem + kRegionDoubles);
     for (int i = tid; i < a.nmeta; i += NT) M[i] = a.meta[i];
     lds_barrier();
+    tick(14);
     const int* __restrict__ Mrounds = M + a.o_rounds;
     const int* __restrict__ Mnodes = M + a.o_nodes;
     const int* __restrict__ Mfptr = M + a.o_fptr;
@@ -723,8 +721,14 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
 #pragma unroll
                 for (int m = 0; m < 7; m++) zz[m] = __shfl(z, (lane < 63 ? 7 * g : 0) + m, 64);
                 if (on && s == 0) {
+                    // zz is the same in the group's 7 lanes: one lane stores it (a per-lane pick
+                    // of zz[ra] compiled to a scratch round trip)
                     bwd7(L, inv, zz);
-                    sX[Mnodes[q] * 7 + ra] = pick7(zz, ra);
+                    if (ra == 0) {
+                        const int xo = Mnodes[q] * 7;
+#pragma unroll
+                        for (int c = 0; c < 7; c++) sX[xo + c] = zz[c];
+                    }
                 }
                 lds_barrier();
                 continue;
@@ -771,7 +775,11 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
                 for (int m = 0; m < 7; m++) zz[m] = __shfl(z, (lane < 63 ? 7 * g : 0) + m, 64);
                 if (on) {
                     bwd7(L, inv, zz);
-                    sX[Mnodes[q] * 7 + ra] = pick7(zz, ra);
+                    if (ra == 0) {
+                        const int xo = Mnodes[q] * 7;
+#pragma unroll
+                        for (int c = 0; c < 7; c++) sX[xo + c] = zz[c];
+                    }
                 }
             }
             lds_barrier();
@@ -828,6 +836,7 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
                 case 11: printf("gn_solve  K: barrier B     %8.2f us\n", us); break;
                 case 12: printf("gn_solve  R: factor (w0)  %8.2f us\n", us); break;
                 case 13: printf("gn_solve  R: schur (w0)   %8.2f us\n", us); break;
+                case 14: printf("gn_solve plan to LDS  %8.2f us\n", us); break;
                 default: printf("gn_solve retract     %8.2f us\n", us); break;
             }
         }

@@ -34,12 +34,14 @@ namespace m3s {
 namespace {
 constexpr int kGroups = 9;  // 7-lane groups per 64-lane workgroup (lane 63 idle)
 constexpr int kLd = 8;      // LDS row stride (doubles) of a staged 7x7 block
+static_assert(kSpInline == kGroups, "a target record inlines one contribution per 7-lane group");
 }  // namespace
 
-// Round targets: tg = (block, begin, end) with contributions tc3 = (v, code_r, code_s);
-// rtg = (pose r | -1, begin, end) with rc4 = (v, code_r, W id | -1, owner node | -1), where
-// code = block * 2 + transposed (the block holds the rows of the other pose).  r = -1 collects
-// the poses without fronts: only their L and y are stored.
+// Round targets: records (kSpRec, gn_kernels.h) {block, begin, end} with contributions
+// (v, code_r, code_s) for block targets, {pose r | -1, begin, end} with (v, code_r, W id | -1,
+// owner node | -1) for RHS targets; code = block * 2 + transposed (the block holds the rows of
+// the other pose).  r = -1 collects the poses without fronts: only their L and y are stored.
+// The first kSpInline contributions ride in the record, the rest come from tc3 / rc4.
 // COH: the all-rounds launch reads, in round r + 1, blocks other workgroups (other XCDs) wrote
 // in round r.  The per-XCD L2s are not coherent, so those A / b accesses are agent-coherent
 // (relaxed agent-scope atomics: sc1 loads and write-through stores) and the grid barrier needs
@@ -57,15 +59,17 @@ __device__ __forceinline__ void stA(double* p, double v) {
 
 template <bool COH>
 __device__ __forceinline__ void sp_round_target(
-    int gi, const int* __restrict__ tg, const int* __restrict__ tc3, int tbeg, int nbt,
-    const int* __restrict__ rtg, const int* __restrict__ rc4, int rbeg, double* __restrict__ A,
-    double* __restrict__ b, double* __restrict__ Lstore, double* __restrict__ W,
-    double* __restrict__ y, int* __restrict__ flags, double (*sR)[7 * kLd], double (*sS)[7 * kLd]) {
+    const int* __restrict__ rec, bool blk, const int* __restrict__ tc3, const int* __restrict__ rc4,
+    const int* __restrict__ done, double* __restrict__ A, double* __restrict__ b,
+    double* __restrict__ Lstore, double* __restrict__ W, double* __restrict__ y, int* __restrict__ flags,
+    double (*sR)[7 * kLd], double (*sS)[7 * kLd]) {
     const int lane = threadIdx.x;
-    const bool blk = gi < nbt;
-    const int* T_ = blk ? tg + 3 * (tbeg + gi) : rtg + 3 * (rbeg + gi - nbt);
-    const int tgt = T_[0], c0 = T_[1], c1 = T_[2];
     const int g = lane / 7, ra = lane - 7 * g;
+    // the record header, this group's inline contribution and (per launch) the flag: one round trip
+    const int4 hd = *reinterpret_cast<const int4*>(rec);
+    const int4 mine = *reinterpret_cast<const int4*>(rec + 4 + 4 * (g < kSpInline ? g : 0));
+    if (done && *done) return;
+    const int tgt = hd.x, c0 = hd.y, c1 = hd.z;
     // this lane's output: entry (er, ec) of the block, or row er of the RHS
     const int nact = tgt < 0 ? 0 : (blk ? 49 : 7);
     const int er = blk ? lane / 7 : lane, ec = lane % 7;
@@ -76,17 +80,12 @@ __device__ __forceinline__ void sp_round_target(
     for (int base = c0; base < c1; base += kGroups) {
         const int c = base + g;
         if (g < kGroups && c < c1) {
-            int v, cr, cs = 0, wid = -1, owner = -1;
-            if (blk) {
-                v = tc3[3 * c];
-                cr = tc3[3 * c + 1];
-                cs = tc3[3 * c + 2];
-            } else {
-                v = rc4[4 * c];
-                cr = rc4[4 * c + 1];
-                wid = rc4[4 * c + 2];
-                owner = rc4[4 * c + 3];
+            int4 C = mine;  // contributions past the inline ones: from the lists
+            if (base != c0) {
+                if (blk) C = make_int4(tc3[3 * c], tc3[3 * c + 1], tc3[3 * c + 2], 0);
+                else C = *reinterpret_cast<const int4*>(rc4 + 4 * c);
             }
+            const int v = C.x, cr = C.y, cs = blk ? C.z : 0, wid = blk ? -1 : C.z, owner = blk ? -1 : C.w;
             double L[28], inv[7], rr[7], rs[7];
             const double* Av = A + (int64_t)v * 49;
 #pragma unroll
@@ -123,10 +122,16 @@ __device__ __forceinline__ void sp_round_target(
 #pragma unroll
                     for (int m = 0; m < 7; m++) Wd[m] = wr[m];
                 }
-                if (owner >= 0) {
-                    y[(int64_t)v * 7 + ra] = b7::pick(ws, ra);
+                if (owner >= 0 && ra == 0) {
+                    // L, inv and y_v are the same in the group's 7 lanes: one lane stores them
+                    // (a per-lane pick by a runtime index compiled to a scratch round trip)
                     double* Ls = Lstore + (int64_t)owner * kLStoreRec;
-                    for (int k = ra; k < 35; k += 7) Ls[k] = k < 28 ? b7::pick(L, k) : b7::pick(inv, k - 28);
+#pragma unroll
+                    for (int m = 0; m < 7; m++) y[(int64_t)v * 7 + m] = ws[m];
+#pragma unroll
+                    for (int k = 0; k < 28; k++) Ls[k] = L[k];
+#pragma unroll
+                    for (int k = 0; k < 7; k++) Ls[28 + k] = inv[k];
                 }
             }
         }
@@ -148,14 +153,14 @@ __device__ __forceinline__ void sp_round_target(
 
 // One round per launch: workgroup = target (the flag is loaded beside the target record).
 __global__ __launch_bounds__(64) void sp_round_kernel(
-    const int* __restrict__ tg, const int* __restrict__ tc3, int tbeg, int nbt,
-    const int* __restrict__ rtg, const int* __restrict__ rc4, int rbeg, double* __restrict__ A,
-    double* __restrict__ b, double* __restrict__ Lstore, double* __restrict__ W,
-    double* __restrict__ y, int* __restrict__ flags) {
+    const int* __restrict__ inl, int ibeg, int nbt, const int* __restrict__ tc3,
+    const int* __restrict__ rc4, double* __restrict__ A, double* __restrict__ b,
+    double* __restrict__ Lstore, double* __restrict__ W, double* __restrict__ y,
+    int* __restrict__ flags) {
     __shared__ double sR[kGroups][7 * kLd];  // rows of W_rv, per contribution of the batch
     __shared__ double sS[kGroups][7 * kLd];  // block target: rows of W_sv; RHS target: y_v
-    if (flags[kFlagDone]) return;
-    sp_round_target<false>(blockIdx.x, tg, tc3, tbeg, nbt, rtg, rc4, rbeg, A, b, Lstore, W, y, flags, sR, sS);
+    sp_round_target<false>(inl + (int64_t)(ibeg + blockIdx.x) * kSpRec, (int)blockIdx.x < nbt, tc3, rc4,
+                           flags + kFlagDone, A, b, Lstore, W, y, flags, sR, sS);
 }
 
 // x_v = L_v^-T (y_v - sum_r W_rv^T x_r), one workgroup per pose of the round; 7-lane group g
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(64) void sp_back_kernel(
         part[g][ra] = s;
     }
     __syncthreads();
-    if (lane < 7) {
+    if (lane == 0) {
 #pragma unroll
         for (int m = 0; m < 7; m++) {
             double a = 0.0;
@@ -200,7 +205,8 @@ __global__ __launch_bounds__(64) void sp_back_kernel(
             z[m] -= a;
         }
         b7::bwd7(L, inv, z);
-        x[(int64_t)v * 7 + lane] = b7::pick(z, lane);
+#pragma unroll
+        for (int m = 0; m < 7; m++) x[(int64_t)v * 7 + m] = z[m];
     }
 }
 
@@ -294,8 +300,8 @@ __global__ __launch_bounds__(64) void sp_rounds_coop_kernel(SpCoopArgs a) {
         const int* R = a.rounds + 8 * rd;  // node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount
         const int tbeg = R[2], nbt = R[3], rbeg = R[4], nrt = R[5];
         for (int t = blockIdx.x; t < nbt + nrt; t += gridDim.x)
-            sp_round_target<true>(t, a.tg, a.tc3, tbeg, nbt, a.rtg, a.rc4, rbeg, a.A, a.b, a.Lstore, a.W, a.y,
-                                  a.flags, sR, sS);
+            sp_round_target<true>(a.inl + (int64_t)(tbeg + rbeg + t) * kSpRec, t < nbt, a.tc3, a.rc4, nullptr,
+                                  a.A, a.b, a.Lstore, a.W, a.y, a.flags, sR, sS);
         if (a.coop)
             cooperative_groups::this_grid().sync();
         else
@@ -315,12 +321,12 @@ __global__ __launch_bounds__(256) void sp_tail_scatter_kernel(const double* __re
 
 // ------------------------------------------------------------------ launchers
 
-hipError_t launch_sp_round(hipStream_t st, const int* tg, const int* tc3, int tbeg, int nbt,
-                           const int* rtg, const int* rc4, int rbeg, int nrt, double* A, double* b,
-                           double* Lstore, double* W, double* y, int* flags) {
+hipError_t launch_sp_round(hipStream_t st, const int* inl, int ibeg, int nbt, int nrt, const int* tc3,
+                           const int* rc4, double* A, double* b, double* Lstore, double* W, double* y,
+                           int* flags) {
     if (nbt + nrt <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sp_round_kernel, dim3(nbt + nrt), dim3(64), 0, st, tg, tc3, tbeg, nbt, rtg,
-                       rc4, rbeg, A, b, Lstore, W, y, flags);
+    hipLaunchKernelGGL(sp_round_kernel, dim3(nbt + nrt), dim3(64), 0, st, inl, ibeg, nbt, tc3, rc4, A, b,
+                       Lstore, W, y, flags);
     return hipGetLastError();
 }
 
