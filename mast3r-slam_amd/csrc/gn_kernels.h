@@ -146,7 +146,10 @@ hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* sl
                             int npose, int n, int npad, double* Hd, const int* flags);
 // Fused single-workgroup solve (gn_solve.hip)
 constexpr int kSolveThreads = 256;
-constexpr int kSolveRoundThreads = 512;  // rounds-only launch of the split solve
+#ifndef M3S_SOLVE_ROUND_THREADS
+#define M3S_SOLVE_ROUND_THREADS 256
+#endif
+constexpr int kSolveRoundThreads = M3S_SOLVE_ROUND_THREADS;  // rounds-only launch of the split solve (512: VGPR spills, cfg2 5 us slower)
 constexpr int kTailMax = 192;      // in-register dense tail: <= 192 unknowns (12 x 16-wide tiles)
 constexpr int kTailPoseMax = 27;   // = kTailMax / 7
 constexpr int kLStoreRec = 40;     // per eliminated pose: packed lower L (28) + 1/diag (7) + pad

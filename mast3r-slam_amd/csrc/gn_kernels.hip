@@ -318,23 +318,25 @@ __global__ __launch_bounds__(kPotrfThreads) void chol_potrf_kernel(double* __res
                 for (int p = 0; p <= i; p++) D[i][p] = A[c0 + i][c0 + p];
 #pragma unroll
             for (int p = 0; p < 8; p++) arow[p] = A[r][c0 + p];
-            double l[8][8];
+            // right-looking in registers: per pivot one rsq + one Newton step, then independent
+            // column scalings and trailing updates (dependent depth O(8), not O(8^2)); 1/l_pp is
+            // the pivot's rsqrt, so the row solve needs no reciprocal
+            double l[8][8], inv[8];
             bool bad = false;
 #pragma unroll
             for (int p = 0; p < 8; p++) {
-                double dpp = D[p][p];
-#pragma unroll
-                for (int q = 0; q < p; q++) dpp = fma(-l[p][q], l[p][q], dpp);
+                const double dpp = D[p][p];
                 if (dpp <= 0.0) bad = true;  // SimplicialLLT: fails iff a pivot <= 0
-                const double inv = rsqrt_f64(dpp);
-                l[p][p] = dpp * inv;
+                double y = __builtin_amdgcn_rsq(dpp);
+                y = y * fma(-0.5 * dpp * y, y, 1.5);
+                inv[p] = y;
+                l[p][p] = dpp * y;
 #pragma unroll
-                for (int i = p + 1; i < 8; i++) {
-                    double a_ = D[i][p];
+                for (int i = p + 1; i < 8; i++) l[i][p] = D[i][p] * y;
 #pragma unroll
-                    for (int q = 0; q < p; q++) a_ = fma(-l[i][q], l[p][q], a_);
-                    l[i][p] = a_ * inv;
-                }
+                for (int i = p + 1; i < 8; i++)
+#pragma unroll
+                    for (int j = p + 1; j <= i; j++) D[i][j] = fma(-l[i][p], l[j][p], D[i][j]);
             }
             if (r < c0 + 8) {
                 const int i = r - c0;
@@ -347,16 +349,15 @@ __global__ __launch_bounds__(kPotrfThreads) void chol_potrf_kernel(double* __res
                 }
                 if (bad && r == c0) fail = 1;
             } else {
-                double x[8];
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
-                    double a_ = arow[p];
+                    const double xp = arow[p] * inv[p];
+                    arow[p] = xp;
 #pragma unroll
-                    for (int q = 0; q < p; q++) a_ = fma(-x[q], l[p][q], a_);
-                    x[p] = a_ * rcp_f64(l[p][p]);
+                    for (int i = p + 1; i < 8; i++) arow[i] = fma(-xp, l[i][p], arow[i]);
                 }
 #pragma unroll
-                for (int p = 0; p < 8; p++) A[r][c0 + p] = x[p];
+                for (int p = 0; p < 8; p++) A[r][c0 + p] = arow[p];
             }
         }
         __syncthreads();
