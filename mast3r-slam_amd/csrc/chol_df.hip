@@ -1,0 +1,500 @@
+// chol_df.hip -- the dense core's tiled LL^T as ONE dataflow launch (replaces the Eigen
+// SimplicialLLT factorisation of gn_kernels.cu:132-153 for cores above the in-register size).
+//
+// The multi-launch tile Cholesky (gn_kernels.hip) costs three dependent launches per 64-column
+// panel (potrf, trsm, update: 48 for cfg4's 141-pose core), ~5 us of dispatch each, and its
+// potrf ran the rank-8 trailing updates and the inverse on VALU from LDS (~30 us per tile).
+// Here every lower tile (i, j) of the (npad + 64) x npad bordered matrix (the border row tile
+// nt carries the RHS, so the forward substitution rides along) is owned by one workgroup of a
+// single co-resident (cooperative) launch, processed left-looking:
+//   acc = A_ij;  for k < j: wait L_ik, L_jk final -> acc -= L_ik L_jk^T  (f64 MFMA)
+//   i == j: potrf of acc in LDS (8-column panels, per-lane 8x8 factor + row solve, MFMA rank-8
+//           trailing updates) and L_jj^-1 by doubling (8x8 blocks from the panel step, MFMA for
+//           the 16 and 32 stages) -> publish Linv_j
+//   i >  j: wait Linv_j -> L_ij = acc Linv_j^T (MFMA) -> publish L_ij
+// Readiness is a per-tile epoch word (ready[i * nt + j] == epoch: final in this launch).  The
+// per-XCD L2s are not coherent, so tile data crosses workgroups with agent-scope relaxed
+// atomics (sc1 loads, write-through stores), the flag with a release store after the data
+// stores completed.  Tiles are numbered column-major and a workgroup walks its tiles in order,
+// so every wait targets a tile earlier in some co-resident workgroup's list: no deadlock; the
+// spin is bounded (a missing producer fails the solve instead of hanging the GPU).
+// Numerics: the same LL^T in a different (left-looking) summation order; the solve is f64 and
+// not a bit-exact path (parity through poses, tests/test_gpu_gn.py).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "gn_kernels.h"
+
+namespace m3s {
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int T = kCholTile;  // 64
+constexpr int NT = 256;       // 4 waves: wave w owns 16-row block row w of a tile
+constexpr int LD = 73;        // LDS row stride (doubles) = 18 dwords mod 64 banks: conflict-free MFMA reads
+
+struct DfArgs {
+    double* Hd;
+    double* Linv;
+    int* ready;
+    int* flags;
+    int npad, nt, ntiles, epoch;  // ntiles = number of tasks (num_tasks)
+    long long* trace;  // diagnostics (tools/ubench_chol_df.hip): 4 timestamps per tile, else null
+};
+
+__device__ __forceinline__ void stamp(const DfArgs& a, int t, int slot) {
+    if (a.trace && threadIdx.x == 0) a.trace[4 * t + slot] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ double ld_coh(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coh(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// thread 0 waits until *f reaches the epoch (bounded; on timeout the solve is failed)
+__device__ __forceinline__ void wait_ready(const int* f, int epoch, int* flags) {
+    int spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 22)) {
+            flags[kFlagFail] = 1;
+            return;
+        }
+    }
+}
+
+// 64x64 tile (row stride ld) -> LDS [64][LD], agent-coherent loads (one 512-B row per wave step)
+__device__ __forceinline__ void load_tile_coh(double* S, const double* src, int64_t ld) {
+    const int tid = threadIdx.x;
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int id = tid + NT * q;
+        v[q] = ld_coh(src + (int64_t)(id >> 6) * ld + (id & 63));
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int id = tid + NT * q;
+        S[(id >> 6) * LD + (id & 63)] = v[q];
+    }
+}
+
+// acc[J] (16x16 block (w, J) of the tile) += sgn * X Y^T, X / Y: [64][LD] in LDS, K = 64.
+// Operand layout of v_mfma_f64_16x16x4f64: lane -> (row | col) = lane & 15, k = lane >> 4;
+// result acc[J][e] at row 16 w + (lane >> 4) + 4 e, column 16 J + (lane & 15).
+__device__ __forceinline__ void gemm_nt(const double* X, const double* Y, d4 acc[4], double sgn) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 15, kq = lane >> 4;
+    const double* xr = X + (16 * w + r) * LD + kq;
+    const double* yr = Y + r * LD + kq;
+#pragma unroll 4
+    for (int s = 0; s < 16; s++) {
+        const double a = sgn * xr[4 * s];
+        double b[4];
+#pragma unroll
+        for (int J = 0; J < 4; J++) b[J] = yr[16 * J * LD + 4 * s];
+#pragma unroll
+        for (int J = 0; J < 4; J++) acc[J] = mfma(a, b[J], acc[J]);
+    }
+}
+
+// D (16x16) = sum_{k < K} P[pr + i][pc + k] * Q[qr + k][qc + j]  (P, Q: [64][LD] in LDS)
+template <int K>
+__device__ __forceinline__ d4 block_mm(const double* P, int pr, int pc, const double* Q, int qr,
+                                       int qc) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 15, kq = lane >> 4;
+    d4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < K / 4; s++)
+        d = mfma(P[(pr + r) * LD + pc + 4 * s + kq], Q[(qr + 4 * s + kq) * LD + qc + r], d);
+    return d;
+}
+
+__device__ __forceinline__ void put_block(double* S, int r0, int c0, d4 d, double sgn) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int e = 0; e < 4; e++) S[(r0 + (lane >> 4) + 4 * e) * LD + c0 + (lane & 15)] = sgn * d[e];
+}
+
+// LL^T of the lower triangle of A (LDS) in place and Li = L^-1 (Li zeroed by the caller).
+// early: a ready word published once every wave's earlier stores landed (after the first panel
+// step, when they long have), so the caller's stores need no waiting on its critical path
+__device__ void potrf_inverse(double* A, double* Li, double* Tm, int* flags, long long* pt, int* early,
+                              int epoch) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, kq = lane >> 4;
+    auto pstamp = [&](int slot) {
+        if (pt && tid == 0) pt[slot] = (long long)__builtin_amdgcn_s_memrealtime();
+    };
+    pstamp(0);
+    for (int s = 0; s < T / 8; s++) {
+        const int c0 = 8 * s;
+        if (w == 0 && lane >= c0) {
+            // every lane factors the 8x8 diagonal block in registers (redundantly: no cross-lane
+            // traffic), right-looking, one rsq + one Newton step per pivot (1/l_pp is that
+            // rsqrt), then ONE forward substitution x = L_pp^-1 a per lane with no divergence:
+            // panel lanes solve their row (a = their row of A), diagonal-block lanes solve
+            // a = e_i, i.e. column i of L_pp^-1 (the doubling inverse's 8x8 blocks)
+            const int r = lane;
+            const bool dg = r < c0 + 8;
+            double D[8][8], x[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int p = 0; p <= i; p++) D[i][p] = A[(c0 + i) * LD + c0 + p];
+#pragma unroll
+            for (int p = 0; p < 8; p++) x[p] = dg ? (r - c0 == p ? 1.0 : 0.0) : A[r * LD + c0 + p];
+            double l[8][8], inv[8];
+            bool bad = false;
+#pragma unroll
+            for (int p = 0; p < 8; p++) {
+                const double dpp = D[p][p];
+                if (dpp <= 0.0) bad = true;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
+                double y = __builtin_amdgcn_rsq(dpp);
+                y = y * fma(-0.5 * dpp * y, y, 1.5);
+                inv[p] = y;
+                l[p][p] = dpp * y;
+#pragma unroll
+                for (int i = p + 1; i < 8; i++) l[i][p] = D[i][p] * y;
+#pragma unroll
+                for (int i = p + 1; i < 8; i++)
+#pragma unroll
+                    for (int j = p + 1; j <= i; j++) D[i][j] = fma(-l[i][p], l[j][p], D[i][j]);
+            }
+            if (bad && r == c0) flags[kFlagFail] = 1;
+#pragma unroll
+            for (int p = 0; p < 8; p++) {
+                const double xp = x[p] * inv[p];
+                x[p] = xp;
+#pragma unroll
+                for (int i = p + 1; i < 8; i++) x[i] = fma(-xp, l[i][p], x[i]);
+            }
+            if (dg) {
+                const int i = r - c0;
+#pragma unroll
+                for (int ii = 0; ii < 8; ii++)
+                    if (ii == i) {
+#pragma unroll
+                        for (int p = 0; p <= ii; p++) A[r * LD + c0 + p] = l[ii][p];
+                    }
+#pragma unroll
+                for (int m = 0; m < 8; m++) Li[(c0 + m) * LD + r] = x[m];
+            } else {
+#pragma unroll
+                for (int p = 0; p < 8; p++) A[r * LD + c0 + p] = x[p];
+            }
+        }
+        if (s == 0 && early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (s == 0 && early && tid == 0)
+            __hip_atomic_store(early, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        pstamp(1 + 2 * s);
+        // rank-8 update of the lower trailing block (rows, cols >= c0 + 8) by MFMA: wave w the
+        // 16x16 blocks (w, J), all operand loads before the MFMAs; only trailing lower entries
+        // are written back
+        const int lo = c0 + 8;
+        if (lo < T && 16 * w + 15 >= lo) {
+            const int Jlo = lo >> 4;
+            const double a0 = -A[(16 * w + r16) * LD + c0 + kq];
+            const double a1 = -A[(16 * w + r16) * LD + c0 + 4 + kq];
+            d4 c[4];
+            double b0[4], b1[4];
+#pragma unroll
+            for (int J = 0; J < 4; J++) {
+                if (J >= Jlo && J <= w) {
+#pragma unroll
+                    for (int e = 0; e < 4; e++) c[J][e] = A[(16 * w + kq + 4 * e) * LD + 16 * J + r16];
+                    b0[J] = A[(16 * J + r16) * LD + c0 + kq];
+                    b1[J] = A[(16 * J + r16) * LD + c0 + 4 + kq];
+                }
+            }
+#pragma unroll
+            for (int J = 0; J < 4; J++) {
+                if (J >= Jlo && J <= w) {
+                    c[J] = mfma(a0, b0[J], c[J]);
+                    c[J] = mfma(a1, b1[J], c[J]);
+                }
+            }
+#pragma unroll
+            for (int J = 0; J < 4; J++) {
+                if (J >= Jlo && J <= w) {
+                    const int col = 16 * J + r16;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int row = 16 * w + kq + 4 * e;
+                        if (col >= lo && col <= row) A[row * LD + col] = c[J][e];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        pstamp(2 + 2 * s);
+    }
+    // inverse by doubling, [[Ai,0],[B,Ci]]^-1 = [[Ai,0],[-Ci B Ai, Ci]]; the 8x8 diagonal
+    // inverses came from the panel steps.  Stage 8 on VALU (one output per thread):
+    {
+        const int p = 16 * (tid >> 6), a = (tid >> 3) & 7, b = tid & 7;
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++)
+            if (m >= b) acc = fma(A[(p + 8 + a) * LD + p + m], Li[(p + m) * LD + p + b], acc);
+        Tm[(p + 8 + a) * LD + p + b] = acc;
+        __syncthreads();
+        acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++)
+            if (m <= a) acc = fma(Li[(p + 8 + a) * LD + p + 8 + m], Tm[(p + 8 + m) * LD + p + b], acc);
+        Li[(p + 8 + a) * LD + p + b] = -acc;
+        __syncthreads();
+    }
+    // stage 16: pairs p = 0, 32 on waves 0, 1 (one 16x16 MFMA block each)
+    if (w < 2) {
+        const int p = 32 * w;
+        put_block(Tm, p + 16, p, block_mm<16>(A, p + 16, p, Li, p, p), 1.0);
+    }
+    __syncthreads();
+    if (w < 2) {
+        const int p = 32 * w;
+        put_block(Li, p + 16, p, block_mm<16>(Li, p + 16, p + 16, Tm, p + 16, p), -1.0);
+    }
+    __syncthreads();
+    // stage 32: the 32x32 off-diagonal block, one 16x16 block per wave
+    {
+        const int bi = w >> 1, bj = w & 1;
+        put_block(Tm, 32 + 16 * bi, 16 * bj, block_mm<32>(A, 32 + 16 * bi, 0, Li, 0, 16 * bj), 1.0);
+        __syncthreads();
+        put_block(Li, 32 + 16 * bi, 16 * bj, block_mm<32>(Li, 32 + 16 * bi, 32, Tm, 32, 16 * bj), -1.0);
+        __syncthreads();
+    }
+    pstamp(17);
+}
+
+// Workgroup 0 runs the whole diagonal chain C: for j = 0 .. nt-1
+//   L_{j,j-1} = P_s(j) Linv_{j-1}^T   (Linv_{j-1} still in LDS from the previous step)
+//   A'_jj     = P_d(j) - L_{j,j-1} L_{j,j-1}^T
+//   potrf(A'_jj) -> L_jj, Linv_j
+// where P_s(j) = A_{j,j-1} - sum_{k<=j-2} L_{j,k} L_{j-1,k}^T and P_d(j) = A_jj - sum_{k<=j-2}
+// L_{j,k} L_{j,k}^T are left-looking partial sums by helper task H_j (they depend on columns
+// <= j-2 only, so they are ready while C factors column j-1).  Between two potrfs only C's own
+// registers / LDS are on the critical path.  Helpers (the other workgroups) walk, column-major,
+// the regular tiles (i, j), i = j+2 .. nt (and (nt, nt-1)), then H_{j+2}, each left-looking:
+//   acc = A_ij - sum_{k<j} L_ik L_jk^T, wait Linv_j, L_ij = acc Linv_j^T.
+// C publishes L_{j,j-1} inside potrf(j) (after its first panel step) and Linv_j once its next
+// loads drained the store queue, so no store latency sits on the chain either.
+__host__ __device__ inline int col_tasks(int j, int nt) {
+    return (j < nt - 1 ? nt - j - 1 : 1) + (j + 2 <= nt - 1 ? 1 : 0);
+}
+__host__ __device__ inline int num_tasks(int nt) {  // helper tasks
+    int n = 0;
+    for (int j = 0; j < nt; j++) n += col_tasks(j, nt);
+    return n;
+}
+__host__ __device__ inline int hflag(int nt, int j) { return (nt + 1) * nt + j; }  // H_j ready word
+
+__device__ __forceinline__ void acc_to_lds(double* S, const d4 acc[4]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int J = 0; J < 4; J++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) S[(16 * w + (lane >> 4) + 4 * e) * LD + 16 * J + (lane & 15)] = acc[J][e];
+}
+template <bool COH>
+__device__ __forceinline__ void load_acc(d4 acc[4], const double* src, int64_t ld) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int J = 0; J < 4; J++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const double* p = src + (int64_t)(16 * w + (lane >> 4) + 4 * e) * ld + 16 * J + (lane & 15);
+            acc[J][e] = COH ? ld_coh(p) : *p;
+        }
+}
+__device__ __forceinline__ void store_acc_coh(double* dst, int64_t ld, const d4 acc[4]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int J = 0; J < 4; J++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) st_coh(dst + (int64_t)(16 * w + (lane >> 4) + 4 * e) * ld + 16 * J + (lane & 15), acc[J][e]);
+}
+// after this workgroup's write-through stores landed, set a ready word
+__device__ __forceinline__ void publish(const DfArgs& a, int idx) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(a.ready + idx, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
+    if (a.flags[kFlagDone]) return;  // written by earlier launches: all workgroups agree
+    __shared__ __attribute__((aligned(16))) double X[T * LD];
+    __shared__ __attribute__((aligned(16))) double Y[T * LD];
+    __shared__ __attribute__((aligned(16))) double Z[T * LD];
+    const int tid = threadIdx.x;
+    const int nt = a.nt;
+    const int64_t ld = a.npad;
+    auto tile = [&](int i, int j) { return a.Hd + (int64_t)i * T * ld + (int64_t)j * T; };
+    long long* ct = a.trace ? a.trace + 4 * a.ntiles + 32 : nullptr;  // C's per-step stamps
+    auto cstamp = [&](int j, int slot) {
+        if (ct && tid == 0) ct[4 * j + slot] = (long long)__builtin_amdgcn_s_memrealtime();
+    };
+    if (blockIdx.x == 0) {
+        // ---- the diagonal chain
+        for (int j = 0; j < nt; j++) {
+            d4 accd[4];
+            if (j >= 2) {
+                if (tid == 0) wait_ready(a.ready + hflag(nt, j), a.epoch, a.flags);
+                __syncthreads();
+            }
+            cstamp(j, 0);
+            if (j == 0) {
+                load_acc<false>(accd, tile(0, 0), ld);
+            } else {
+                d4 accs[4];
+                if (j == 1) {
+                    load_acc<false>(accs, tile(1, 0), ld);
+                    load_acc<false>(accd, tile(1, 1), ld);
+                } else {
+                    load_acc<true>(accs, tile(j, j - 1), ld);
+                    load_acc<true>(accd, tile(j, j), ld);
+                }
+                // the loads drained the queue: Linv_{j-1}'s stores have landed
+                publish(a, (j - 1) * nt + (j - 1));
+                acc_to_lds(X, accs);
+                __syncthreads();
+#pragma unroll
+                for (int J = 0; J < 4; J++) accs[J] = d4{0.0, 0.0, 0.0, 0.0};
+                gemm_nt(X, Y, accs, 1.0);  // L_{j,j-1}
+                store_acc_coh(tile(j, j - 1), ld, accs);
+                __syncthreads();
+                acc_to_lds(X, accs);
+                __syncthreads();
+                gemm_nt(X, X, accd, -1.0);
+                __syncthreads();
+            }
+            cstamp(j, 1);
+            acc_to_lds(X, accd);
+            for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;
+            __syncthreads();
+            potrf_inverse(X, Y, Z, a.flags, a.trace && j == 0 ? a.trace + 4 * a.ntiles : nullptr,
+                          j >= 1 ? a.ready + j * nt + (j - 1) : nullptr, a.epoch);
+            cstamp(j, 2);
+            double* Lk = a.Linv + (int64_t)j * T * T;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int id = tid + NT * q;
+                st_coh(Lk + id, Y[(id >> 6) * LD + (id & 63)]);
+            }
+        }
+        publish(a, (nt - 1) * nt + (nt - 1));
+        cstamp(nt - 1, 3);
+        return;
+    }
+    for (int t = blockIdx.x - 1; t < a.ntiles; t += gridDim.x - 1) {
+        int j = 0, rem = t;
+        while (rem >= col_tasks(j, nt)) {
+            rem -= col_tasks(j, nt);
+            j++;
+        }
+        stamp(a, t, 0);
+        const int nreg = j < nt - 1 ? nt - j - 1 : 1;
+        if (rem == nreg) {
+            // ---- H_{j+2}: partial sums of tiles (h, h-1), (h, h) over k <= j = h-2
+            const int h = j + 2;
+            d4 accs[4], accd[4];
+            load_acc<false>(accs, tile(h, h - 1), ld);
+            load_acc<false>(accd, tile(h, h), ld);
+            for (int k = 0; k <= j; k++) {
+                if (tid == 0) {
+                    wait_ready(a.ready + h * nt + k, a.epoch, a.flags);
+                    wait_ready(a.ready + (h - 1) * nt + k, a.epoch, a.flags);
+                }
+                __syncthreads();
+                load_tile_coh(X, tile(h, k), ld);
+                load_tile_coh(Y, tile(h - 1, k), ld);
+                __syncthreads();
+                gemm_nt(X, Y, accs, -1.0);
+                gemm_nt(X, X, accd, -1.0);
+                __syncthreads();
+            }
+            stamp(a, t, 1);
+            store_acc_coh(tile(h, h - 1), ld, accs);
+            store_acc_coh(tile(h, h), ld, accd);
+            publish(a, hflag(nt, h));
+            stamp(a, t, 3);
+        } else {
+            // ---- regular tile (i, j), left-looking
+            const int i = j < nt - 1 ? j + 2 + rem : nt;
+            d4 acc[4];
+            load_acc<false>(acc, tile(i, j), ld);
+            for (int k = 0; k < j; k++) {
+                if (tid == 0) {
+                    wait_ready(a.ready + i * nt + k, a.epoch, a.flags);
+                    wait_ready(a.ready + j * nt + k, a.epoch, a.flags);
+                }
+                __syncthreads();
+                load_tile_coh(X, tile(i, k), ld);
+                load_tile_coh(Y, tile(j, k), ld);
+                __syncthreads();
+                gemm_nt(X, Y, acc, -1.0);
+                __syncthreads();
+            }
+            stamp(a, t, 1);
+            acc_to_lds(X, acc);
+            if (tid == 0) wait_ready(a.ready + j * nt + j, a.epoch, a.flags);
+            __syncthreads();
+            stamp(a, t, 2);
+            load_tile_coh(Y, a.Linv + (int64_t)j * T * T, T);
+            __syncthreads();
+#pragma unroll
+            for (int J = 0; J < 4; J++) acc[J] = d4{0.0, 0.0, 0.0, 0.0};
+            gemm_nt(X, Y, acc, 1.0);
+            store_acc_coh(tile(i, j), ld, acc);
+            publish(a, i * nt + j);
+            stamp(a, t, 3);
+        }
+    }
+}
+
+}  // namespace
+
+size_t chol_ready_bytes(int npad) {
+    const int nt = npad / T;
+    return sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + (size_t)nt);
+}
+
+hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
+                                int epoch, int* flags) {
+    static int maxg = 0;
+    if (maxg == 0) {
+        int dev = 0, ncu = 0, per = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)chol_df_kernel, NT, 0);
+        if (e != hipSuccess) return e;
+        maxg = ncu * per;
+        if (maxg <= 0) return hipErrorLaunchFailure;
+    }
+    DfArgs a{};
+    a.Hd = Hd;
+    a.Linv = Linv;
+    a.ready = ready;
+    a.flags = flags;
+    a.npad = npad;
+    a.nt = npad / T;
+    a.ntiles = num_tasks(a.nt);
+    a.epoch = epoch;
+    const int grid = 1 + a.ntiles < maxg ? 1 + a.ntiles : maxg;  // workgroup 0 = the diagonal chain
+    void* kargs[] = {&a};
+    return hipLaunchCooperativeKernel((const void*)chol_df_kernel, dim3(grid), dim3(NT), kargs, 0, st);
+}
+
+}  // namespace m3s

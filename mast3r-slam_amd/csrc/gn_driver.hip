@@ -685,7 +685,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     sp.o_xd = take(sizeof(double) * (size_t)std::max(sp.npad_tail, 1));
     if (sp.npad_tail > 0) {
         sp.o_dense = take(sizeof(double) * (size_t)(sp.npad_tail + kCholTile) * sp.npad_tail);
-        sp.o_linv = take(sizeof(double) * (size_t)sp.npad_tail * kCholTile);
+        sp.o_linv = take(chol_linv_bytes(sp.npad_tail));
     }
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
     // the plan integers in one array (layout: SparsePlan), the rounds after tmap
@@ -706,6 +706,9 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     }
     sp.o_int = take(sizeof(int) * std::max<size_t>(n, 1));
     M3S_HIP_CHECK(hipMallocAsync((void**)&sp.dbuf, off, st));
+    if (sp.npad_tail > 0)  // the dataflow factor's ready words start below every epoch
+        M3S_HIP_CHECK(hipMemsetAsync(chol_ready_ptr(sp.dptr<double>(sp.o_linv), sp.npad_tail), 0,
+                                     chol_ready_bytes(sp.npad_tail), st));
     if (n > 0) {
         int* h = reinterpret_cast<int*>(g_stage_out.get(sizeof(int) * n));
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
@@ -786,6 +789,7 @@ struct Ctx {
     // tile inverses and the (npose x npose) slot table, one stream-ordered allocation
     char* dyn = nullptr;
     size_t o_dense = 0, o_linv = 0, o_slot = 0;
+    int chol_epoch = 0;  // dataflow factorisations enqueued in this call (chol_df.hip ready words)
     template <typename T>
     T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
     template <typename T>
@@ -798,9 +802,10 @@ struct Ctx {
             return o;
         };
         o_dense = take(sizeof(double) * (size_t)(npad + kCholTile) * npad);
-        o_linv = take(sizeof(double) * (size_t)npad * kCholTile);
+        o_linv = take(chol_linv_bytes(npad));
         o_slot = take(sizeof(int) * (size_t)npose * npose);
         M3S_HIP_CHECK(hipMallocAsync((void**)&dyn, off, st));
+        M3S_HIP_CHECK(hipMemsetAsync(chol_ready_ptr(dyn_at<double>(o_linv), npad), 0, chol_ready_bytes(npad), st));
         return M3S_OK;
     }
     Ctx() = default;
@@ -1043,7 +1048,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     if (!c.sp.enabled) {
         M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.dyn_at<int>(c.o_slot), c.plan.nblk,
                                    npose, 7 * npose, L.npad, c.dyn_at<double>(c.o_dense),
-                                   c.dyn_at<double>(c.o_linv), c.at<double>(L.x), flags));
+                                   c.dyn_at<double>(c.o_linv), c.at<double>(L.x), flags, ++c.chol_epoch));
         return M3S_OK;
     }
     SparsePlan& sp = c.sp;
@@ -1173,7 +1178,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     }
     M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
                                  sp.npad_tail, sp.dptr<double>(sp.o_dense), sp.dptr<double>(sp.o_linv),
-                                 sp.dptr<double>(sp.o_xd), x, flags));
+                                 sp.dptr<double>(sp.o_xd), x, flags, ++c.chol_epoch));
     for (auto it = sp.rounds.rbegin(); it != sp.rounds.rend(); ++it)
         M3S_HIP_CHECK(launch_sp_back(c.st, it->nnodes, sp.iptr(sp.i_nodes), sp.iptr(sp.i_fptr),
                                      sp.iptr(sp.i_fronts), it->node_begin, Ls, W, y, x, flags));

@@ -111,10 +111,21 @@ hipError_t launch_assemble(hipStream_t st, const double* edgeblk, const int* blk
                            int nblocks, int npose, int bpad, double* out, const int* flags);
 hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                         int npose, int n, int npad, double* Hd, double* Linv, double* x,
-                        int* flags);
+                        int* flags, int epoch);
 constexpr int kMaxNpad = 8192;  // dense solve limit: N <= 1171 keyframes
+// Linv region: the npad / 64 tile inverses (64 x 64 f64 each), then the dataflow factor's
+// per-tile ready words (chol_df.hip; zeroed once per call, epoch = 1, 2, ... per factorisation)
+size_t chol_ready_bytes(int npad);
+inline size_t chol_linv_bytes(int npad) {
+    return sizeof(double) * (size_t)npad * kCholTile + chol_ready_bytes(npad);
+}
+inline int* chol_ready_ptr(double* Linv, int npad) {
+    return reinterpret_cast<int*>(Linv + (size_t)npad * kCholTile);
+}
+hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
+                                int epoch, int* flags);
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
-                                     double* x, int* flags);
+                                     double* x, int* flags, int epoch);
 // multi-launch block-sparse elimination (gn_sparse.hip): one launch per round
 // every elimination round (+ optionally the hybrid core's dense fill) in one cooperative launch
 // Per round target, one record of kSpRec ints: {target, c0, c1, 0} then the first kSpInline
@@ -141,7 +152,7 @@ hipError_t launch_sp_tail_fill(hipStream_t st, const double* A, const double* b,
                                const int* tail, int ntail, int npad, double* Hd, const int* flags);
 hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, const int* tmap,
                           const int* tail, int ntail, int npad, double* Hd, double* Linv,
-                          double* xd, double* x, int* flags);
+                          double* xd, double* x, int* flags, int epoch);
 hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                             int npose, int n, int npad, double* Hd, const int* flags);
 // Fused single-workgroup solve (gn_solve.hip)

@@ -624,18 +624,27 @@ hipError_t launch_assemble(hipStream_t st, const double* edgeblk, const int* blk
 }
 
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
-                                     double* x, int* flags) {
+                                     double* x, int* flags, int epoch) {
     const int nt = npad / T;
-    for (int k = 0; k < nt; k++) {
-        hipLaunchKernelGGL(chol_potrf_kernel, dim3(1), dim3(kPotrfThreads), 0, st, Hd, npad, k, Linv,
-                           flags);
-        hipLaunchKernelGGL(chol_trsm_kernel, dim3(nt - k), dim3(kGemmThreads), 0, st, Hd, npad, k, Linv,
-                           flags);
-        int nupd = 0;
-        for (int j = k + 1; j < nt; j++) nupd += nt - j + 1;
-        if (nupd > 0)
-            hipLaunchKernelGGL(chol_update_kernel, dim3(nupd), dim3(kGemmThreads), 0, st, Hd, npad, nt, k,
+    // M3S_CHOL_DF=1 (default): the whole LL^T as one dataflow launch (chol_df.hip); 0: one
+    // potrf / trsm / update launch triple per panel
+    const char* df_env = getenv("M3S_CHOL_DF");
+    const int df = df_env ? atoi(df_env) : 1;
+    if (df) {
+        hipError_t e = launch_chol_dataflow(st, npad, Hd, Linv, chol_ready_ptr(Linv, npad), epoch, flags);
+        if (e != hipSuccess) return e;
+    } else {
+        for (int k = 0; k < nt; k++) {
+            hipLaunchKernelGGL(chol_potrf_kernel, dim3(1), dim3(kPotrfThreads), 0, st, Hd, npad, k, Linv,
                                flags);
+            hipLaunchKernelGGL(chol_trsm_kernel, dim3(nt - k), dim3(kGemmThreads), 0, st, Hd, npad, k,
+                               Linv, flags);
+            int nupd = 0;
+            for (int j = k + 1; j < nt; j++) nupd += nt - j + 1;
+            if (nupd > 0)
+                hipLaunchKernelGGL(chol_update_kernel, dim3(nupd), dim3(kGemmThreads), 0, st, Hd, npad, nt,
+                                   k, flags);
+        }
     }
     hipLaunchKernelGGL(chol_backsolve_kernel, dim3(1), dim3(kBackThreads), 0, st, Hd, npad, Linv,
                        x, flags);
@@ -644,14 +653,14 @@ hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, doubl
 
 hipError_t launch_solve(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                         int npose, int n, int npad, double* Hd, double* Linv, double* x,
-                        int* flags) {
+                        int* flags, int epoch) {
     const int64_t total = (int64_t)(npad + kCholTile) * npad;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     hipLaunchKernelGGL(gn_fill_dense_kernel, dim3(blocks), dim3(256), 0, st, compact, slotmap,
                        nblk, npose, n, npad, Hd, flags);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_dense_factor_solve(st, npad, Hd, Linv, x, flags);
+    return launch_dense_factor_solve(st, npad, Hd, Linv, x, flags, epoch);
 }
 
 hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,

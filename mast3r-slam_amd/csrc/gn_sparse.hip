@@ -372,11 +372,11 @@ hipError_t launch_sp_tail_fill(hipStream_t st, const double* A, const double* b,
 
 hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, const int* tmap,
                           const int* tail, int ntail, int npad, double* Hd, double* Linv,
-                          double* xd, double* x, int* flags) {
+                          double* xd, double* x, int* flags, int epoch) {
     if (ntail <= 0) return hipSuccess;
     hipError_t e = launch_sp_tail_fill(st, A, b, tmap, tail, ntail, npad, Hd, flags);
     if (e != hipSuccess) return e;
-    e = launch_dense_factor_solve(st, npad, Hd, Linv, xd, flags);
+    e = launch_dense_factor_solve(st, npad, Hd, Linv, xd, flags, epoch);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sp_tail_scatter_kernel, dim3((ntail * 7 + 255) / 256), dim3(256), 0, st, xd,
                        tail, ntail, x, flags);

@@ -399,3 +399,35 @@ def test_cfg4_full_size_one_and_ten_iterations(backend, oracle):
     T10, _, it = _run_oracle(oracle, g, "rays", 10)
     assert it == 10
     assert _rel(Ta, T10) < 1e-5, _rel(Ta, T10)
+
+
+@pytest.mark.parametrize("topo", ["cfg4", "cfg3", "clique28", "pair"])
+@pytest.mark.parametrize("dense", [True, False])
+def test_dataflow_factor_matches_multilaunch_factor(backend, monkeypatch, topo, dense):
+    """The one-launch dataflow tile LL^T (chol_df.hip, default) against the per-panel
+    potrf / trsm / update launches (M3S_CHOL_DF=0) on the same systems, 2 GN iterations: the
+    same factorisation in a left- instead of right-looking summation order -> updates agree to
+    ~1e-9.  dense=True factors the whole system (cfg4: 255 poses, 1785 unknowns in 28 tile
+    columns = 434 tiles, more than one per workgroup); False the sparse solver's dense core
+    (cfg4: 141 poses, 16 tile columns); clique28 a 189-unknown core (3 tile columns); pair one
+    tile column."""
+    if topo == "clique28":
+        N = 29
+        und = [(a, b) for a in range(N) for b in range(a + 1, N)]
+        g = synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
+    elif topo == "pair":
+        g = synth.make_graph(dict(N=2, E=1), H=24, W=32, seed=3, edges_only=[(0, 1)])
+    else:
+        g = synth.make_graph(topo, H=24, W=32, seed=6)
+    if dense:
+        monkeypatch.setenv("M3S_SOLVER_DENSE", "1")
+    else:
+        monkeypatch.setenv("M3S_SOLVER", "2")
+    monkeypatch.setenv("M3S_CHOL_DF", "0")
+    T_m, dx_m = _run_gpu(backend, g, "rays", 2)
+    monkeypatch.setenv("M3S_CHOL_DF", "1")
+    T_f, dx_f = _run_gpu(backend, g, "rays", 2)
+    T_f2, _ = _run_gpu(backend, g, "rays", 2)
+    assert np.isfinite(dx_f).all() and np.array_equal(T_f, T_f2)  # deterministic
+    assert np.abs(dx_f - dx_m).max() <= 1e-8 * max(np.abs(dx_m).max(), 1e-6)
+    assert _rel(T_f, T_m) < 1e-6
