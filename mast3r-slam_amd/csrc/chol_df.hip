@@ -91,19 +91,24 @@ __device__ __forceinline__ void load_tile_coh(double* S, const double* src, int6
 // acc[J] (16x16 block (w, J) of the tile) += sgn * X Y^T, X / Y: [64][LD] in LDS, K = 64.
 // Operand layout of v_mfma_f64_16x16x4f64: lane -> (row | col) = lane & 15, k = lane >> 4;
 // result acc[J][e] at row 16 w + (lane >> 4) + 4 e, column 16 J + (lane & 15).
+// TRI: Y is lower triangular (a tile inverse), so block column J needs k < 16 J + 16 only:
+// 40 instead of 64 MFMAs per wave on the trsm's chain.
+template <bool TRI = false>
 __device__ __forceinline__ void gemm_nt(const double* X, const double* Y, d4 acc[4], double sgn) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 15, kq = lane >> 4;
     const double* xr = X + (16 * w + r) * LD + kq;
     const double* yr = Y + r * LD + kq;
-#pragma unroll 4
+#pragma unroll
     for (int s = 0; s < 16; s++) {
         const double a = sgn * xr[4 * s];
         double b[4];
 #pragma unroll
-        for (int J = 0; J < 4; J++) b[J] = yr[16 * J * LD + 4 * s];
+        for (int J = 0; J < 4; J++)
+            if (!TRI || s <= 4 * J + 3) b[J] = yr[16 * J * LD + 4 * s];
 #pragma unroll
-        for (int J = 0; J < 4; J++) acc[J] = mfma(a, b[J], acc[J]);
+        for (int J = 0; J < 4; J++)
+            if (!TRI || s <= 4 * J + 3) acc[J] = mfma(a, b[J], acc[J]);
     }
 }
 
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 __syncthreads();
 #pragma unroll
                 for (int J = 0; J < 4; J++) accs[J] = d4{0.0, 0.0, 0.0, 0.0};
-                gemm_nt(X, Y, accs, 1.0);  // L_{j,j-1}
+                gemm_nt<true>(X, Y, accs, 1.0);  // L_{j,j-1}
                 store_acc_coh(tile(j, j - 1), ld, accs);
                 __syncthreads();
                 acc_to_lds(X, accs);
@@ -456,7 +461,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             __syncthreads();
 #pragma unroll
             for (int J = 0; J < 4; J++) acc[J] = d4{0.0, 0.0, 0.0, 0.0};
-            gemm_nt(X, Y, acc, 1.0);
+            gemm_nt<true>(X, Y, acc, 1.0);
             store_acc_coh(tile(i, j), ld, acc);
             publish(a, i * nt + j);
             stamp(a, t, 3);
