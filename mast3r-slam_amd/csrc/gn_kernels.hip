@@ -40,10 +40,26 @@ __global__ __launch_bounds__(64) void gn_edge_reduce_kernel(const float* __restr
     __shared__ double g[7];
     __shared__ double A[7][7];
     __shared__ double AM[7][7];
+    // the pose loads (ii -> Twc, two dependent trips) are issued first, so they overlap the
+    // chunk-partial loads instead of following them
+    float Ti[8];
+    if (tid < 3) {
+        const float* Tp = Twc + (int64_t)ii_loc[e] * 8;
+#pragma unroll
+        for (int k = 0; k < 8; k++) Ti[k] = Tp[k];
+    }
     if (tid < kNacc) {
         const float* p = partials + (int64_t)e * nchunks * kNaccPad + tid;
         double s = 0.0;
-        for (int c = 0; c < nchunks; c++) s += (double)p[(int64_t)c * kNaccPad];
+        int c = 0;
+        for (; c + 8 <= nchunks; c += 8) {  // 8 loads in flight, summed in chunk order
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = p[(int64_t)(c + u) * kNaccPad];
+#pragma unroll
+            for (int u = 0; u < 8; u++) s += (double)v[u];
+        }
+        for (; c < nchunks; c++) s += (double)p[(int64_t)c * kNaccPad];
         if (tid < 28) {
             int a = 0, r = tid;
             while (r >= 7 - a) { r -= 7 - a; a++; }
@@ -58,7 +74,6 @@ __global__ __launch_bounds__(64) void gn_edge_reduce_kernel(const float* __restr
     __syncthreads();
     if (tid < 3) {
         // column tid of the adjoint map of apply_Sim3_adj_inv (gn_kernels.cu:277-297)
-        const float* Ti = Twc + (int64_t)ii_loc[e] * 8;
         const double t0 = Ti[0], t1 = Ti[1], t2 = Ti[2];
         const double qx = Ti[3], qy = Ti[4], qz = Ti[5], qw = Ti[6];
         const double s_inv = 1.0 / (double)Ti[7];
@@ -122,11 +137,20 @@ __global__ __launch_bounds__(64) void gn_compact_kernel(
     const int tid = threadIdx.x;
     if (s < nblk) {
         if (tid < 28) {
+            // entries in batches of 8 (codes, then values in flight together), summed in entry
+            // order as before
             double acc = 0.0;
-            for (int k = blk_ptr[s]; k < blk_ptr[s + 1]; k++) {
-                const int code = blk_ent[k];
-                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + tid];
-                acc += (code & 1) ? -v : v;
+            const int k1 = blk_ptr[s + 1];
+            for (int k = blk_ptr[s]; k < k1; k += 8) {
+                int code[8];
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) code[u] = k + u < k1 ? blk_ent[k + u] : 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = k + u < k1 ? edgeblk[(int64_t)(code[u] >> 1) * kEdgeBlk + tid] : 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (k + u < k1) acc += (code[u] & 1) ? -v[u] : v[u];
             }
             compact[(int64_t)s * 28 + tid] = acc;
         }
@@ -134,10 +158,17 @@ __global__ __launch_bounds__(64) void gn_compact_kernel(
         const int p = s - nblk;
         if (p < npose && tid < 7) {
             double acc = 0.0;
-            for (int k = grad_ptr[p]; k < grad_ptr[p + 1]; k++) {
-                const int code = grad_ent[k];
-                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + 28 + tid];
-                acc += (code & 1) ? -v : v;
+            const int k1 = grad_ptr[p + 1];
+            for (int k = grad_ptr[p]; k < k1; k += 8) {
+                int code[8];
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) code[u] = k + u < k1 ? grad_ent[k + u] : 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = k + u < k1 ? edgeblk[(int64_t)(code[u] >> 1) * kEdgeBlk + 28 + tid] : 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (k + u < k1) acc += (code[u] & 1) ? -v[u] : v[u];
             }
             compact[(int64_t)nblk * 28 + p * 7 + tid] = acc;
         }
@@ -158,11 +189,20 @@ __global__ __launch_bounds__(64) void gn_assemble_kernel(
     const int tid = threadIdx.x;
     if (s < nblk) {
         if (tid < 28) {
+            // entries in batches of 8 (codes, then values in flight together), summed in entry
+            // order as before
             double acc = 0.0;
-            for (int k = blk_ptr[s]; k < blk_ptr[s + 1]; k++) {
-                const int code = blk_ent[k];
-                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + tid];
-                acc += (code & 1) ? -v : v;
+            const int k1 = blk_ptr[s + 1];
+            for (int k = blk_ptr[s]; k < k1; k += 8) {
+                int code[8];
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) code[u] = k + u < k1 ? blk_ent[k + u] : 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = k + u < k1 ? edgeblk[(int64_t)(code[u] >> 1) * kEdgeBlk + tid] : 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (k + u < k1) acc += (code[u] & 1) ? -v[u] : v[u];
             }
             int a = 0, r = tid;
             while (r >= 7 - a) {
@@ -180,10 +220,17 @@ __global__ __launch_bounds__(64) void gn_assemble_kernel(
         const int p = s - nblocks;
         if (p < npose && tid < 7) {
             double acc = 0.0;
-            for (int k = grad_ptr[p]; k < grad_ptr[p + 1]; k++) {
-                const int code = grad_ent[k];
-                const double v = edgeblk[(int64_t)(code >> 1) * kEdgeBlk + 28 + tid];
-                acc += (code & 1) ? -v : v;
+            const int k1 = grad_ptr[p + 1];
+            for (int k = grad_ptr[p]; k < k1; k += 8) {
+                int code[8];
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) code[u] = k + u < k1 ? grad_ent[k + u] : 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = k + u < k1 ? edgeblk[(int64_t)(code[u] >> 1) * kEdgeBlk + 28 + tid] : 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (k + u < k1) acc += (code[u] & 1) ? -v[u] : v[u];
             }
             out[p * 7 + tid] = acc;
         }

@@ -431,3 +431,25 @@ def test_dataflow_factor_matches_multilaunch_factor(backend, monkeypatch, topo, 
     assert np.isfinite(dx_f).all() and np.array_equal(T_f, T_f2)  # deterministic
     assert np.abs(dx_f - dx_m).max() <= 1e-8 * max(np.abs(dx_m).max(), 1e-6)
     assert _rel(T_f, T_m) < 1e-6
+
+
+@pytest.mark.parametrize("chol_df", ["1", "0"])
+@pytest.mark.parametrize("dense", [True, False])
+def test_singular_core_fails_through_tile_factor(backend, monkeypatch, dense, chol_df):
+    """SimplicialLLT's failure semantics (pivot <= 0 => dx = 0, loop exits;
+    gn_kernels.cu:142-150, 1219-1222) through the tiled dense factorisations: a 29-keyframe
+    clique (no low-degree elimination set: its 196-unknown core goes to the tile LL^T) with no
+    valid observation.  dense=True factors the whole system, False the sparse solver's core;
+    chol_df selects the dataflow launch or the per-panel launches."""
+    N = 29
+    und = [(a, b) for a in range(N) for b in range(a + 1, N)]
+    g = synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
+    g.valid[:] = False
+    if dense:
+        monkeypatch.setenv("M3S_SOLVER_DENSE", "1")
+    else:
+        monkeypatch.setenv("M3S_SOLVER", "2")
+    monkeypatch.setenv("M3S_CHOL_DF", chol_df)
+    T_g, dx_g = _run_gpu(backend, g, "rays", 10, delta=1e-8)
+    assert np.array_equal(T_g, g.Twc.numpy())
+    assert np.all(dx_g == 0)
