@@ -131,119 +131,120 @@ __device__ __forceinline__ void put_block(double* S, int r0, int c0, d4 d, doubl
     for (int e = 0; e < 4; e++) S[(r0 + (lane >> 4) + 4 * e) * LD + c0 + (lane & 15)] = sgn * d[e];
 }
 
+// Panel step of the tile LL^T, run by wave 0 (lanes >= c0): columns c0 .. c0+7 of rows >= c0
+// are final after it, and the diagonal lanes have written the 8x8 inverse block into Li.
+__device__ __forceinline__ void panel_factor(double* A, double* Li, int c0, int* flags) {
+    const int lane = threadIdx.x & 63;
+    if (lane >= c0) {
+        // every lane factors the 8x8 diagonal block in registers (redundantly: no cross-lane
+        // traffic), right-looking, one rsq + one Newton step per pivot (1/l_pp is that
+        // rsqrt), then ONE forward substitution x = L_pp^-1 a per lane with no divergence:
+        // panel lanes solve their row (a = their row of A), diagonal-block lanes solve
+        // a = e_i, i.e. column i of L_pp^-1 (the doubling inverse's 8x8 blocks)
+        const int r = lane;
+        const bool dg = r < c0 + 8;
+        double D[8][8], x[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int p = 0; p <= i; p++) D[i][p] = A[(c0 + i) * LD + c0 + p];
+#pragma unroll
+        for (int p = 0; p < 8; p++) x[p] = dg ? (r - c0 == p ? 1.0 : 0.0) : A[r * LD + c0 + p];
+        double l[8][8], inv[8];
+        bool bad = false;
+#pragma unroll
+        for (int p = 0; p < 8; p++) {
+            const double dpp = D[p][p];
+            if (dpp <= 0.0) bad = true;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
+            double y = __builtin_amdgcn_rsq(dpp);
+            y = y * fma(-0.5 * dpp * y, y, 1.5);
+            inv[p] = y;
+            l[p][p] = dpp * y;
+#pragma unroll
+            for (int i = p + 1; i < 8; i++) l[i][p] = D[i][p] * y;
+#pragma unroll
+            for (int i = p + 1; i < 8; i++)
+#pragma unroll
+                for (int j = p + 1; j <= i; j++) D[i][j] = fma(-l[i][p], l[j][p], D[i][j]);
+        }
+        if (bad && r == c0) flags[kFlagFail] = 1;
+#pragma unroll
+        for (int p = 0; p < 8; p++) {
+            const double xp = x[p] * inv[p];
+            x[p] = xp;
+#pragma unroll
+            for (int i = p + 1; i < 8; i++) x[i] = fma(-xp, l[i][p], x[i]);
+        }
+        if (dg) {
+            const int i = r - c0;
+#pragma unroll
+            for (int ii = 0; ii < 8; ii++)
+                if (ii == i) {
+#pragma unroll
+                    for (int p = 0; p <= ii; p++) A[r * LD + c0 + p] = l[ii][p];
+                }
+#pragma unroll
+            for (int m = 0; m < 8; m++) Li[(c0 + m) * LD + r] = x[m];
+        } else {
+#pragma unroll
+            for (int p = 0; p < 8; p++) A[r * LD + c0 + p] = x[p];
+        }
+    }
+}
+
+// A[I-block rows][J-block cols] -= P_I P_J^T with the panel at columns c0 .. c0+7 (MFMA, two
+// K = 4 steps); only trailing lower entries (row >= col >= c0 + 8) are written back.
+__device__ __forceinline__ void trail_block(double* A, int c0, int I, int J) {
+    const int lane = threadIdx.x & 63;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int lo = c0 + 8;
+    d4 c;
+#pragma unroll
+    for (int e = 0; e < 4; e++) c[e] = A[(16 * I + kq + 4 * e) * LD + 16 * J + r16];
+    const double a0 = -A[(16 * I + r16) * LD + c0 + kq], a1 = -A[(16 * I + r16) * LD + c0 + 4 + kq];
+    const double b0 = A[(16 * J + r16) * LD + c0 + kq], b1 = A[(16 * J + r16) * LD + c0 + 4 + kq];
+    c = mfma(a0, b0, c);
+    c = mfma(a1, b1, c);
+    const int col = 16 * J + r16;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const int row = 16 * I + kq + 4 * e;
+        if (col >= lo && col <= row) A[row * LD + col] = c[e];
+    }
+}
+
 // LL^T of the lower triangle of A (LDS) in place and Li = L^-1 (Li zeroed by the caller).
+// Look-ahead: in step s wave 0 applies panel s to the block column holding panel s+1 and
+// factors panel s+1 right away, while waves 1-3 apply panel s to the block columns right of it
+// (one barrier per step; the single-wave panel factor overlaps the rest of the update).
 // early: a ready word published once every wave's earlier stores landed (after the first panel
 // step, when they long have), so the caller's stores need no waiting on its critical path
 __device__ void potrf_inverse(double* A, double* Li, double* Tm, int* flags, long long* pt, int* early,
                               int epoch) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r16 = lane & 15, kq = lane >> 4;
+    const int tid = threadIdx.x, w = tid >> 6;
     auto pstamp = [&](int slot) {
         if (pt && tid == 0) pt[slot] = (long long)__builtin_amdgcn_s_memrealtime();
     };
     pstamp(0);
-    for (int s = 0; s < T / 8; s++) {
+    if (w == 0) panel_factor(A, Li, 0, flags);
+    if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (early && tid == 0) __hip_atomic_store(early, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    pstamp(1);
+    for (int s = 0; s + 1 < T / 8; s++) {
         const int c0 = 8 * s;
-        if (w == 0 && lane >= c0) {
-            // every lane factors the 8x8 diagonal block in registers (redundantly: no cross-lane
-            // traffic), right-looking, one rsq + one Newton step per pivot (1/l_pp is that
-            // rsqrt), then ONE forward substitution x = L_pp^-1 a per lane with no divergence:
-            // panel lanes solve their row (a = their row of A), diagonal-block lanes solve
-            // a = e_i, i.e. column i of L_pp^-1 (the doubling inverse's 8x8 blocks)
-            const int r = lane;
-            const bool dg = r < c0 + 8;
-            double D[8][8], x[8];
+        const int J1 = (c0 + 8) >> 4;  // block column holding panel s+1
+        if (w == 0) {
 #pragma unroll
-            for (int i = 0; i < 8; i++)
-#pragma unroll
-                for (int p = 0; p <= i; p++) D[i][p] = A[(c0 + i) * LD + c0 + p];
-#pragma unroll
-            for (int p = 0; p < 8; p++) x[p] = dg ? (r - c0 == p ? 1.0 : 0.0) : A[r * LD + c0 + p];
-            double l[8][8], inv[8];
-            bool bad = false;
-#pragma unroll
-            for (int p = 0; p < 8; p++) {
-                const double dpp = D[p][p];
-                if (dpp <= 0.0) bad = true;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
-                double y = __builtin_amdgcn_rsq(dpp);
-                y = y * fma(-0.5 * dpp * y, y, 1.5);
-                inv[p] = y;
-                l[p][p] = dpp * y;
-#pragma unroll
-                for (int i = p + 1; i < 8; i++) l[i][p] = D[i][p] * y;
-#pragma unroll
-                for (int i = p + 1; i < 8; i++)
-#pragma unroll
-                    for (int j = p + 1; j <= i; j++) D[i][j] = fma(-l[i][p], l[j][p], D[i][j]);
-            }
-            if (bad && r == c0) flags[kFlagFail] = 1;
-#pragma unroll
-            for (int p = 0; p < 8; p++) {
-                const double xp = x[p] * inv[p];
-                x[p] = xp;
-#pragma unroll
-                for (int i = p + 1; i < 8; i++) x[i] = fma(-xp, l[i][p], x[i]);
-            }
-            if (dg) {
-                const int i = r - c0;
-#pragma unroll
-                for (int ii = 0; ii < 8; ii++)
-                    if (ii == i) {
-#pragma unroll
-                        for (int p = 0; p <= ii; p++) A[r * LD + c0 + p] = l[ii][p];
-                    }
-#pragma unroll
-                for (int m = 0; m < 8; m++) Li[(c0 + m) * LD + r] = x[m];
-            } else {
-#pragma unroll
-                for (int p = 0; p < 8; p++) A[r * LD + c0 + p] = x[p];
-            }
-        }
-        if (s == 0 && early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (s == 0 && early && tid == 0)
-            __hip_atomic_store(early, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        pstamp(1 + 2 * s);
-        // rank-8 update of the lower trailing block (rows, cols >= c0 + 8) by MFMA: wave w the
-        // 16x16 blocks (w, J), all operand loads before the MFMAs; only trailing lower entries
-        // are written back
-        const int lo = c0 + 8;
-        if (lo < T && 16 * w + 15 >= lo) {
-            const int Jlo = lo >> 4;
-            const double a0 = -A[(16 * w + r16) * LD + c0 + kq];
-            const double a1 = -A[(16 * w + r16) * LD + c0 + 4 + kq];
-            d4 c[4];
-            double b0[4], b1[4];
-#pragma unroll
-            for (int J = 0; J < 4; J++) {
-                if (J >= Jlo && J <= w) {
-#pragma unroll
-                    for (int e = 0; e < 4; e++) c[J][e] = A[(16 * w + kq + 4 * e) * LD + 16 * J + r16];
-                    b0[J] = A[(16 * J + r16) * LD + c0 + kq];
-                    b1[J] = A[(16 * J + r16) * LD + c0 + 4 + kq];
-                }
-            }
-#pragma unroll
-            for (int J = 0; J < 4; J++) {
-                if (J >= Jlo && J <= w) {
-                    c[J] = mfma(a0, b0[J], c[J]);
-                    c[J] = mfma(a1, b1[J], c[J]);
-                }
-            }
-#pragma unroll
-            for (int J = 0; J < 4; J++) {
-                if (J >= Jlo && J <= w) {
-                    const int col = 16 * J + r16;
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        const int row = 16 * w + kq + 4 * e;
-                        if (col >= lo && col <= row) A[row * LD + col] = c[J][e];
-                    }
-                }
-            }
+            for (int I = 0; I < 4; I++)
+                if (I >= J1) trail_block(A, c0, I, J1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS writes before the reads
+            panel_factor(A, Li, c0 + 8, flags);
+        } else {
+            for (int J = J1 + 1; J <= w; J++) trail_block(A, c0, w, J);
         }
         __syncthreads();
-        pstamp(2 + 2 * s);
+        pstamp(2 + s);
     }
     // inverse by doubling, [[Ai,0],[B,Ci]]^-1 = [[Ai,0],[-Ci B Ai, Ci]]; the 8x8 diagonal
     // inverses came from the panel steps.  Stage 8 on VALU (one output per thread):
