@@ -677,10 +677,14 @@ hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, doubl
     // potrf / trsm / update launch triple per panel
     const char* df_env = getenv("M3S_CHOL_DF");
     const int df = df_env ? atoi(df_env) : 1;
+    bool done = false;
     if (df) {
-        hipError_t e = launch_chol_dataflow(st, npad, Hd, Linv, chol_ready_ptr(Linv, npad), epoch, flags);
-        if (e != hipSuccess) return e;
-    } else {
+        // a cooperative launch the device cannot hold (or refuses) falls back to the per-panel
+        // launches below instead of failing the call
+        done = launch_chol_dataflow(st, npad, Hd, Linv, chol_ready_ptr(Linv, npad), epoch, flags) == hipSuccess;
+        if (!done) (void)hipGetLastError();
+    }
+    if (!done) {
         for (int k = 0; k < nt; k++) {
             hipLaunchKernelGGL(chol_potrf_kernel, dim3(1), dim3(kPotrfThreads), 0, st, Hd, npad, k, Linv,
                                flags);
