@@ -47,6 +47,13 @@
 #include "gn_kernels.h"
 #include "sim3.h"
 
+// 1: the tail's pose step factors L_KK in every thread and fuses the panel-row solve into it
+// (no L_KK^-1 round trip through LDS, one barrier less per pose); 0: wave 0 factors and inverts,
+// a barrier, then a matvec per panel row
+#ifndef M3S_TAIL_FUSED_A
+#define M3S_TAIL_FUSED_A 1
+#endif
+
 namespace m3s {
 
 namespace {
@@ -154,7 +161,7 @@ __device__ __forceinline__ void bwd7(const double (&L)[28], const double (&inv)[
 }
 
 // Li = L^-1 (packed lower) from L and inv = 1/diag
-__device__ __forceinline__ void inv7(const double (&L)[28], const double (&inv)[7], double (&Li)[28]) {
+[[maybe_unused]] __device__ __forceinline__ void inv7(const double (&L)[28], const double (&inv)[7], double (&Li)[28]) {
 #pragma unroll
     for (int j = 0; j < 7; j++) {
         Li[pk(j, j)] = inv[j];
@@ -260,9 +267,62 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
     lds_barrier();
     tick(6);
 
+#if M3S_TAIL_FUSED_A
+    double yprev[7];  // y of the previous pose, written to sZ by one thread a phase later
+#endif
     for (int K = 0; K < nt; K++) {
         const int c0 = 7 * K;
         const int nrows = n - c0 - 7;  // panel rows below the diagonal block
+#if M3S_TAIL_FUSED_A
+        // A. every thread factors L_KK in registers (redundantly: no barrier, no L_KK^-1 round
+        //    trip through LDS) and runs two forward substitutions: y_K = L_KK^-1 z_K and one
+        //    input of its role -- panel row i = c0+7+tid (its row of L, RHS update), or, for the
+        //    7 threads after them, e_m (column m of L_KK^-1, for the back-substitution)
+        double yK[7];
+        if (K > 0 && tid == kThreads - 8) {  // the previous pose's y (nobody reads it in this phase)
+#pragma unroll
+            for (int c = 0; c < 7; c++) sZ[c0 - 7 + c] = yprev[c];
+        }
+        {
+            double L[28], inv[7], z[7], in[7], out[7];
+            const bool prow = tid < nrows;
+            const int m = tid - nrows;  // diagonal-column role: 0 <= m < 7
+            const int i = c0 + 7 + tid;
+#pragma unroll
+            for (int r = 0; r < 7; r++) {
+#pragma unroll
+                for (int j = 0; j <= r; j++) L[pk(r, j)] = sPn[(c0 + r) * kPS + j];
+                z[r] = sZ[c0 + r];
+            }
+#pragma unroll
+            for (int c = 0; c < 7; c++) in[c] = prow ? sPn[i * kPS + c] : (c == m ? 1.0 : 0.0);
+            const double zr0 = prow ? sZ[i] : 0.0;
+            chol7(L, inv, bad);
+            fwd7(L, inv, z, yK);
+            fwd7(L, inv, in, out);
+            if (prow) {
+                double* Lg = a.Lg + (int64_t)i * n + c0;
+                double zr = zr0;
+#pragma unroll
+                for (int c = 0; c < 7; c++) {
+                    sPop[i * kPS + c] = out[c];
+                    Lg[c] = out[c];
+                    zr = fma(-out[c], yK[c], zr);
+                }
+                sZ[i] = zr;
+            } else if (m < 7) {
+#pragma unroll
+                for (int c = 0; c < 7; c++)
+                    if (c >= m) sL[K * kLRec + pk(c, 0) + m] = out[c];
+            }
+            if (tid >= kThreads - 7) {  // the pose's own rows leave the MFMA operand
+                const int rr = c0 + (tid - (kThreads - 7));
+#pragma unroll
+                for (int c = 0; c < 8; c++) sPop[rr * kPS + c] = 0.0;
+            }
+        }
+        if (K >= 3 && K < 5) tick(7);
+#else
         // A1. wave 0: L_KK (in-lane serial, every lane), L_KK^-1 and y_K = L_KK^-1 z_K
         if (W == 0) {
             double L[28], inv[7], z[7], y[7], Li[28];
@@ -323,8 +383,13 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
                 for (int c = 0; c < 8; c++) sPop[rr * kPS + c] = 0.0;
             }
         }
+#endif
         if (K >= 3 && K < 5) tick(8);
         lds_barrier();
+#if M3S_TAIL_FUSED_A
+#pragma unroll
+        for (int c = 0; c < 7; c++) yprev[c] = yK[c];  // stored at the next phase A (or after the loop)
+#endif
         // B. -C_IJ += P_I P_J^T for the live tiles (J >= Jmin), operands from registers.  The
         //    slots are sorted by J, so the live ones are a suffix [kf, NS): a fall-through
         //    switch enters the unrolled MFMA sequence at kf with no per-slot tests.  Then the
@@ -402,6 +467,12 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
         if (K >= 3 && K < 5) tick(11);
     }
     tick(2);
+#if M3S_TAIL_FUSED_A
+    if (nt > 0 && tid == kThreads - 8) {
+#pragma unroll
+        for (int c = 0; c < 7; c++) sZ[7 * (nt - 1) + c] = yprev[c];
+    }
+#endif
 
     __syncthreads();  // the L rows (global, written by every wave) are read below
     // back-substitution L^T x = y over the tail, right-looking: x_K = L_KK^-T z_K, then every
