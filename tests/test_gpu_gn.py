@@ -401,7 +401,7 @@ def test_cfg4_full_size_one_and_ten_iterations(backend, oracle):
     assert _rel(Ta, T10) < 1e-5, _rel(Ta, T10)
 
 
-@pytest.mark.parametrize("topo", ["cfg4", "cfg3", "clique28", "pair"])
+@pytest.mark.parametrize("topo", ["cfg4", "cfg3", "clique28", "clique20", "clique12", "pair"])
 @pytest.mark.parametrize("dense", [True, False])
 def test_dataflow_factor_matches_multilaunch_factor(backend, monkeypatch, topo, dense):
     """The one-launch dataflow tile LL^T (chol_df.hip, default) against the per-panel
@@ -411,8 +411,8 @@ def test_dataflow_factor_matches_multilaunch_factor(backend, monkeypatch, topo, 
     columns = 434 tiles, more than one per workgroup); False the sparse solver's dense core
     (cfg4: 141 poses, 16 tile columns); clique28 a 189-unknown core (3 tile columns); pair one
     tile column."""
-    if topo == "clique28":
-        N = 29
+    if topo.startswith("clique"):  # 28 / 19 / 11 free poses: 3 / 3 / 2 tile columns (dense)
+        N = {"clique28": 29, "clique20": 20, "clique12": 12}[topo]
         und = [(a, b) for a in range(N) for b in range(a + 1, N)]
         g = synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
     elif topo == "pair":
