@@ -411,7 +411,7 @@ def test_dataflow_factor_matches_multilaunch_factor(backend, monkeypatch, topo, 
     columns = 434 tiles, more than one per workgroup); False the sparse solver's dense core
     (cfg4: 141 poses, 16 tile columns); clique28 a 189-unknown core (3 tile columns); pair one
     tile column."""
-    if topo.startswith("clique"):  # 28 / 19 / 11 free poses: 3 / 3 / 2 tile columns (dense)
+    if topo.startswith("clique"):  # 28 / 19 / 11 free poses: 4 / 3 / 2 tile columns (dense)
         N = {"clique28": 29, "clique20": 20, "clique12": 12}[topo]
         und = [(a, b) for a in range(N) for b in range(a + 1, N)]
         g = synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
