@@ -409,7 +409,8 @@ def test_dataflow_factor_matches_multilaunch_factor(backend, monkeypatch, topo, 
     same factorisation in a left- instead of right-looking summation order -> updates agree to
     ~1e-9.  dense=True factors the whole system (cfg4: 255 poses, 1785 unknowns in 28 tile
     columns = 434 tiles, more than one per workgroup); False the sparse solver's dense core
-    (cfg4: 141 poses, 16 tile columns); clique28 a 189-unknown core (3 tile columns); pair one
+    (cfg4: 141 poses, 16 tile columns); the cliques 196 / 133 / 77 unknowns (4 / 3 / 2 tile
+    columns); pair one
     tile column."""
     if topo.startswith("clique"):  # 28 / 19 / 11 free poses: 4 / 3 / 2 tile columns (dense)
         N = {"clique28": 29, "clique20": 20, "clique12": 12}[topo]
