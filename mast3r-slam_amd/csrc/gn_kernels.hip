@@ -546,13 +546,15 @@ __global__ __launch_bounds__(kBackThreads) void chol_backsolve_kernel(
     const int nt = npad / T;
     const double* yrow = Hd + (int64_t)npad * npad;
     for (int c = tid; c < npad; c += kBackThreads) y[c] = yrow[c];
-    for (int k = nt - 1; k >= 0; k--) {
-        const double* Lk = Linv + (int64_t)k * T * T;
+    {
+        const double* Lk = Linv + (int64_t)(nt - 1) * T * T;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int id = tid + q * kBackThreads;
             Li[id >> 6][id & 63] = Lk[id];
         }
+    }
+    for (int k = nt - 1; k >= 0; k--) {
         __syncthreads();
         {   // x_k[c] = sum_r Li[r][c] y_k[r]: 16 partial sums of 4 rows per column
             const int c = tid & 63, g = tid >> 6;
@@ -570,6 +572,14 @@ __global__ __launch_bounds__(kBackThreads) void chol_backsolve_kernel(
             x[k * T + tid] = acc;
         }
         __syncthreads();
+        // the next step's tile inverse in flight (registers) during the row-panel update, then
+        // into LDS (its reads of this step's inverse are behind the barrier above)
+        double lnext[4];
+        if (k > 0) {
+            const double* Ln = Linv + (int64_t)(k - 1) * T * T;
+#pragma unroll
+            for (int q = 0; q < 4; q++) lnext[q] = Ln[tid + q * kBackThreads];
+        }
         const double* Lrow = Hd + (int64_t)k * T * npad;  // row panel k: tiles (k, j<k)
         for (int c = tid; c < k * T; c += kBackThreads) {
             double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -577,7 +587,13 @@ __global__ __launch_bounds__(kBackThreads) void chol_backsolve_kernel(
             for (int b = 0; b < T; b++) acc[b & 3] = fma(Lrow[(int64_t)b * npad + c], xk[b], acc[b & 3]);
             y[c] -= (acc[0] + acc[1]) + (acc[2] + acc[3]);
         }
-        __syncthreads();
+        if (k > 0) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int id = tid + q * kBackThreads;
+                Li[id >> 6][id & 63] = lnext[q];
+            }
+        }
     }
 }
 
