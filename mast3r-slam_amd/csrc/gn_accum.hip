@@ -17,6 +17,7 @@
 #include <climits>
 #include <cstdint>
 
+#include "edge_reduce.h"
 #include "gn_kernels.h"
 #include "sim3.h"
 
@@ -308,7 +309,7 @@ __device__ __forceinline__ float row_sum16(float v) {
 // Per wave a reduce-scatter: 36 values -> 18 (32-lane halves) -> 9 (16-lane rows, row r of
 // register j holding value j + 9r), then a 16-lane row sum (126 lane ops instead of the
 // 35 x 6 shuffle-adds of a butterfly per value); then the 4 waves in fixed order.
-__device__ __forceinline__ void block_partial(const float* accs, float* __restrict__ out) {
+__device__ __forceinline__ void block_partial(const float* accs, float* __restrict__ out, bool coh = false) {
     __shared__ float red[kAccThreads / 64][kNaccPad];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     static_assert(kNaccPad == 36, "reduce-scatter is laid out for 36 values");
@@ -327,7 +328,10 @@ __device__ __forceinline__ void block_partial(const float* accs, float* __restri
         float s = red[0][tid];
 #pragma unroll
         for (int w = 1; w < kAccThreads / 64; w++) s += red[w][tid];
-        out[tid] = s;
+        if (coh)  // write-through: read by the edge's last workgroup, possibly on another XCD
+            __hip_atomic_store(out + tid, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            out[tid] = s;
     }
 }
 
@@ -754,7 +758,8 @@ void gn_accum_packed_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Zs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int4* __restrict__ pack,
     AccParams P, const int4* __restrict__ sched, float* __restrict__ partials,
-    const int* __restrict__ flags, const float* __restrict__ px, const int* __restrict__ pcnt) {
+    const int* __restrict__ flags, const float* __restrict__ px, const int* __restrict__ pcnt,
+    int* __restrict__ ecnt, double* __restrict__ edgeblk) {
     const int4 tk = sched[blockIdx.x];  // {edge, chunk, ix, jx}, loaded together with the flag
     if (flags[kFlagDone]) return;
     const int e = tk.x, c = tk.y, ix = tk.z, jx = tk.w;
@@ -816,7 +821,22 @@ void gn_accum_packed_kernel(
     else
         accum_steps<MODE, false>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
 #endif
-    block_partial(acc, partials + ((int64_t)e * P.nchunks + c) * kNaccPad);
+    block_partial(acc, partials + ((int64_t)e * P.nchunks + c) * kNaccPad, ecnt != nullptr);
+    if (ecnt != nullptr) {
+        // fused edge reduce: the edge's last workgroup to finish sums its chunk partials (in
+        // chunk order: bitwise the separate gn_edge_reduce_kernel) -- one launch less per
+        // iteration, and the reduce overlaps the other edges' accumulation
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores landed
+        __syncthreads();
+        if (threadIdx.x == 0)
+            s_last = __hip_atomic_fetch_add(ecnt + e, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P.nchunks - 1;
+        __syncthreads();
+        if (s_last) {
+            edge_reduce_body<true>(partials, P.nchunks, Twc, ii_loc, edgeblk, e);
+            if (threadIdx.x == 0) __hip_atomic_store(ecnt + e, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const float* Twc,
@@ -872,10 +892,10 @@ hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float*
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,
                                const int4* sched, float* partials, const int* flags, const float* px,
-                               const int* pcnt) {
+                               const int* pcnt, int* ecnt, double* edgeblk) {
 #define M3S_ACCP(MODE, CP)                                                                       \
     hipLaunchKernelGGL((gn_accum_packed_kernel<MODE, CP>), grid, dim3(kAccThreads), 0, st, Twc, Xs, Zs, \
-                       ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt)
+                       ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt, edgeblk)
     const bool cp = px != nullptr;
     if (mode == GN_RAYS) {
         if (cp) M3S_ACCP(GN_RAYS, true); else M3S_ACCP(GN_RAYS, false);

@@ -161,7 +161,7 @@ int chunk_points(int64_t HW, int nchunks) {
 
 struct Layout {
     size_t partials, edgeblk, compact, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent, blk_ref, grad_ptr,
-        grad_ent, sched, pack, packx, pcnt, zs, total;
+        grad_ent, ecnt, sched, pack, packx, pcnt, zs, total;
     int nchunks, npad, nblk_max;
 };
 
@@ -198,6 +198,7 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.blk_ref = take(sizeof(int) * (size_t)E_local * 4);  // reference-order assembly codes
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
+    L.ecnt = take(sizeof(int) * (size_t)E_local);  // fused edge reduce: finished chunks per edge
     L.sched = take(sizeof(int) * 4 * (size_t)E_local * L.nchunks);  // {edge, chunk, ix, jx} per task
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
@@ -928,6 +929,7 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     put(L.blk_ref, p.blk_ref);
     put(L.grad_ptr, p.grad_ptr);
     put(L.grad_ent, p.grad_ent);
+    std::memset(h + (L.ecnt - lo), 0, sizeof(int) * (size_t)a.E_local);  // (the kernel re-zeroes them)
     M3S_HIP_CHECK(g_stage_ws.upload(c.ws + lo, h, L.sched - lo, c.st));
     if (early_pack) {
         rc = prepare_iterations(a, c);
@@ -997,21 +999,27 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
     if (a.E_local > 0) {
         g_prof.mark(c.st, true);
         const dim3 grid((unsigned)(L.nchunks * a.E_local));
+        // M3S_GN_FUSE_REDUCE=1 (default): the packed accumulate's last workgroup per edge does
+        // the edge reduce (no separate launch); 0: gn_edge_reduce_kernel
+        const bool fuse_reduce = env_int("M3S_GN_FUSE_REDUCE", 1) != 0;
+        const bool fused = c.packed && fuse_reduce;
         if (c.packed)
             M3S_HIP_CHECK(launch_accum_packed(a.mode, grid, c.st, a.Twc, a.Xs, c.at<float>(L.zs),
                                               c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
                                               c.at<int4>(L.pack), c.P, c.at<int4>(L.sched),
                                               c.at<float>(L.partials), flags,
                                               c.compact ? c.at<float>(L.packx) : nullptr,
-                                              c.at<int>(L.pcnt)));
+                                              c.at<int>(L.pcnt), fused ? c.at<int>(L.ecnt) : nullptr,
+                                              c.at<double>(L.edgeblk)));
         else
             M3S_HIP_CHECK(launch_accum(a.mode, c.vec, grid, c.st, a.Twc, a.Xs, a.Cs,
                                        c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), c.es, c.P,
                                        c.at<int4>(L.sched), c.at<float>(L.partials),
                                        flags));
         g_prof.mark(c.st, true);
-        M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
-                                         a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
+        if (!fused)
+            M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
+                                             a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
     }
     const int npose = (int)(a.N - 1);
     if (c.sp.enabled) {

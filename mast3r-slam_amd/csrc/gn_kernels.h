@@ -99,7 +99,7 @@ hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float*
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,
                                const int4* sched, float* partials, const int* flags, const float* px,
-                               const int* pcnt);
+                               const int* pcnt, int* ecnt = nullptr, double* edgeblk = nullptr);
 hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
                               const float* Twc, const int* ii_loc, double* edgeblk,
                               const int* flags);

@@ -454,3 +454,18 @@ def test_singular_core_fails_through_tile_factor(backend, monkeypatch, dense, ch
     T_g, dx_g = _run_gpu(backend, g, "rays", 10, delta=1e-8)
     assert np.array_equal(T_g, g.Twc.numpy())
     assert np.all(dx_g == 0)
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib", "points"])
+def test_fused_edge_reduce_is_bitwise_the_separate_launch(backend, monkeypatch, mode):
+    """The packed accumulate's last workgroup per edge runs the edge reduce (default) instead of
+    gn_edge_reduce_kernel (M3S_GN_FUSE_REDUCE=0): the same f32 partials summed in chunk order,
+    read back with agent-coherent loads from other workgroups / XCDs -> bitwise the same poses
+    over 4 iterations (the per-edge counters are re-zeroed by the kernel between iterations)."""
+    g = synth.make_graph("cfg3", H=48, W=64, seed=6)
+    monkeypatch.setenv("M3S_GN_FUSE_REDUCE", "0")
+    T_s, dx_s = _run_gpu(backend, g, mode, 4)
+    monkeypatch.setenv("M3S_GN_FUSE_REDUCE", "1")
+    T_f, dx_f = _run_gpu(backend, g, mode, 4)
+    assert np.isfinite(T_f).all()
+    assert np.array_equal(T_f, T_s) and np.array_equal(dx_f, dx_s)
