@@ -60,15 +60,19 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// thread 0 waits until *f reaches the epoch (bounded; on timeout the solve is failed)
+// thread 0 waits until *f reaches the epoch (bounded; on timeout the solve is failed, and once
+// the solve has failed -- a timeout or a pivot <= 0 -- later waits give up early, so a failed
+// factorisation drains quickly; its result is discarded: dx = 0)
 __device__ __forceinline__ void wait_ready(const int* f, int epoch, int* flags) {
     int spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1 << 22)) {
-            flags[kFlagFail] = 1;
+            __hip_atomic_store(flags + kFlagFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
+        if ((spins & 1023) == 0 && __hip_atomic_load(flags + kFlagFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return;
     }
 }
 
