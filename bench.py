@@ -56,11 +56,50 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(args) -> int:
+    """``--gpus N > 1`` without a torch.distributed launcher (no WORLD_SIZE): start N ranks of this
+    script with torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a CHILD
+    process -- nothing here has touched the GPU -- and return its exit status."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def _dump_maps_at_exit(path):
+    """Diagnostics (M3S_EXIT_MAPS=path): this process's /proc/self/maps at interpreter exit, to
+    resolve the program counters of a fault during the C-level exit handlers that follow."""
+    import atexit
+
+    def dump():
+        try:
+            with open("/proc/self/maps") as f, open(path, "w") as o:
+                o.write(f.read())
+        except OSError:
+            pass
+
+    atexit.register(dump)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU)")
+    if os.environ.get("M3S_BENCH_SPAWN_CHECK"):  # tests/test_bench_cli.py: the launch, no GPU work
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank}), flush=True)
+        return
+    if os.environ.get("M3S_EXIT_MAPS"):
+        _dump_maps_at_exit(os.environ["M3S_EXIT_MAPS"])
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -302,6 +341,12 @@ def matching_bench(dev, reps=10):
         t_glue = wall_ms(True)        # the fused pipeline op (csrc/match_glue.hip)
         t_torch_glue = wall_ms(False)  # the reference's torch glue around the two ops
         npx = B * h * w
+        # the fused op's glue rounds like the reference's glue on the HOST (normalize / 3x3
+        # conv); torch's GPU kernels round differently: how many matches that changes here
+        i_f, v_f = match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=True)
+        i_t, v_t = match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=False)
+        glue_diff = {"idx_differ": int((i_f != i_t).sum()), "valid_differ": int((v_f != v_t).sum()),
+                     "pixels": npx}
         res[f"B{B}"] = {
             "pairs_per_s_kernels": B / ((t_ip + t_rf) * 1e-3),
             "pairs_per_s_glue": B / (t_glue * 1e-3),
@@ -321,6 +366,7 @@ def matching_bench(dev, reps=10):
             },
             "match_iterative_proj_ms": t_glue,
             "match_iterative_proj_torch_glue_ms": t_torch_glue,
+            "fused_vs_torch_gpu_glue": glue_diff,
             "iter_proj_GBps": 65 * npx / (t_ip * 1e-3) / 1e9,
             "refine_GBps": 128 * npx / (t_rf * 1e-3) / 1e9,
             "refine_candidate_GBps": 245 * 48 * npx / (t_rf * 1e-3) / 1e9,
@@ -425,11 +471,29 @@ def _cpu_model():
     return "unknown"
 
 
+def _host_cores():
+    """The host's CPUs as this process sees them: nproc (the machine), the affinity set, the cgroup
+    CPU quota; ``usable`` = what the oracle's OpenMP pool is sized to (affinity, capped by the
+    quota -- the GPU box gives a job a share of a larger machine)."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable}
+
+
 def cpu_baseline(g, mode, E_und, iters):
     """The CPU oracle (restatement of the reference backend, which has no CPU path) on a
     bounded sample: ONE GN iteration of the same graph (all directed edges, full 512x384),
-    2 warm-ups then the median of 5 timed runs, OpenMP threads =
-    OMP_NUM_THREADS.  Also produces the accuracy references: the oracle's poses after 1 and
+    2 warm-ups then the median of 5 timed runs, OpenMP threads = every CPU
+    this process may use (``_host_cores``: affinity set capped by the cgroup quota; nproc,
+    affinity and quota are recorded beside it).  Also produces the accuracy references: the oracle's poses after 1 and
     after ``iters`` iterations, and after 1 iteration with the float terms summed in double."""
     import statistics
 
@@ -447,6 +511,8 @@ def cpu_baseline(g, mode, E_und, iters):
                              LOCAL["Q_conf"], max_iter=n_iter, delta_thresh=0.0)
 
     arrs = [c(g.Twc), c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx), c(g.valid), c(g.Q)]
+    hw = _host_cores()
+    O.set_num_threads(hw["usable"])  # every core this process may run on
     P1 = params(1)
     times = []
     for r in range(7):
@@ -463,6 +529,7 @@ def cpu_baseline(g, mode, E_und, iters):
         "value": E_und * 1 / dt,
         "unit": "keyframe-pair GN iters/s",
         "cores": O.num_threads(),
+        "host": hw,
         "cpu_model": _cpu_model(),
         "kind": "port",
         "sample": f"1 GN iteration of the same graph ({E_und} pairs, {2 * E_und} directed edges, "

@@ -33,12 +33,34 @@ enum {
     M3S_ERR_INVALID = 1, /* bad shape / argument */
     M3S_ERR_HIP = 2,     /* HIP runtime error */
     M3S_ERR_WORKSPACE = 3,
-    M3S_ERR_COMM = 4
+    M3S_ERR_COMM = 4,
+    M3S_ERR_TIMEOUT = 5  /* a bounded device-side wait (dataflow factorisation / grid barrier)
+                            gave up: the solve's result was discarded -- not a singular system */
 };
 
 const char* m3s_last_error(void);
 /* Library build identifier ("m3s <version> gfx950"). */
 const char* m3s_version(void);
+/* Releases the library's cached host resources (pinned staging buffers, events).  Registered
+ * with atexit when the library is loaded (and called by the Python module's atexit hook), so no
+ * HIP call runs from a static or thread-local destructor during exit().  Idempotent; no other
+ * entry point may be called afterwards. */
+void m3s_shutdown(void);
+
+/*
+ * FMA-contraction convention of the reference build's float arithmetic.  The reference is built
+ * by nvcc -O3 (setup.py:29-37: --fmad=true), which fuses a multiply into the add that consumes it;
+ * for `a*b + c*d` the left product is fused (LLVM / NVPTX combine order).  The parity paths
+ * (iter_proj, refine_matches f32/f64, the reference-order GN accumulate and the retraction)
+ * restate that explicitly (mast3r-slam_amd/csrc/contract.h); OFF and NVCC_RIGHT are variants for
+ * measuring the convention's effect.
+ */
+enum {
+    M3S_CONTRACT_OFF = 0,        /* IEEE multiply, then add (no fusion) */
+    M3S_CONTRACT_NVCC = 1,       /* nvcc --fmad=true, left product of a two-product sum fused */
+    M3S_CONTRACT_NVCC_RIGHT = 2, /* the same, right product fused */
+    M3S_CONTRACT_DEFAULT = M3S_CONTRACT_NVCC
+};
 
 /*
  * iter_proj -- replaces iter_proj (gn.cpp:84-99 -> matching_kernels.cu:279-316).
@@ -52,6 +74,12 @@ int m3s_iter_proj(const float* rays, const float* pts, const float* p_init,
                   float* p_new, uint8_t* converged,
                   int64_t B, int64_t H, int64_t W, int64_t N,
                   int max_iter, float lambda_init, float cost_thresh, void* stream);
+/* The same with an explicit contraction convention (M3S_CONTRACT_*); m3s_iter_proj uses
+ * M3S_CONTRACT_DEFAULT. */
+int m3s_iter_proj_ex(const float* rays, const float* pts, const float* p_init,
+                     float* p_new, uint8_t* converged,
+                     int64_t B, int64_t H, int64_t W, int64_t N,
+                     int max_iter, float lambda_init, float cost_thresh, int contract, void* stream);
 
 /*
  * refine_matches -- replaces refine_matches (gn.cpp:101-114 -> matching_kernels.cu:84-116).
@@ -75,7 +103,7 @@ int m3s_refine_matches_f64(const double* D11, const double* D21,
 /*
  * match_iterative_proj -- the whole matching pipeline of the reference's Python caller
  * (matching.py:52-90: prep_for_iter_proj, iter_proj, p.long(), the occlusion test, refine on
- * .half() descriptors, pixel_to_lin) in five launches.
+ * .half() descriptors, pixel_to_lin) in five launches.  `contract`: iter_proj's M3S_CONTRACT_*.
  *   X11, X21  [B,H,W,3] f32      D11, D21 [B,H,W,F] f32
  *   idx_init  [B,H*W]   i64 or NULL (identity start)
  *   idx_out   [B,H*W]   i64 out  (u + W v)      valid_out [B,H*W] u8 out (bool)
@@ -85,8 +113,8 @@ size_t m3s_match_workspace_bytes(int64_t B, int64_t H, int64_t W, int64_t F);
 int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D11, const float* D21,
                              const int64_t* idx_init, int64_t B, int64_t H, int64_t W, int64_t F,
                              int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
-                             int radius, int dilation_max, int64_t* idx_out, uint8_t* valid_out,
-                             void* ws, size_t ws_bytes, void* stream);
+                             int radius, int dilation_max, int contract, int64_t* idx_out,
+                             uint8_t* valid_out, void* ws, size_t ws_bytes, void* stream);
 
 /*
  * Diagnostics of the MFMA refine path (env M3S_REFINE_MFMA=1): out2 = {candidates re-scored

@@ -43,6 +43,7 @@ struct DfArgs {
     int* ready;
     int* flags;
     int npad, nt, ntiles, epoch;  // ntiles = number of tasks (num_tasks)
+    int spin_limit;  // bound of a ready wait (s_sleep(1) steps); < 0: every wait times out (test hook)
     long long* trace;  // diagnostics (tools/ubench_chol_df.hip): 4 timestamps per tile, else null
 };
 
@@ -60,14 +61,17 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// thread 0 waits until *f reaches the epoch (bounded; on timeout the solve is failed, and once
-// the solve has failed -- a timeout or a pivot <= 0 -- later waits give up early, so a failed
-// factorisation drains quickly; its result is discarded: dx = 0)
-__device__ __forceinline__ void wait_ready(const int* f, int epoch, int* flags) {
+// thread 0 waits until *f reaches the epoch (bounded; on timeout the solve is failed AND the
+// sticky timeout flag is raised, which the driver reports as M3S_ERR_TIMEOUT -- a lost publish
+// or a starved producer must not pass for a singular system.  Once the solve has failed -- a
+// timeout or a pivot <= 0 -- later waits give up early, so a failed factorisation drains
+// quickly; its result is discarded: dx = 0)
+__device__ __forceinline__ void wait_ready(const int* f, int epoch, int* flags, int spin_limit) {
     int spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
+    while (spin_limit < 0 || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1 << 22)) {
+        if (++spins > spin_limit) {
+            __hip_atomic_store(flags + kFlagTimeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(flags + kFlagFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
         for (int j = 0; j < nt; j++) {
             d4 accd[4];
             if (j >= 2) {
-                if (tid == 0) wait_ready(a.ready + hflag(nt, j), a.epoch, a.flags);
+                if (tid == 0) wait_ready(a.ready + hflag(nt, j), a.epoch, a.flags, a.spin_limit);
                 __syncthreads();
             }
             cstamp(j, 0);
@@ -424,8 +428,8 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             load_acc<false>(accd, tile(h, h), ld);
             for (int k = 0; k <= j; k++) {
                 if (tid == 0) {
-                    wait_ready(a.ready + h * nt + k, a.epoch, a.flags);
-                    wait_ready(a.ready + (h - 1) * nt + k, a.epoch, a.flags);
+                    wait_ready(a.ready + h * nt + k, a.epoch, a.flags, a.spin_limit);
+                    wait_ready(a.ready + (h - 1) * nt + k, a.epoch, a.flags, a.spin_limit);
                 }
                 __syncthreads();
                 load_tile_coh(X, tile(h, k), ld);
@@ -447,8 +451,8 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             load_acc<false>(acc, tile(i, j), ld);
             for (int k = 0; k < j; k++) {
                 if (tid == 0) {
-                    wait_ready(a.ready + i * nt + k, a.epoch, a.flags);
-                    wait_ready(a.ready + j * nt + k, a.epoch, a.flags);
+                    wait_ready(a.ready + i * nt + k, a.epoch, a.flags, a.spin_limit);
+                    wait_ready(a.ready + j * nt + k, a.epoch, a.flags, a.spin_limit);
                 }
                 __syncthreads();
                 load_tile_coh(X, tile(i, k), ld);
@@ -459,7 +463,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             }
             stamp(a, t, 1);
             acc_to_lds(X, acc);
-            if (tid == 0) wait_ready(a.ready + j * nt + j, a.epoch, a.flags);
+            if (tid == 0) wait_ready(a.ready + j * nt + j, a.epoch, a.flags, a.spin_limit);
             __syncthreads();
             stamp(a, t, 2);
             load_tile_coh(Y, a.Linv + (int64_t)j * T * T, T);
@@ -502,6 +506,10 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
     a.nt = npad / T;
     a.ntiles = num_tasks(a.nt);
     a.epoch = epoch;
+    // M3S_TEST_FORCE_TIMEOUT=1 (tests only): every ready wait gives up at once, to exercise the
+    // timeout -> M3S_ERR_TIMEOUT path without a real hang
+    const char* ft = getenv("M3S_TEST_FORCE_TIMEOUT");
+    a.spin_limit = (ft && atoi(ft) != 0) ? -1 : (1 << 22);
     const int grid = 1 + a.ntiles < maxg ? 1 + a.ntiles : maxg;  // workgroup 0 = the diagonal chain
     void* kargs[] = {&a};
     return hipLaunchCooperativeKernel((const void*)chol_df_kernel, dim3(grid), dim3(NT), kargs, 0, st);

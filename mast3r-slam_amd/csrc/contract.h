@@ -1,0 +1,50 @@
+// contract.h -- the FMA-contraction convention of the reference build, as explicit arithmetic.
+//
+// The reference extension is compiled by nvcc with -O3 and no --fmad flag (reference setup.py:
+// 29-37), so --fmad=true: every `a * b + c` whose product feeds the add is emitted as one fused
+// multiply-add.  For a sum of two products `a * b + c * d` the fused product is the one the
+// compiler's DAG combine visits first: LLVM's generic combine and NVPTX's own FADD combine both
+// try the LEFT operand first when both are single-use products (M3S_CONTRACT_NVCC); the other
+// choice (M3S_CONTRACT_NVCC_RIGHT) is kept as a variant because NVVM is closed and its
+// canonicalisation may commute the operands.  M3S_CONTRACT_OFF is plain IEEE multiply then add
+// (the round-1/2 convention, `-ffp-contract=off`).  DESIGN.md §2 records the residual ambiguity.
+//
+// Every file that includes this header must be compiled with contraction OFF (these helpers
+// are the only source of fused operations in the parity paths).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/m3s_backend.h"
+
+namespace m3s {
+
+// a * b + c  (the product fused into the add under nvcc)
+template <int CM>
+__device__ __forceinline__ float cmad(float a, float b, float c) {
+    if constexpr (CM == M3S_CONTRACT_OFF) return a * b + c;
+    else return __builtin_fmaf(a, b, c);
+}
+
+// a * b + c * d
+template <int CM>
+__device__ __forceinline__ float cmm(float a, float b, float c, float d) {
+    if constexpr (CM == M3S_CONTRACT_OFF) return a * b + c * d;
+    else if constexpr (CM == M3S_CONTRACT_NVCC) return __builtin_fmaf(a, b, c * d);
+    else return __builtin_fmaf(c, d, a * b);
+}
+
+// (a0 b0 + a1 b1) + a2 b2 (left-to-right, as the reference source writes its 3-term sums)
+template <int CM>
+__device__ __forceinline__ float cdot3(float a0, float b0, float a1, float b1, float a2, float b2) {
+    return cmad<CM>(a2, b2, cmm<CM>(a0, b0, a1, b1));
+}
+
+// ((a0 b0 + a1 b1) + a2 b2) + a3 b3
+template <int CM>
+__device__ __forceinline__ float cdot4(float a0, float b0, float a1, float b1, float a2, float b2, float a3,
+                                       float b3) {
+    return cmad<CM>(a3, b3, cmad<CM>(a2, b2, cmm<CM>(a0, b0, a1, b1)));
+}
+
+}  // namespace m3s

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <utility>
@@ -73,6 +74,24 @@ void set_error(const char* fmt, ...) {
 const char* get_error() { return g_err.c_str(); }
 
 namespace {
+struct HostResources {
+    std::mutex mu;
+    std::vector<std::pair<void*, void (*)(void*)>> items;
+    bool shut = false;
+};
+HostResources& host_resources() {
+    static HostResources* r = new HostResources;  // never destroyed (used from atexit)
+    return *r;
+}
+}  // namespace
+
+void register_host_resource(void* obj, void (*release)(void*)) {
+    HostResources& r = host_resources();
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.items.emplace_back(obj, release);
+}
+
+namespace {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -85,10 +104,16 @@ struct Staging {
     size_t cap = 0;
     hipEvent_t done = nullptr;
     bool pending = false;
-    ~Staging() {
-        if (pending) (void)hipEventSynchronize(done);
-        if (done) (void)hipEventDestroy(done);
-        if (buf) (void)hipHostFree(buf);
+    // no destructor: released by m3s_shutdown (m3s_common.h)
+    static void release(void* p) {
+        Staging* s = static_cast<Staging*>(p);
+        if (s->pending) (void)hipEventSynchronize(s->done);
+        if (s->done) (void)hipEventDestroy(s->done);
+        if (s->buf) (void)hipHostFree(s->buf);
+        s->buf = s->dev = nullptr;
+        s->cap = 0;
+        s->done = nullptr;
+        s->pending = false;
     }
     // a buffer of >= bytes, free of in-flight copies
     char* get(size_t bytes) {
@@ -129,9 +154,28 @@ struct Staging {
         return e;
     }
 };
-thread_local Staging g_stage_in;   // D2H
-thread_local Staging g_stage_out;  // H2D: the sparse solver's plan
-thread_local Staging g_stage_ws;   // H2D: the workspace's plan (CSR lists, schedule)
+// Per host thread, created on first use and registered for m3s_shutdown (a thread that ends
+// leaves its buffers to the shutdown).  The thread_local objects are plain pointers: nothing
+// runs at thread or process exit.
+struct Stagings {
+    Staging in;   // D2H
+    Staging out;  // H2D: the sparse solver's plan
+    Staging ws;   // H2D: the workspace's plan (CSR lists, schedule)
+    static void release(void* p) {
+        Stagings* s = static_cast<Stagings*>(p);
+        Staging::release(&s->in);
+        Staging::release(&s->out);
+        Staging::release(&s->ws);
+    }
+};
+thread_local Stagings* t_stagings = nullptr;
+Stagings& stagings() {
+    if (!t_stagings) {
+        t_stagings = new Stagings;
+        register_host_resource(t_stagings, &Stagings::release);
+    }
+    return *t_stagings;
+}
 
 // Number of point chunks per directed edge: chunks of ~kChunkTarget points (the per-XCD
 // working set of a chunk-major schedule is ~16 keyframes x chunk x 16 B), and at least
@@ -277,7 +321,7 @@ void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_l
 
 int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     const int64_t E = a.E_total;
-    char* hb = g_stage_in.get(sizeof(int64_t) * 2 * (size_t)E + 64);
+    char* hb = stagings().in.get(sizeof(int64_t) * 2 * (size_t)E + 64);
     M3S_REQUIRE(hb != nullptr, "gauss_newton: pinned host allocation failed");
     int64_t* hii = reinterpret_cast<int64_t*>(hb);
     int64_t* hjj = hii + E;
@@ -711,7 +755,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         M3S_HIP_CHECK(hipMemsetAsync(chol_ready_ptr(sp.dptr<double>(sp.o_linv), sp.npad_tail), 0,
                                      chol_ready_bytes(sp.npad_tail), st));
     if (n > 0) {
-        int* h = reinterpret_cast<int*>(g_stage_out.get(sizeof(int) * n));
+        int* h = reinterpret_cast<int*>(stagings().out.get(sizeof(int) * n));
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
         for (size_t k = 0; k < parts.size(); k++)
             if (!parts[k]->empty()) std::memcpy(h + *offs[k], parts[k]->data(), sizeof(int) * parts[k]->size());
@@ -721,8 +765,8 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
             std::memcpy(hr, v, sizeof(v));
             hr += 8;
         }
-        M3S_HIP_CHECK(g_stage_out.upload(sp.dbuf + sp.o_int, reinterpret_cast<const char*>(h), sizeof(int) * n, st));
-        M3S_HIP_CHECK(g_stage_out.mark(st));  // no host sync: the staging buffer outlives the copy
+        M3S_HIP_CHECK(stagings().out.upload(sp.dbuf + sp.o_int, reinterpret_cast<const char*>(h), sizeof(int) * n, st));
+        M3S_HIP_CHECK(stagings().out.mark(st));  // no host sync: the staging buffer outlives the copy
     }
     return M3S_OK;
 }
@@ -791,6 +835,7 @@ struct Ctx {
     char* dyn = nullptr;
     size_t o_dense = 0, o_linv = 0, o_slot = 0;
     int chol_epoch = 0;  // dataflow factorisations enqueued in this call (chol_df.hip ready words)
+    bool may_timeout = false;  // a solver with bounded device-side waits ran (kFlagTimeout)
     template <typename T>
     T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
     template <typename T>
@@ -911,7 +956,7 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
         rc = c.alloc_dense(L.npad, (int)std::max<int64_t>(a.N - 1, 0));
         if (rc) return rc;
     }
-    char* h = g_stage_ws.get(hi - lo + sizeof(int) * nslot);
+    char* h = stagings().ws.get(hi - lo + sizeof(int) * nslot);
     M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
     std::memset(h, 0, L.ii_loc - lo);  // flags
     // M3S_GN_RAYCHECK=1: let the packed calib accumulate take the ray-constrained path
@@ -930,7 +975,7 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     put(L.grad_ptr, p.grad_ptr);
     put(L.grad_ent, p.grad_ent);
     std::memset(h + (L.ecnt - lo), 0, sizeof(int) * (size_t)a.E_local);  // (the kernel re-zeroes them)
-    M3S_HIP_CHECK(g_stage_ws.upload(c.ws + lo, h, L.sched - lo, c.st));
+    M3S_HIP_CHECK(stagings().ws.upload(c.ws + lo, h, L.sched - lo, c.st));
     if (early_pack) {
         rc = prepare_iterations(a, c);
         if (rc) return rc;
@@ -940,13 +985,13 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     // the accumulate's task records carry the edge's keyframes: one load, not three levels
     build_schedule(p.ii_loc, p.jj_loc, L.nchunks, reinterpret_cast<int*>(h + (L.sched - lo)));
     if (ntask > 0)
-        M3S_HIP_CHECK(g_stage_ws.upload(c.ws + L.sched, h + (L.sched - lo), hi - L.sched, c.st));
+        M3S_HIP_CHECK(stagings().ws.upload(c.ws + L.sched, h + (L.sched - lo), hi - L.sched, c.st));
     if (nslot) {  // the dense (npose x npose) slot table
         std::memcpy(h + (hi - lo), p.slotmap.data(), sizeof(int) * nslot);
         M3S_HIP_CHECK(hipMemcpyAsync(c.dyn + c.o_slot, h + (hi - lo), sizeof(int) * nslot,
                                      hipMemcpyHostToDevice, c.st));
     }
-    M3S_HIP_CHECK(g_stage_ws.mark(c.st));
+    M3S_HIP_CHECK(stagings().ws.mark(c.st));
     if (prof_host) {
         auto us = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
             return std::chrono::duration<double, std::micro>(y - x).count();
@@ -1054,6 +1099,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     const int npose = (int)(a.N - 1);
     int* flags = c.at<int>(L.flags);
     if (!c.sp.enabled) {
+        c.may_timeout = true;  // dense factorisation: chol_df's ready waits
         M3S_HIP_CHECK(launch_solve(c.st, c.at<double>(L.compact), c.dyn_at<int>(c.o_slot), c.plan.nblk,
                                    npose, 7 * npose, L.npad, c.dyn_at<double>(c.o_dense),
                                    c.dyn_at<double>(c.o_linv), c.at<double>(L.x), flags, ++c.chol_epoch));
@@ -1143,6 +1189,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     static const int coop_mode = env_int("M3S_SOLVE_COOP", 0);
     const bool coop = coop_mode != 0;
     if (coop) {
+        c.may_timeout = true;  // grid barriers
         SpCoopArgs ca{};
         ca.inl = sp.iptr(sp.i_inl);
         ca.tc3 = sp.iptr(sp.i_tc3);
@@ -1184,6 +1231,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         M3S_HIP_CHECK(launch_gn_solve(c.st, S));
         return M3S_OK;
     }
+    if (sp.ntail > 0) c.may_timeout = true;  // the core's dataflow factorisation (chol_df)
     M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
                                  sp.npad_tail, sp.dptr<double>(sp.o_dense), sp.dptr<double>(sp.o_linv),
                                  sp.dptr<double>(sp.o_xd), x, flags, ++c.chol_epoch));
@@ -1262,12 +1310,25 @@ int run(const m3s_gn_args& a) {
         g_prof.mark(c.st);
     }
     // (the per-call solver buffers are released by ~Ctx on this and every error path)
+    if (c.may_timeout && a.max_iter > 0) {
+        // a bounded device-side wait that gave up discarded that iteration's solve (dx = 0): an
+        // error, not a singular system (the reference's host Eigen solve cannot time out)
+        int* hf = reinterpret_cast<int*>(stagings().in.get(64));
+        M3S_REQUIRE(hf != nullptr, "gauss_newton: pinned host allocation failed");
+        M3S_HIP_CHECK(hipMemcpyAsync(hf, flags + kFlagTimeout, sizeof(int), hipMemcpyDeviceToHost, c.st));
+        M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+        if (hf[0] != 0) {
+            set_error("gauss_newton: a device-side wait of the factorisation timed out (the solve "
+                      "was discarded; not a singular system)");
+            return M3S_ERR_TIMEOUT;
+        }
+    }
     if (env_int("M3S_GN_DEBUG_FLAGS", 0)) {  // diagnostics: the device flags after the call
         int hf[kNumFlags];
         M3S_HIP_CHECK(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c.st));
         M3S_HIP_CHECK(hipStreamSynchronize(c.st));
-        fprintf(stderr, "gn flags: done %d fail %d not_ray %d packed %d\n", hf[kFlagDone], hf[kFlagFail],
-                hf[kFlagNotRay], (int)c.packed);
+        fprintf(stderr, "gn flags: done %d fail %d not_ray %d timeout %d packed %d\n", hf[kFlagDone],
+                hf[kFlagFail], hf[kFlagNotRay], hf[kFlagTimeout], (int)c.packed);
     }
     return M3S_OK;
 }
@@ -1280,6 +1341,21 @@ using namespace m3s;
 extern "C" const char* m3s_last_error(void) { return m3s::get_error(); }
 
 extern "C" const char* m3s_version(void) { return "m3s 0.1.0 gfx950"; }
+
+extern "C" void m3s_shutdown(void) {
+    HostResources& r = host_resources();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (r.shut) return;
+    r.shut = true;
+    for (auto& it : r.items) it.second(it.first);
+    r.items.clear();
+}
+
+namespace {
+// Registered when the library is loaded: after the HIP runtime's own exit-time teardown (and a
+// profiler's) was registered, so m3s_shutdown runs before them.
+__attribute__((constructor)) void m3s_register_shutdown() { std::atexit(m3s_shutdown); }
+}  // namespace
 
 extern "C" size_t m3s_gn_workspace_bytes(int mode, int64_t N, int64_t HW, int64_t E_total,
                                          int64_t E_local) {

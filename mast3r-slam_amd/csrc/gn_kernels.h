@@ -18,6 +18,8 @@ constexpr int kCholTile = 64;  // dense Cholesky tile
 constexpr int kFlagDone = 0;   // set once ||dx|| < delta_thresh (skips later iterations)
 constexpr int kFlagFail = 1;   // set by the factorisation when a pivot <= 0
 constexpr int kFlagNotRay = 2; // calib: some Xs point is not its pixel's ray times its depth
+constexpr int kFlagTimeout = 3; // sticky for the call: a bounded device-side wait gave up (chol_df
+                                // ready word, grid barrier); the driver returns M3S_ERR_TIMEOUT
 constexpr int kFlagBarCount = 4;  // grid barrier of the all-rounds launch: arrivals
 constexpr int kFlagBarGen = 5;    // ... and its generation
 constexpr int kNumFlags = 16;
@@ -139,7 +141,7 @@ struct SpCoopArgs {
     double *A, *b, *Lstore, *W, *y, *Hd;
     int* flags;
     int nrounds, ntail, npad;
-    int coop;  // 1: hipLaunchCooperativeKernel + cooperative-groups grid sync; 0: own barrier
+    int coop;  // 1: cooperative-groups grid sync; 0: own barrier (both as a cooperative launch)
 };
 hipError_t launch_sp_rounds_coop(hipStream_t st, const SpCoopArgs& args);
 hipError_t launch_sp_round(hipStream_t st, const int* inl, int ibeg, int nbt, int nrt, const int* tc3,

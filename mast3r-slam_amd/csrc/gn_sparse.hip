@@ -263,7 +263,9 @@ __global__ __launch_bounds__(256) void sp_tail_fill_kernel(const double* __restr
 // CU): arrival counter + generation word in the flags area.  Release = the arrival atomic
 // (writes back this XCD's L2), acquire = a fence after the generation moved (invalidates L1/L2),
 // so blocks written in one round are read fresh in the next on any XCD.  The spin is bounded
-// (~0.1 s): a workgroup that never arrives fails the solve instead of hanging the GPU.
+// (~0.1 s): a workgroup that never arrives fails the solve and raises the sticky timeout flag
+// (reported by the driver as M3S_ERR_TIMEOUT) instead of hanging the GPU; the caller then
+// leaves the launch (the arrival counter is no longer consistent).
 template <bool FENCED>
 __device__ __forceinline__ void grid_barrier(int* __restrict__ flags, unsigned nwg) {
     if constexpr (!FENCED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my write-through stores landed
@@ -282,7 +284,8 @@ __device__ __forceinline__ void grid_barrier(int* __restrict__ flags, unsigned n
             while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1 << 22)) {
-                    flags[kFlagFail] = 1;
+                    __hip_atomic_store(flags + kFlagTimeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(flags + kFlagFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
@@ -302,10 +305,14 @@ __global__ __launch_bounds__(64) void sp_rounds_coop_kernel(SpCoopArgs a) {
         for (int t = blockIdx.x; t < nbt + nrt; t += gridDim.x)
             sp_round_target<true>(a.inl + (int64_t)(tbeg + rbeg + t) * kSpRec, t < nbt, a.tc3, a.rc4, nullptr,
                                   a.A, a.b, a.Lstore, a.W, a.y, a.flags, sR, sS);
-        if (a.coop)
+        if (a.coop) {
             cooperative_groups::this_grid().sync();
-        else
+        } else {
             grid_barrier<false>(a.flags, gridDim.x);
+            // a timed-out barrier leaves the arrival counter inconsistent: abandon the launch
+            // (every workgroup reaches this test after its own barrier wait)
+            if (__hip_atomic_load(a.flags + kFlagTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        }
     }
     if (a.ntail > 0 && a.Hd) sp_tail_fill<true>(a.A, a.b, a.tmap, a.tail, a.ntail, a.npad, a.Hd);
 }
@@ -342,13 +349,11 @@ hipError_t launch_sp_rounds_coop(hipStream_t st, const SpCoopArgs& args) {
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(ncu * std::max(per, 1), 256));  // <= one workgroup per CU
     }
+    // both barrier flavours need every workgroup resident at once: always a cooperative launch
+    // (it refuses a grid the device cannot hold); `coop` only picks the barrier implementation
     SpCoopArgs a = args;
-    if (a.coop) {
-        void* kargs[] = {&a};
-        return hipLaunchCooperativeKernel((const void*)sp_rounds_coop_kernel, dim3(grid), dim3(64), kargs, 0, st);
-    }
-    hipLaunchKernelGGL(sp_rounds_coop_kernel, dim3(grid), dim3(64), 0, st, a);
-    return hipGetLastError();
+    void* kargs[] = {&a};
+    return hipLaunchCooperativeKernel((const void*)sp_rounds_coop_kernel, dim3(grid), dim3(64), kargs, 0, st);
 }
 
 hipError_t launch_sp_back(hipStream_t st, int nnodes, const int* nodes, const int* fptr,

@@ -13,6 +13,13 @@ namespace m3s {
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 const char* get_error();
 
+// Host resources (pinned buffers, events) cached per host thread are released by m3s_shutdown()
+// -- registered with atexit when the library is loaded, and by the Python module -- never by
+// static or thread-local destructors: those run inside exit(), where the HIP runtime or a
+// profiler's interception layer may already be finalised.  `release(obj)` frees obj's HIP
+// resources; it is called once, under the registry's lock, with the HIP runtime alive.
+void register_host_resource(void* obj, void (*release)(void*));
+
 }  // namespace m3s
 
 #define M3S_HIP_CHECK(expr)                                                              \

@@ -5,9 +5,11 @@
 //   refine_matches  : dilated-window descriptor argmax with c10::Half per-op rounding
 //                     (reference matching_kernels.cu:25-81)
 //
-// Parity contract: bit-exact with the CPU oracle (oracle/m3s_oracle.c).  FMA contraction
-// is OFF for this whole file (also -ffp-contract=off in the Makefile) and every double
-// literal promotion of the reference source is an explicit double operation.
+// Parity contract: bit-exact with the CPU oracle (oracle/m3s_oracle.c) under each FMA-contraction
+// convention (contract.h; M3S_CONTRACT_NVCC, the reference build's, by default).  The file is
+// compiled with contraction OFF (-ffp-contract=off and the pragma below): every fused operation
+// is an explicit helper call placed where nvcc --fmad=true fuses the reference source, and every
+// double literal promotion of the reference source is an explicit double operation.
 //
 // Launch shape (MI355X-first, not the reference's 16-thread blocks): 256-thread
 // workgroups (4 wave64s), one point per lane, consecutive lanes on consecutive pixels
@@ -20,9 +22,14 @@
 #include <cstdlib>
 
 #include "../../include/m3s_backend.h"
+#include "contract.h"
 #include "m3s_common.h"
 
 #pragma clang fp contract(off)
+
+using m3s::cdot3;
+using m3s::cmad;
+using m3s::cmm;
 
 namespace {
 
@@ -60,14 +67,15 @@ __device__ __forceinline__ Bilin make_bilin(const float* __restrict__ img, int W
     return b;
 }
 
+// w11 r11 + w12 r12 + w21 r21 + w22 r22, left to right (matching_kernels.cu:174-183): under nvcc
+// the first two products form one fma and the last two are fused into the running sum
+template <int CM>
 __device__ __forceinline__ float interp(const Bilin& b, int j) {
-    const float a = b.w11 * b.r11[j];
-    const float c = b.w12 * b.r12[j];
-    const float d = b.w21 * b.r21[j];
-    const float e = b.w22 * b.r22[j];
-    return ((a + c) + d) + e;
+    return cmad<CM>(b.w22, b.r22[j], cmad<CM>(b.w21, b.r21[j], cmm<CM>(b.w11, b.r11[j], b.w12, b.r12[j])));
 }
 
+// matching_kernels.cu:119-275 under contraction convention CM
+template <int CM>
 __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
     const float* __restrict__ rays, const float* __restrict__ pts, const float* __restrict__ p_init,
     float* __restrict__ p_new, uint8_t* __restrict__ converged, int H, int W, int64_t N,
@@ -87,39 +95,37 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
     uint8_t conv = 0;
     for (int it = 0; it < max_iter; it++) {
         const Bilin bl = make_bilin(img, W, u, v);
-        float r0 = interp(bl, 0), r1 = interp(bl, 1), r2 = interp(bl, 2);
-        const float gx0 = interp(bl, 3), gx1 = interp(bl, 4), gx2 = interp(bl, 5);
-        const float gy0 = interp(bl, 6), gy1 = interp(bl, 7), gy2 = interp(bl, 8);
+        const float r0 = interp<CM>(bl, 0), r1 = interp<CM>(bl, 1), r2 = interp<CM>(bl, 2);
+        const float gx0 = interp<CM>(bl, 3), gx1 = interp<CM>(bl, 4), gx2 = interp<CM>(bl, 5);
+        const float gy0 = interp<CM>(bl, 6), gy1 = interp<CM>(bl, 7), gy2 = interp<CM>(bl, 8);
 
-        const float r_norm = sqrtf((r0 * r0 + r1 * r1) + r2 * r2);
-        const float r_norm_inv = inv_d(r_norm);
-        r0 *= r_norm_inv;
-        r1 *= r_norm_inv;
-        r2 *= r_norm_inv;
-        const float e0 = r0 - px, e1 = r1 - py, e2 = r2 - pz;
-        const float cost = (e0 * e0 + e1 * e1) + e2 * e2;
+        // :186-198: r *= 1/|r| then err = r - pts (the scaled ray feeds only the subtraction: fused)
+        const float r_norm_inv = inv_d(sqrtf(cdot3<CM>(r0, r0, r1, r1, r2, r2)));
+        const float e0 = cmad<CM>(r0, r_norm_inv, -px), e1 = cmad<CM>(r1, r_norm_inv, -py),
+                    e2 = cmad<CM>(r2, r_norm_inv, -pz);
+        const float cost = cdot3<CM>(e0, e0, e1, e1, e2, e2);
 
-        float A00 = (gx0 * gx0 + gx1 * gx1) + gx2 * gx2;
-        const float A01 = (gx0 * gy0 + gx1 * gy1) + gx2 * gy2;
-        float A11 = (gy0 * gy0 + gy1 * gy1) + gy2 * gy2;
-        const float b0 = -((e0 * gx0 + e1 * gx1) + e2 * gx2);
-        const float b1 = -((e0 * gy0 + e1 * gy1) + e2 * gy2);
+        // :202-210
+        float A00 = cdot3<CM>(gx0, gx0, gx1, gx1, gx2, gx2);
+        const float A01 = cdot3<CM>(gx0, gy0, gx1, gy1, gx2, gy2);
+        float A11 = cdot3<CM>(gy0, gy0, gy1, gy1, gy2, gy2);
+        const float b0 = -cdot3<CM>(e0, gx0, e1, gx1, e2, gx2);
+        const float b1 = -cdot3<CM>(e0, gy0, e1, gy1, e2, gy2);
         A00 += lambda;
         A11 += lambda;
 
-        const float det_inv = inv_d(A00 * A11 - A01 * A01);
-        const float delta_u = det_inv * (A11 * b0 - A01 * b1);
-        const float delta_v = det_inv * ((-A01) * b0 + A00 * b1);
+        // :213-219: u + det_inv * (...) is a fused multiply-add under nvcc
+        const float det_inv = inv_d(cmm<CM>(A00, A11, -A01, A01));
+        const float u_new = clamp_ref(cmad<CM>(det_inv, cmm<CM>(A11, b0, -A01, b1), u), 1.0f, umax);
+        const float v_new = clamp_ref(cmad<CM>(det_inv, cmm<CM>(-A01, b0, A00, b1), v), 1.0f, vmax);
 
-        const float u_new = clamp_ref(u + delta_u, 1.0f, umax);
-        const float v_new = clamp_ref(v + delta_v, 1.0f, vmax);
-
+        // :225-256 the cost at the new pixel (ray channels only)
         const Bilin bn = make_bilin(img, W, u_new, v_new);
-        const float t0 = interp(bn, 0), t1 = interp(bn, 1), t2 = interp(bn, 2);
-        const float n2 = sqrtf((t0 * t0 + t1 * t1) + t2 * t2);
-        const float n2_inv = inv_d(n2);
-        const float f0 = t0 * n2_inv - px, f1 = t1 * n2_inv - py, f2 = t2 * n2_inv - pz;
-        const float new_cost = (f0 * f0 + f1 * f1) + f2 * f2;
+        const float t0 = interp<CM>(bn, 0), t1 = interp<CM>(bn, 1), t2 = interp<CM>(bn, 2);
+        const float n2_inv = inv_d(sqrtf(cdot3<CM>(t0, t0, t1, t1, t2, t2)));
+        const float f0 = cmad<CM>(t0, n2_inv, -px), f1 = cmad<CM>(t1, n2_inv, -py),
+                    f2 = cmad<CM>(t2, n2_inv, -pz);
+        const float new_cost = cdot3<CM>(f0, f0, f1, f1, f2, f2);
 
         if (new_cost < cost) {
             u = u_new;
@@ -878,6 +884,16 @@ __device__ __forceinline__ float zero_score<float>() { return 0.0f; }
 template <>
 __device__ __forceinline__ double zero_score<double>() { return 0.0; }
 
+// `score += D21[k] * D11[k]` (matching_kernels.cu:62): c10::Half rounds the product to half
+// before the add (operator* returns Half), so nothing fuses; float / double are fused by nvcc
+// --fmad=true (contract.h, M3S_CONTRACT_NVCC)
+__device__ __forceinline__ half_t acc_score(half_t s, half_t a, half_t b) {
+    const half_t p = a * b;
+    return s + p;
+}
+__device__ __forceinline__ float acc_score(float s, float a, float b) { return __builtin_fmaf(a, b, s); }
+__device__ __forceinline__ double acc_score(double s, double a, double b) { return __builtin_fma(a, b, s); }
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void refine_generic_kernel(
     const T* __restrict__ D11, const T* __restrict__ D21, const int64_t* __restrict__ p1,
@@ -902,10 +918,7 @@ __global__ __launch_bounds__(kBlock) void refine_generic_kernel(
                 if (inside_image(u, v, W, H)) {
                     const T* row = img + (v * W + u) * F;
                     T score = zero_score<T>();
-                    for (int64_t k = 0; k < F; k++) {
-                        const T p = q[k] * row[k];
-                        score = score + p;
-                    }
+                    for (int64_t k = 0; k < F; k++) score = acc_score(score, q[k], row[k]);
                     if (score > max_score) {
                         max_score = score;
                         u_new = u;
@@ -928,6 +941,16 @@ extern "C" int m3s_iter_proj(const float* rays, const float* pts, const float* p
                              float* p_new, uint8_t* converged, int64_t B, int64_t H, int64_t W,
                              int64_t N, int max_iter, float lambda_init, float cost_thresh,
                              void* stream) {
+    return m3s_iter_proj_ex(rays, pts, p_init, p_new, converged, B, H, W, N, max_iter, lambda_init,
+                            cost_thresh, M3S_CONTRACT_DEFAULT, stream);
+}
+
+extern "C" int m3s_iter_proj_ex(const float* rays, const float* pts, const float* p_init,
+                                float* p_new, uint8_t* converged, int64_t B, int64_t H, int64_t W,
+                                int64_t N, int max_iter, float lambda_init, float cost_thresh,
+                                int contract, void* stream) {
+    M3S_REQUIRE(contract >= M3S_CONTRACT_OFF && contract <= M3S_CONTRACT_NVCC_RIGHT,
+                "iter_proj: unknown contraction convention %d", contract);
     M3S_REQUIRE(B >= 0 && N >= 0, "iter_proj: negative sizes");
     M3S_REQUIRE(H >= 3 && W >= 3, "iter_proj: ray image must be at least 3x3 (got %lldx%lld)",
                 (long long)H, (long long)W);
@@ -935,9 +958,14 @@ extern "C" int m3s_iter_proj(const float* rays, const float* pts, const float* p
     const int64_t total = B * N;
     if (total == 0) return M3S_OK;
     M3S_REQUIRE(rays && pts && p_init && p_new && converged, "iter_proj: null pointer");
-    hipLaunchKernelGGL(iter_proj_kernel, dim3(grid_for(total)), dim3(kBlock), 0,
-                       (hipStream_t)stream, rays, pts, p_init, p_new, converged, (int)H, (int)W, N,
-                       total, max_iter, lambda_init, cost_thresh);
+#define M3S_IP(CM)                                                                                      \
+    hipLaunchKernelGGL(iter_proj_kernel<CM>, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream, \
+                       rays, pts, p_init, p_new, converged, (int)H, (int)W, N, total, max_iter,            \
+                       lambda_init, cost_thresh)
+    if (contract == M3S_CONTRACT_OFF) M3S_IP(M3S_CONTRACT_OFF);
+    else if (contract == M3S_CONTRACT_NVCC) M3S_IP(M3S_CONTRACT_NVCC);
+    else M3S_IP(M3S_CONTRACT_NVCC_RIGHT);
+#undef M3S_IP
     M3S_LAUNCH_CHECK();
     return M3S_OK;
 }

@@ -362,14 +362,24 @@ __global__ __launch_bounds__(64) void track_final_kernel(const float* __restrict
     }
 }
 
-// Pinned host copy of the state flags, one per host thread.
+// Pinned host copy of the state flags, one per host thread, released by m3s_shutdown (no
+// exit-time destructor, m3s_common.h).
 struct TrkFlags {
     TrackState* h = nullptr;
-    ~TrkFlags() {
-        if (h) (void)hipHostFree(h);
+    static void release(void* p) {
+        TrkFlags* f = static_cast<TrkFlags*>(p);
+        if (f->h) (void)hipHostFree(f->h);
+        f->h = nullptr;
     }
 };
-thread_local TrkFlags g_trk_flags;
+thread_local TrkFlags* t_trk_flags = nullptr;
+TrkFlags& trk_flags() {
+    if (!t_trk_flags) {
+        t_trk_flags = new TrkFlags;
+        register_host_resource(t_trk_flags, &TrkFlags::release);
+    }
+    return *t_trk_flags;
+}
 
 }  // namespace
 }  // namespace m3s
@@ -417,8 +427,8 @@ extern "C" int m3s_track_sim3(const m3s_track_args* args) {
     P.delta_norm = (float)a.delta_norm;
     P.max_iters = a.max_iters;
 
-    if (!g_trk_flags.h)
-        M3S_HIP_CHECK(hipHostMalloc((void**)&g_trk_flags.h, sizeof(TrackState), hipHostMallocDefault));
+    if (!trk_flags().h)
+        M3S_HIP_CHECK(hipHostMalloc((void**)&trk_flags().h, sizeof(TrackState), hipHostMallocDefault));
     hipLaunchKernelGGL(track_init_kernel, dim3(1), dim3(64), 0, st, a.T_WCf, a.T_WCk, state, a.info);
     M3S_LAUNCH_CHECK();
     const int every = a.check_every > 0 ? a.check_every : 4;
@@ -436,10 +446,10 @@ extern "C" int m3s_track_sim3(const m3s_track_args* args) {
                            a.info, a.cost);
         M3S_LAUNCH_CHECK();
         if ((it + 1) % every == 0 && it + 1 < a.max_iters) {
-            M3S_HIP_CHECK(hipMemcpyAsync(g_trk_flags.h, state, sizeof(TrackState),
+            M3S_HIP_CHECK(hipMemcpyAsync(trk_flags().h, state, sizeof(TrackState),
                                          hipMemcpyDeviceToHost, st));
             M3S_HIP_CHECK(hipStreamSynchronize(st));
-            if (g_trk_flags.h->done) break;
+            if (trk_flags().h->done) break;
         }
     }
     hipLaunchKernelGGL(track_final_kernel, dim3(1), dim3(64), 0, st, a.T_WCk, state, a.T_WCf_out,

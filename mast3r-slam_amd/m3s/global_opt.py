@@ -373,9 +373,15 @@ class DeviceFactorGraph(FactorGraph):
         else:
             s0, s1 = c["sigma_ray"], c["sigma_dist"]
         idx_f, valid_f, Q_f = self.edges.forward()
+        # the op pins only pose 0 (num_fix = 1, gn_kernels.cu:741); the reference writes back
+        # T_WCs[pin:] only (global_opt.py:158/213): with pin > 1 the store's rows 1..pin-1 must
+        # keep their values when the op updates the store in place
+        keep = pose_data[1:pin].clone() if in_place and pin > 1 else None
         mast3r_slam_backends._run_gn(
             mode, pose_data, Xs, Cs, ii, jj, idx_f, valid_f, Q_f, c["max_iters"], c["delta_norm"],
             s0, s1, c["C_conf"], c["Q_conf"], second_half=self.edges.backward(), **kw)
+        if keep is not None:
+            pose_data[1:pin] = keep
         if not in_place:
             self.frames.update_T_WCs(PoseBatch(pose_data[pin:, None]), unique_kf_idx[pin:])
 

@@ -52,7 +52,9 @@ def prep_for_iter_proj(X11, X21, idx_1_to_2_init):
     return rays_with_grad, pts3d_norm, p_init
 
 
-def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, fused=None):
+def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, fused=None, contract=None):
+    """``contract``: iter_proj's FMA-contraction convention (default: the reference build's,
+    mast3r_slam_backends.CONTRACT)."""
     cfg = (cfg if cfg is not None else _global_config)["matching"]
     b, h, w = X21.shape[:3]
     device = X11.device
@@ -63,7 +65,7 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, fus
             X11.contiguous(), X21.contiguous(), D11.contiguous(), D21.contiguous(),
             None if idx_1_to_2_init is None else idx_1_to_2_init.contiguous(),
             cfg["max_iter"], cfg["lambda_init"], cfg["convergence_thresh"], cfg["dist_thresh"],
-            cfg["radius"], cfg["dilation_max"],
+            cfg["radius"], cfg["dilation_max"], contract=contract,
         )
         return idx_1_to_2, valid
 
@@ -71,6 +73,7 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, fus
     p1, valid_proj2 = mast3r_slam_backends.iter_proj(
         rays_with_grad, pts3d_norm, p_init,
         cfg["max_iter"], cfg["lambda_init"], cfg["convergence_thresh"],
+        **({} if contract is None else {"contract": contract}),
     )
     p1 = p1.long()
 

@@ -12,6 +12,7 @@ import time.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 
@@ -51,8 +52,13 @@ _f = ctypes.c_float
 _i = ctypes.c_int
 
 lib.m3s_last_error.restype = ctypes.c_char_p
+lib.m3s_shutdown.restype = None
+# pinned staging buffers / events are released here, while the HIP runtime is alive (not by
+# exit-time destructors inside the library)
+atexit.register(lib.m3s_shutdown)
 lib.m3s_version.restype = ctypes.c_char_p
 lib.m3s_iter_proj.argtypes = [_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _vp]
+lib.m3s_iter_proj_ex.argtypes = [_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _i, _vp]
 lib.m3s_refine_matches_f16.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_refine_matches_f32.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_refine_matches_f64.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
@@ -60,8 +66,21 @@ lib.m3s_refine_mfma_stats.argtypes = [_i, _vp]
 lib.m3s_refine_mfma_stats.restype = None
 lib.m3s_match_workspace_bytes.argtypes = [_c_int64] * 4
 lib.m3s_match_workspace_bytes.restype = ctypes.c_size_t
-lib.m3s_match_iterative_proj.argtypes = ([_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _f, _i, _i]
+lib.m3s_match_iterative_proj.argtypes = ([_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _f, _i, _i, _i]
                                          + [_vp, _vp, _vp, ctypes.c_size_t, _vp])
+
+# FMA-contraction convention of the parity paths (include/m3s_backend.h M3S_CONTRACT_*): the
+# reference's nvcc build fuses multiply-adds ("nvcc": the left product of a two-product sum, the
+# default); "nvcc_right" and "off" are variants for measuring the convention
+CONTRACT = {"off": 0, "nvcc": 1, "nvcc_right": 2}
+
+
+def _contract(c):
+    if c is None:
+        return CONTRACT["nvcc"]
+    if c not in CONTRACT:
+        raise ValueError(f"unknown contraction convention {c!r} (expected one of {sorted(CONTRACT)})")
+    return CONTRACT[c]
 lib.m3s_gn_workspace_bytes.restype = ctypes.c_size_t
 lib.m3s_gn_workspace_bytes.argtypes = [_i, _c_int64, _c_int64, _c_int64, _c_int64]
 
@@ -201,8 +220,11 @@ def _ptr(t):
 # ---------------------------------------------------------------------------------
 
 
-def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh):
-    """gn.cpp:84-99 / matching_kernels.cu:279-316 -> [p_new f32[B,N,2], converged bool[B,N]]."""
+def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh,
+              contract=None):
+    """gn.cpp:84-99 / matching_kernels.cu:279-316 -> [p_new f32[B,N,2], converged bool[B,N]].
+
+    ``contract``: FMA-contraction convention (``CONTRACT``; default the reference build's)."""
     _check(rays_img_with_grad, "rays_img_with_grad", torch.float32, 4)
     _check(pts_3d_norm, "pts_3d_norm", torch.float32, 3)
     _check(p_init, "p_init", torch.float32, 3)
@@ -218,10 +240,10 @@ def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, co
     p_new = torch.zeros((Bp, N, 2), dtype=p_init.dtype, device=dev)
     converged = torch.zeros((Bp, N), dtype=torch.bool, device=dev)
     with torch.cuda.device(dev):
-        rc = lib.m3s_iter_proj(
+        rc = lib.m3s_iter_proj_ex(
             _ptr(rays_img_with_grad), _ptr(pts_3d_norm), _ptr(p_init), _ptr(p_new),
             _ptr(converged), B, H, W, N, int(max_iter), float(lambda_init),
-            float(cost_thresh), _stream(dev),
+            float(cost_thresh), _contract(contract), _stream(dev),
         )
     _raise(rc, "iter_proj")
     return [p_new, converged]
@@ -261,7 +283,7 @@ def refine_mfma_stats(enable=True):
 
 
 def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init, max_iter, lambda_init, cost_thresh,
-                         dist_thresh, radius, dilation_max):
+                         dist_thresh, radius, dilation_max, contract=None):
     """The whole Python matching caller (matching.py:52-90) as one op: prep_for_iter_proj,
     iter_proj, ``p.long()``, the occlusion test on the pre-refine pixels, refine_matches on the
     ``.half()`` descriptors and ``pixel_to_lin`` -> [idx i64[B,H*W], valid bool[B,H*W,1]].
@@ -288,7 +310,8 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init, max_iter, lambda_i
         rc = lib.m3s_match_iterative_proj(
             _ptr(X11), _ptr(X21), _ptr(D11), _ptr(D21), _ptr(idx_1_to_2_init), B, H, W, F,
             int(max_iter), float(lambda_init), float(cost_thresh), float(dist_thresh), int(radius),
-            int(dilation_max), _ptr(idx), _ptr(valid), _ptr(ws), nbytes, _stream(dev),
+            int(dilation_max), _contract(contract), _ptr(idx), _ptr(valid), _ptr(ws), nbytes,
+            _stream(dev),
         )
     _raise(rc, "match_iterative_proj")
     return [idx, valid]

@@ -27,6 +27,14 @@ int oracle_num_threads(void) {
 #endif
 }
 
+void oracle_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 /* ------------------------------------------------------------------------ */
 /* fp16 (c10::Half) helpers                                                 */
 /* ------------------------------------------------------------------------ */
@@ -84,6 +92,30 @@ static inline uint16_t hadd(uint16_t a, uint16_t b) {
 }
 
 /* ------------------------------------------------------------------------ */
+/* FMA contraction convention of the reference build                        */
+/* ------------------------------------------------------------------------ */
+/* The reference is compiled by nvcc -O3 (setup.py:29-37, so --fmad=true): a multiply feeding an
+ * add is fused into one fma; of `a*b + c*d` the LEFT product is fused (ORACLE_CONTRACT_NVCC,
+ * LLVM / NVPTX combine order), ORACLE_CONTRACT_NVCC_RIGHT fuses the right one, ORACLE_CONTRACT_OFF
+ * is multiply-then-add.  This file is compiled with -ffp-contract=off: these helpers are the only
+ * fused operations.  (The same helpers as mast3r-slam_amd/csrc/contract.h, restated in C.) */
+static int g_contract = ORACLE_CONTRACT_NVCC; /* the GN restatement's convention */
+void oracle_set_contract(int cm) { g_contract = cm; }
+int oracle_get_contract(void) { return g_contract; }
+
+static inline float cmad(int cm, float a, float b, float c) { /* a*b + c */
+    return cm != ORACLE_CONTRACT_OFF ? fmaf(a, b, c) : a * b + c;
+}
+static inline float cmm(int cm, float a, float b, float c, float d) { /* a*b + c*d */
+    if (cm == ORACLE_CONTRACT_OFF) return a * b + c * d;
+    if (cm == ORACLE_CONTRACT_NVCC) return fmaf(a, b, c * d);
+    return fmaf(c, d, a * b);
+}
+static inline float cdot3(int cm, float a0, float b0, float a1, float b1, float a2, float b2) {
+    return cmad(cm, a2, b2, cmm(cm, a0, b0, a1, b1)); /* (a0 b0 + a1 b1) + a2 b2 */
+}
+
+/* ------------------------------------------------------------------------ */
 /* iter_proj  (matching_kernels.cu:119-275)                                 */
 /* ------------------------------------------------------------------------ */
 
@@ -91,7 +123,7 @@ static inline uint16_t hadd(uint16_t a, uint16_t b) {
 static inline float clampf_ref(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
 /* matching_kernels.cu:155-183 (bilinear interpolation of C channels) */
-static inline void bilinear(const float* img, int64_t W, float u, float v, int C, float* out) {
+static inline void bilinear(int cm, const float* img, int64_t W, float u, float v, int C, float* out) {
     int u11 = (int)floorf(u);
     int v11 = (int)floorf(v);
     float du = u - (float)u11;
@@ -106,19 +138,15 @@ static inline void bilinear(const float* img, int64_t W, float u, float v, int C
     const float* r12 = img + ((int64_t)(v11 + 1) * W + u11) * 9;
     const float* r21 = img + ((int64_t)v11 * W + (u11 + 1)) * 9;
     const float* r22 = img + ((int64_t)v11 * W + u11) * 9;
-    for (int j = 0; j < C; j++) {
-        float a = w11 * r11[j];
-        float b = w12 * r12[j];
-        float c = w21 * r21[j];
-        float d = w22 * r22[j];
-        out[j] = ((a + b) + c) + d;
-    }
+    /* ((w11 r11 + w12 r12) + w21 r21) + w22 r22 */
+    for (int j = 0; j < C; j++)
+        out[j] = cmad(cm, w22, r22[j], cmad(cm, w21, r21[j], cmm(cm, w11, r11[j], w12, r12[j])));
 }
 
 void oracle_iter_proj(const float* rays, const float* pts, const float* p_init,
                       float* p_new, uint8_t* converged,
                       int64_t B, int64_t H, int64_t W, int64_t N,
-                      int max_iter, float lambda_init, float cost_thresh) {
+                      int max_iter, float lambda_init, float cost_thresh, int cm) {
     const int64_t total = B * N;
 #pragma omp parallel for schedule(static)
     for (int64_t g = 0; g < total; g++) {
@@ -133,41 +161,39 @@ void oracle_iter_proj(const float* rays, const float* pts, const float* p_init,
         uint8_t conv = 0; /* torch::zeros init (:300-301) */
         for (int i = 0; i < max_iter; i++) {
             float s[9];
-            bilinear(img, W, u, v, 9, s);
-            float r0 = s[0], r1 = s[1], r2 = s[2];
+            bilinear(cm, img, W, u, v, 9, s);
+            const float r0 = s[0], r1 = s[1], r2 = s[2];
             const float gx0 = s[3], gx1 = s[4], gx2 = s[5];
             const float gy0 = s[6], gy1 = s[7], gy2 = s[8];
-            /* :186-191 normalise */
-            float r_norm = sqrtf((r0 * r0 + r1 * r1) + r2 * r2);
-            float r_norm_inv = (float)(1.0 / (double)r_norm);
-            r0 *= r_norm_inv;
-            r1 *= r_norm_inv;
-            r2 *= r_norm_inv;
-            /* :194-198 error + cost */
-            float e0 = r0 - px, e1 = r1 - py, e2 = r2 - pz;
-            float cost = (e0 * e0 + e1 * e1) + e2 * e2;
+            /* :186-198 normalise, error (r *= inv; err = r - pts: the product feeds the
+             * subtraction, fused under nvcc), cost */
+            const float r_norm = sqrtf(cdot3(cm, r0, r0, r1, r1, r2, r2));
+            const float r_norm_inv = (float)(1.0 / (double)r_norm);
+            const float e0 = cmad(cm, r0, r_norm_inv, -px);
+            const float e1 = cmad(cm, r1, r_norm_inv, -py);
+            const float e2 = cmad(cm, r2, r_norm_inv, -pz);
+            const float cost = cdot3(cm, e0, e0, e1, e1, e2, e2);
             /* :202-210 normal equations */
-            float A00 = (gx0 * gx0 + gx1 * gx1) + gx2 * gx2;
-            float A01 = (gx0 * gy0 + gx1 * gy1) + gx2 * gy2;
-            float A11 = (gy0 * gy0 + gy1 * gy1) + gy2 * gy2;
-            float b0 = -((e0 * gx0 + e1 * gx1) + e2 * gx2);
-            float b1 = -((e0 * gy0 + e1 * gy1) + e2 * gy2);
+            float A00 = cdot3(cm, gx0, gx0, gx1, gx1, gx2, gx2);
+            const float A01 = cdot3(cm, gx0, gy0, gx1, gy1, gx2, gy2);
+            float A11 = cdot3(cm, gy0, gy0, gy1, gy1, gy2, gy2);
+            const float b0 = -cdot3(cm, e0, gx0, e1, gx1, e2, gx2);
+            const float b1 = -cdot3(cm, e0, gy0, e1, gy1, e2, gy2);
             A00 += lambda;
             A11 += lambda;
-            /* :213-215 */
-            float det_inv = (float)(1.0 / (double)(A00 * A11 - A01 * A01));
-            float delta_u = det_inv * (A11 * b0 - A01 * b1);
-            float delta_v = det_inv * ((-A01) * b0 + A00 * b1);
-            /* :218-221 */
-            float u_new = clampf_ref(u + delta_u, 1.0f, (float)(W - 2));
-            float v_new = clampf_ref(v + delta_v, 1.0f, (float)(H - 2));
+            /* :213-221  u + det_inv * (...) fused under nvcc */
+            const float det_inv = (float)(1.0 / (double)cmm(cm, A00, A11, -A01, A01));
+            const float u_new = clampf_ref(cmad(cm, det_inv, cmm(cm, A11, b0, -A01, b1), u), 1.0f, (float)(W - 2));
+            const float v_new = clampf_ref(cmad(cm, det_inv, cmm(cm, -A01, b0, A00, b1), v), 1.0f, (float)(H - 2));
             /* :225-256 cost at the new pixel (ray channels only) */
             float t[3];
-            bilinear(img, W, u_new, v_new, 3, t);
-            float n2 = sqrtf((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2]);
-            float n2_inv = (float)(1.0 / (double)n2);
-            float f0 = t[0] * n2_inv - px, f1 = t[1] * n2_inv - py, f2 = t[2] * n2_inv - pz;
-            float new_cost = (f0 * f0 + f1 * f1) + f2 * f2;
+            bilinear(cm, img, W, u_new, v_new, 3, t);
+            const float n2 = sqrtf(cdot3(cm, t[0], t[0], t[1], t[1], t[2], t[2]));
+            const float n2_inv = (float)(1.0 / (double)n2);
+            const float f0 = cmad(cm, t[0], n2_inv, -px);
+            const float f1 = cmad(cm, t[1], n2_inv, -py);
+            const float f2 = cmad(cm, t[2], n2_inv, -pz);
+            const float new_cost = cdot3(cm, f0, f0, f1, f1, f2, f2);
             /* :259-268  lambda *= 0.1 is a DOUBLE multiply (0.1 != 0.1f) */
             if (new_cost < cost) {
                 u = u_new;
@@ -314,8 +340,9 @@ void oracle_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
 /* refine_matches_kernel<float> / <double>: the same loop in the accumulator type T, with
  * max_score starting at numeric_limits<T>::min() (specialised for float and double: FLT_MIN,
  * DBL_MIN).  matching_kernels.cu:25-81, dispatched by AT_DISPATCH_FLOATING_TYPES_AND_HALF
- * (:103). */
-#define ORACLE_REFINE_REAL(NAME, T, MIN_INIT)                                               \
+ * (:103).  `score += D21 * D11` is one fused multiply-add per term in the nvcc build
+ * (ORACLE_CONTRACT_NVCC; c10::Half's operator* rounds first, so the fp16 path has no fusion). */
+#define ORACLE_REFINE_REAL(NAME, T, MIN_INIT, FMA)                                          \
     void NAME(const T* D11, const T* D21, const int64_t* p1, int64_t* p1_new, int64_t B,     \
               int64_t H, int64_t W, int64_t N, int64_t F, int radius, int dilation_max) {     \
         const int64_t total = B * N;                                                          \
@@ -337,7 +364,7 @@ void oracle_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
                         if (inside_image(u, v, W, H)) {                                       \
                             const T* d11 = D11 + ((b * H + v) * W + u) * F;                   \
                             T score = 0;                                                      \
-                            for (int64_t k = 0; k < F; k++) score += d21[k] * d11[k];         \
+                            for (int64_t k = 0; k < F; k++) score = FMA(d21[k], d11[k], score); \
                             if (score > max_score) {                                          \
                                 max_score = score;                                            \
                                 u_new = u;                                                    \
@@ -354,8 +381,8 @@ void oracle_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
         }                                                                                     \
     }
 
-ORACLE_REFINE_REAL(oracle_refine_matches_f32, float, 1.17549435e-38f)
-ORACLE_REFINE_REAL(oracle_refine_matches_f64, double, 2.2250738585072014e-308)
+ORACLE_REFINE_REAL(oracle_refine_matches_f32, float, 1.17549435e-38f, fmaf)
+ORACLE_REFINE_REAL(oracle_refine_matches_f64, double, 2.2250738585072014e-308, fma)
 
 /* ------------------------------------------------------------------------ */
 /* Sim3 device library (gn_kernels.cu:172-413), restated in float           */

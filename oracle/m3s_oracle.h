@@ -18,8 +18,10 @@
  *     (tests/golden/make_golden.py -> tests/golden/ fixtures).
  *
  * Numerics convention (pinned identically in oracle and HIP kernels):
- *   - no FMA contraction (-ffp-contract=off here, #pragma clang fp contract(off)
- *     in the matching kernels);
+ *   - FMA contraction as the reference's nvcc build does it (--fmad=true, setup.py:29-37):
+ *     ORACLE_CONTRACT_NVCC by default, every fused multiply-add explicit (fmaf), the file
+ *     itself compiled with -ffp-contract=off; ORACLE_CONTRACT_OFF / _NVCC_RIGHT are variants
+ *     for measuring the convention;
  *   - every double-literal promotion in the reference source is reproduced as an
  *     explicit double operation followed by a cast to float;
  *   - fp16 arithmetic of refine_matches rounds after every * and += (c10::Half).
@@ -33,16 +35,22 @@
 extern "C" {
 #endif
 
-/* matching_kernels.cu:119-275 (iter_proj_kernel) + :279-316 (launcher) */
+/* FMA contraction conventions (mast3r-slam_amd/csrc/contract.h) */
+enum { ORACLE_CONTRACT_OFF = 0, ORACLE_CONTRACT_NVCC = 1, ORACLE_CONTRACT_NVCC_RIGHT = 2 };
+/* the GN restatement's convention (alignment kernels, Sim3 library, retraction); default NVCC */
+void oracle_set_contract(int cm);
+int oracle_get_contract(void);
+
 /* matching glue of the reference's Python caller (matching.py:25-90), host arithmetic */
 void oracle_match_prep(const float* X11, const float* X21, const int64_t* idx_init, int64_t B, int64_t H,
                        int64_t W, float* rays9, float* pts, float* p_init);
 void oracle_match_post(const float* X11, const float* X21, const float* p_new, const uint8_t* conv,
                        int64_t B, int64_t H, int64_t W, float dist_thresh, int64_t* p1, uint8_t* valid);
+/* matching_kernels.cu:119-275 (iter_proj_kernel) + :279-316 (launcher), contraction cm */
 void oracle_iter_proj(const float* rays, const float* pts, const float* p_init,
                       float* p_new, uint8_t* converged,
                       int64_t B, int64_t H, int64_t W, int64_t N,
-                      int max_iter, float lambda_init, float cost_thresh);
+                      int max_iter, float lambda_init, float cost_thresh, int cm);
 
 /* matching_kernels.cu:25-81 (refine_matches_kernel<c10::Half>) */
 void oracle_refine_matches_f16(const uint16_t* D11, const uint16_t* D21,
@@ -141,6 +149,7 @@ void oracle_apply_sim3_adj_inv(const float* t, const float* q, const float* s,
                                const float* X, float* Y);
 
 int oracle_num_threads(void);
+void oracle_set_num_threads(int n);
 
 /* 1: sum the reference's float terms in double (a precision reference); 0 (default): the
  * reference's float sums in its order */

@@ -26,7 +26,9 @@ if not os.path.exists(LIB_PATH):
 _lib = ctypes.CDLL(LIB_PATH)
 _vp, _i64, _i, _f = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
 
-_lib.oracle_iter_proj.argtypes = [_vp] * 5 + [_i64] * 4 + [_i, _f, _f]
+_lib.oracle_iter_proj.argtypes = [_vp] * 5 + [_i64] * 4 + [_i, _f, _f, _i]
+_lib.oracle_set_contract.argtypes = [_i]
+_lib.oracle_get_contract.restype = _i
 _lib.oracle_refine_matches_f16.argtypes = [_vp] * 4 + [_i64] * 5 + [_i, _i]
 _lib.oracle_refine_matches_f32.argtypes = [_vp] * 4 + [_i64] * 5 + [_i, _i]
 _lib.oracle_refine_matches_f64.argtypes = [_vp] * 4 + [_i64] * 5 + [_i, _i]
@@ -35,6 +37,7 @@ _lib.oracle_f32_to_f16.argtypes = [_f]
 _lib.oracle_f16_to_f32.restype = _f
 _lib.oracle_f16_to_f32.argtypes = [ctypes.c_uint16]
 _lib.oracle_num_threads.restype = _i
+_lib.oracle_set_num_threads.argtypes = [_i]
 _lib.oracle_set_exact_sums.argtypes = [_i]
 _lib.oracle_match_prep.argtypes = [_vp] * 3 + [_i64] * 3 + [_vp] * 3
 _lib.oracle_match_post.argtypes = [_vp] * 4 + [_i64] * 3 + [_f, _vp, _vp]
@@ -73,6 +76,30 @@ _lib.oracle_retr_sim3.argtypes = [_vp] * 7
 _lib.oracle_apply_sim3_adj_inv.argtypes = [_vp] * 5
 
 MODES = {"points": 0, "rays": 1, "calib": 2}
+# FMA contraction conventions (m3s_oracle.h / mast3r-slam_amd/csrc/contract.h): the reference's nvcc
+# build fuses multiply-adds (NVCC, left product of a two-product sum; the default), NVCC_RIGHT the
+# right product, OFF multiply-then-add
+CONTRACT = {"off": 0, "nvcc": 1, "nvcc_right": 2}
+CONTRACT_DEFAULT = "nvcc"
+
+
+def _cm(contract):
+    return CONTRACT[contract] if isinstance(contract, str) else int(contract)
+
+
+class contract:
+    """Context: the GN restatement's contraction convention (alignment kernels, Sim3 library,
+    retraction) -- ``with contract("off"): ...``."""
+
+    def __init__(self, cm):
+        self.cm = _cm(cm)
+
+    def __enter__(self):
+        self.prev = _lib.oracle_get_contract()
+        _lib.oracle_set_contract(self.cm)
+
+    def __exit__(self, *a):
+        _lib.oracle_set_contract(self.prev)
 
 
 def _c(a, dtype):
@@ -86,6 +113,10 @@ def _p(a):
 
 def num_threads():
     return _lib.oracle_num_threads()
+
+
+def set_num_threads(n):
+    _lib.oracle_set_num_threads(int(n))
 
 
 class exact_sums:
@@ -107,7 +138,7 @@ def f16_bits_to_f32(h: int) -> float:
     return _lib.oracle_f16_to_f32(int(h))
 
 
-def iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh):
+def iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh, contract=CONTRACT_DEFAULT):
     rays = _c(rays, np.float32)
     pts = _c(pts, np.float32)
     p_init = _c(p_init, np.float32)
@@ -117,7 +148,7 @@ def iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh):
     p_new = np.zeros((B, N, 2), np.float32)
     conv = np.zeros((B, N), np.uint8)
     _lib.oracle_iter_proj(_p(rays), _p(pts), _p(p_init), _p(p_new), _p(conv), B, H, W, N,
-                          int(max_iter), float(lambda_init), float(cost_thresh))
+                          int(max_iter), float(lambda_init), float(cost_thresh), _cm(contract))
     return p_new, conv.astype(bool)
 
 
@@ -137,24 +168,28 @@ def match_prep(X11, X21, idx_init=None):
 
 
 def match_iterative_proj(X11, X21, D11, D21, idx_init, max_iter, lambda_init, cost_thresh, dist_thresh,
-                         radius, dilation_max):
+                         radius, dilation_max, contract=CONTRACT_DEFAULT, return_pre=False):
     """The reference's match_iterative_proj (matching.py:52-90): glue with the host arithmetic,
     the oracle's iter_proj / refine_matches -> idx [B,HW] i64, valid [B,HW,1] bool."""
     X11 = _c(X11, np.float32)
     X21 = _c(X21, np.float32)
     B, H, W, _ = X11.shape
     rays, pts, p_init = match_prep(X11, X21, idx_init)
-    p_new, conv = iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh)
+    p_new, conv = iter_proj(rays, pts, p_init, max_iter, lambda_init, cost_thresh, contract)
     p1 = np.zeros((B, H * W, 2), np.int64)
     valid = np.zeros((B, H * W), np.uint8)
     conv8 = np.ascontiguousarray(conv.astype(np.uint8))
     _lib.oracle_match_post(_p(X11), _p(X21), _p(p_new), _p(conv8), B, H, W, float(dist_thresh), _p(p1),
                            _p(valid))
+    p1_pre = p1
     if radius > 0:
         d11 = np.asarray(D11, np.float32).astype(np.float16)
         d21 = np.asarray(D21, np.float32).reshape(B, H * W, -1).astype(np.float16)
         p1 = refine_matches(d11, d21, p1, radius, dilation_max)
-    return p1[..., 0] + W * p1[..., 1], valid.astype(bool)[..., None]
+    out = (p1[..., 0] + W * p1[..., 1], valid.astype(bool)[..., None])
+    if return_pre:  # + iter_proj's p_new and the truncated pre-refine pixels p.long()
+        return out + (p_new, p1_pre)
+    return out
 
 
 def refine_matches(D11, D21, p1, radius, dilation_max):

@@ -9,7 +9,9 @@ What is pinned (reference file:line):
   * match_iterative_proj post-process  mast3r_slam/matching.py:52-90, driven through a
     stub `mast3r_slam_backends` whose iter_proj/refine_matches are the CPU ORACLE
     (so the fixture pins the reference glue: p.long(), occlusion test on the pre-refine
-    pixels, .half() descriptors, u + W*v)
+    pixels, .half() descriptors, u + W*v) -- once per FMA-contraction convention of the
+    oracle's iter_proj: match_<start>_idx/valid under the reference build's (nvcc, the
+    default), match_<start>_<conv>_idx/valid for every convention (off, nvcc, nvcc_right)
   * constrain_points_to_ray            mast3r_slam/geometry.py:37-42, 107-123
   * FactorGraph.solve_GN_rays / _calib  mast3r_slam/global_opt.py:104-213: the exact
     positional argument tuple handed to the op and the update_T_WCs write-back,
@@ -54,13 +56,15 @@ class _Sim3:
 
 
 captured = {}
+_contract = ["nvcc"]  # the stub iter_proj's convention (oracle.CONTRACT)
 
 
 def _stub_backend():
     m = types.ModuleType("mast3r_slam_backends")
 
     def iter_proj(rays, pts, p_init, max_iter, lam, thr):
-        p, c = O.iter_proj(rays.numpy(), pts.numpy(), p_init.numpy(), max_iter, lam, thr)
+        p, c = O.iter_proj(rays.numpy(), pts.numpy(), p_init.numpy(), max_iter, lam, thr,
+                           contract=_contract[0])
         captured["iter_proj_in"] = (rays.clone(), pts.clone(), p_init.clone(), max_iter, lam, thr)
         return [torch.from_numpy(p), torch.from_numpy(c)]
 
@@ -143,12 +147,19 @@ def main():
     _, _, p_init_w = rmatch.prep_for_iter_proj(mp.X11, mp.X21, mp.idx_init)
     out.update(prep_pinit_warm=p_init_w.numpy())
 
-    # match_iterative_proj (reference glue + oracle kernels)
-    for tag, init in (("id", None), ("warm", mp.idx_init)):
-        idx, valid = rmatch.match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, init)
-        out[f"match_{tag}_idx"] = idx.numpy()
-        out[f"match_{tag}_valid"] = valid.numpy()
-        out[f"match_{tag}_p1_pre"] = captured["refine_in"][2].numpy()
+    # match_iterative_proj (reference glue + oracle kernels), per contraction convention
+    for cm in O.CONTRACT:
+        _contract[0] = cm
+        for tag, init in (("id", None), ("warm", mp.idx_init)):
+            idx, valid = rmatch.match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, init)
+            out[f"match_{tag}_{cm}_idx"] = idx.numpy()
+            out[f"match_{tag}_{cm}_valid"] = valid.numpy()
+            out[f"match_{tag}_{cm}_p1_pre"] = captured["refine_in"][2].numpy()
+            if cm == O.CONTRACT_DEFAULT:
+                out[f"match_{tag}_idx"] = idx.numpy()
+                out[f"match_{tag}_valid"] = valid.numpy()
+                out[f"match_{tag}_p1_pre"] = captured["refine_in"][2].numpy()
+    _contract[0] = O.CONTRACT_DEFAULT
 
     # constrain_points_to_ray
     Xs = torch.randn((3, 12 * 16, 3), generator=g).abs() + 0.5

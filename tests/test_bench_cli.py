@@ -1,0 +1,33 @@
+"""bench.py's launch contract on the CPU (no GPU work): ``--gpus N`` without a torch.distributed
+launcher starts N ranks itself (torch.distributed.run, rendezvous on 127.0.0.1), and a rank whose
+WORLD_SIZE disagrees with --gpus refuses to run (VERDICT r02 "what's missing" 3)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(extra_env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_gpus_flag_spawns_one_rank_per_gpu():
+    r = _run(["--gpus", "2"], {"M3S_BENCH_SPAWN_CHECK": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 for d in lines)
+    assert sorted(d["local_rank"] for d in lines) == [0, 1]
+
+
+def test_world_size_must_match_gpus_flag():
+    r = _run(["--gpus", "1"], {"M3S_BENCH_SPAWN_CHECK": "1", "WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr

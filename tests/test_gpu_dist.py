@@ -36,10 +36,16 @@ def _free_port():
     return p
 
 
-def _graph(mode):
+# cfg2 topology at 96x128; cfg4's (256 keyframes, 1024 pair edges: the multi-launch solve with the
+# dataflow core factorisation, BASELINE configs[3]'s sharded graph) at a reduced 48x64
+SIZES = {"cfg2": (96, 128), "cfg4": (48, 64)}
+
+
+def _graph(mode, cfg="cfg2"):
     from m3s import synth
 
-    g = synth.make_graph("cfg2", H=96, W=128, seed=7)
+    H, W = SIZES[cfg]
+    g = synth.make_graph(cfg, H=H, W=W, seed=7)
     if mode == "calib":
         from m3s.geometry import constrain_points_to_ray
 
@@ -54,7 +60,7 @@ def _params(g, mode):
     return p
 
 
-def _worker(rank, world, port, mode, layout, out_q):
+def _worker(rank, world, port, mode, layout, cfg, out_q):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -66,7 +72,7 @@ def _worker(rank, world, port, mode, layout, out_q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        g = _graph(mode)
+        g = _graph(mode, cfg)
         lo, hi = shard_range(g.ii.shape[0], world, rank)
         if layout == "two_way":  # uneven split: rank 0's range spans both halves of the store
             E = g.ii.shape[0] // 2
@@ -95,16 +101,17 @@ def _worker(rank, world, port, mode, layout, out_q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("mode,layout", [("rays", "contiguous"), ("calib", "contiguous"),
-                                         ("rays", "two_way")])
-def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout):
+@pytest.mark.parametrize("mode,layout,cfg", [("rays", "contiguous", "cfg2"), ("calib", "contiguous", "cfg2"),
+                                             ("rays", "two_way", "cfg2"), ("rays", "contiguous", "cfg4")])
+def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cfg):
     """layout "two_way": each rank passes its directed-edge range of a two-way edge store as
-    the op's two halves (m3s.dist.two_way_range) -- the owner-sharded store layout."""
+    the op's two halves (m3s.dist.two_way_range) -- the owner-sharded store layout.  cfg4: the
+    scaling graph's topology (BASELINE configs[3]) at reduced resolution."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, layout, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, layout, cfg, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -123,7 +130,7 @@ def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout):
     # bitwise identical poses on every rank: same all-reduced system, same deterministic solve
     assert np.array_equal(T0, T1)
 
-    g = _graph(mode)
+    g = _graph(mode, cfg)
     c = lambda t: t.cuda()
     Twc = c(g.Twc)
     if mode == "rays":

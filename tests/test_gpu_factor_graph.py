@@ -161,3 +161,21 @@ def test_device_factor_graph_solve_is_bitwise_the_reference_path(mode, ids):
     # the keyframes moved
     g0 = synth.make_graph(dict(N=len(ids), E=9), H=48, W=64, seed=23)
     assert not torch.equal(s_dev.T_WC[ids[1:], 0].cpu(), g0.Twc[1:])
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_device_factor_graph_pin_2_keeps_pinned_rows(mode):
+    """cfg pin = 2: the op fixes only pose 0 (num_fix = 1, gn_kernels.cu:741) and the reference
+    writes back T_WCs[pin:] (global_opt.py:158/213), so keyframe row 1 keeps its pose; the in-place
+    store path must agree bitwise with the reference-compatible FactorGraph."""
+    ids = [3, 4, 5, 6, 7, 8]
+    fg, dg, (s_ref, s_dev) = _device_setup(mode, ids)
+    cfg = dict(DEFAULT_CONFIG, pin=2)
+    fg.cfg, dg.cfg = cfg, dict(cfg)
+    before = s_dev.T_WC.clone()
+    (fg.solve_GN_rays if mode == "rays" else fg.solve_GN_calib)()
+    (dg.solve_GN_rays if mode == "rays" else dg.solve_GN_calib)()
+    torch.cuda.synchronize()
+    assert torch.equal(s_dev.T_WC[ids[:2]], before[ids[:2]])
+    assert torch.equal(s_ref.T_WC, s_dev.T_WC)
+    assert not torch.equal(s_dev.T_WC[ids[2:]], before[ids[2:]])

@@ -1,8 +1,10 @@
 """GPU parity of the matching ops against the CPU oracle (bit-exact indices/flags).
 
 The HIP kernels are called through the drop-in module (C ABI) on identical inputs; the
-oracle is the checker.  Sizes: full 512x384 for B=1 (the tracking shape) plus ragged /
-edge-case shapes.
+oracle is the checker.  Sizes: full 512x384 for B=1 (the tracking shape) and B=8 (add_factors'
+batch), plus ragged / edge-case shapes.  iter_proj is bit-exact under every FMA-contraction
+convention (CONTRACTS: the reference build's nvcc --fmad=true, the default; its right-product
+variant; contraction off), each against the oracle in the same convention.
 """
 import numpy as np
 import pytest
@@ -14,28 +16,43 @@ from m3s.matching import prep_for_iter_proj
 pytestmark = pytest.mark.gpu
 
 CFG = dict(max_iter=10, lambda_init=1e-8, cost_thresh=1e-6)
+CONTRACTS = ["nvcc", "nvcc_right", "off"]
 
 
-def _iter_proj_both(backend, oracle, rays, pts, p_init, **kw):
+def _iter_proj_both(backend, oracle, rays, pts, p_init, contract=None, **kw):
     c = dict(CFG, **kw)
     p_g, conv_g = backend.iter_proj(rays.cuda(), pts.cuda(), p_init.cuda(), c["max_iter"],
-                                    c["lambda_init"], c["cost_thresh"])
+                                    c["lambda_init"], c["cost_thresh"], contract=contract)
     p_o, conv_o = oracle.iter_proj(rays.numpy(), pts.numpy(), p_init.numpy(), c["max_iter"],
-                                   c["lambda_init"], c["cost_thresh"])
+                                   c["lambda_init"], c["cost_thresh"], contract=contract or "nvcc")
     return p_g.cpu().numpy(), conv_g.cpu().numpy(), p_o, conv_o
 
 
+@pytest.mark.parametrize("contract", CONTRACTS)
 @pytest.mark.parametrize("B,H,W,warm", [(1, 384, 512, False), (1, 384, 512, True), (2, 48, 64, False), (3, 5, 7, True)])
-def test_iter_proj_bit_exact(backend, oracle, B, H, W, warm):
+def test_iter_proj_bit_exact(backend, oracle, B, H, W, warm, contract):
     mp = synth.make_match_pair(B=B, H=H, W=W, seed=3 + H)
     rays, pts, p_init = prep_for_iter_proj(mp.X11, mp.X21, mp.idx_init if warm else None)
-    p_g, c_g, p_o, c_o = _iter_proj_both(backend, oracle, rays, pts, p_init)
+    p_g, c_g, p_o, c_o = _iter_proj_both(backend, oracle, rays, pts, p_init, contract)
     # bit-exact floats and flags
     assert np.array_equal(p_g.view(np.uint32), p_o.view(np.uint32)), (
         f"{(p_g != p_o).sum()} of {p_o.size} coordinates differ")
     assert np.array_equal(c_g, c_o)
     # and the truncated match indices the caller uses (p.long())
     assert np.array_equal(p_g.astype(np.int64), p_o.astype(np.int64))
+
+
+@pytest.mark.parametrize("warm", [False, True])
+def test_iter_proj_bit_exact_b8_default_convention(backend, oracle, warm):
+    """The bench's / add_factors' batch: 8 pairs at 512x384 under the default convention (the
+    reference build's), bitwise; and the default equals an explicit contract="nvcc"."""
+    mp = synth.make_match_pair(B=8, H=384, W=512, seed=11)
+    rays, pts, p_init = prep_for_iter_proj(mp.X11, mp.X21, mp.idx_init if warm else None)
+    p_g, c_g, p_o, c_o = _iter_proj_both(backend, oracle, rays, pts, p_init)
+    assert np.array_equal(p_g.view(np.uint32), p_o.view(np.uint32)), (p_g != p_o).sum()
+    assert np.array_equal(c_g, c_o)
+    p_n, c_n, _, _ = _iter_proj_both(backend, oracle, rays[:1], pts[:1], p_init[:1], "nvcc")
+    assert np.array_equal(p_n.view(np.uint32), p_g[:1].view(np.uint32)) and np.array_equal(c_n, c_g[:1])
 
 
 def test_iter_proj_edge_cases(backend, oracle):
@@ -48,10 +65,11 @@ def test_iter_proj_edge_cases(backend, oracle):
     p_init[0, :, 0] = torch.linspace(-100, 100, 50)
     p_init[0, :, 1] = torch.linspace(50, -50, 50)
     p_init[0, 3] = float("nan")
-    for kw in (dict(), dict(max_iter=0), dict(max_iter=1), dict(lambda_init=10.0, cost_thresh=2.0)):
-        p_g, c_g, p_o, c_o = _iter_proj_both(backend, oracle, rays, pts, p_init, **kw)
-        assert np.array_equal(p_g.view(np.uint32), p_o.view(np.uint32)), kw
-        assert np.array_equal(c_g, c_o), kw
+    for cm in CONTRACTS:
+        for kw in (dict(), dict(max_iter=0), dict(max_iter=1), dict(lambda_init=10.0, cost_thresh=2.0)):
+            p_g, c_g, p_o, c_o = _iter_proj_both(backend, oracle, rays, pts, p_init, cm, **kw)
+            assert np.array_equal(p_g.view(np.uint32), p_o.view(np.uint32)), (cm, kw)
+            assert np.array_equal(c_g, c_o), (cm, kw)
 
 
 def test_iter_proj_empty(backend):
@@ -156,9 +174,9 @@ def test_match_pipeline_against_golden(backend, oracle):
 
     ob = types.SimpleNamespace()
 
-    def o_iter_proj(rays, pts, p_init, max_iter, lam, thr):
+    def o_iter_proj(rays, pts, p_init, max_iter, lam, thr, contract="nvcc"):
         p, c = oracle.iter_proj(rays.cpu().numpy(), pts.cpu().numpy(), p_init.cpu().numpy(),
-                                max_iter, lam, thr)
+                                max_iter, lam, thr, contract=contract)
         return [torch.from_numpy(p).to(rays.device), torch.from_numpy(c).to(rays.device)]
 
     def o_refine(D11, D21, p1, radius, dmax):
@@ -181,31 +199,37 @@ def test_match_pipeline_against_golden(backend, oracle):
         assert agree > 0.999 and vagree > 0.999, (tag, agree, vagree)
 
 
-def test_fused_pipeline_bitwise_equals_reference_fixture(backend):
+@pytest.mark.parametrize("contract", [None] + CONTRACTS)
+def test_fused_pipeline_bitwise_equals_reference_fixture(backend, contract):
     """The fused op (csrc/match_glue.hip: prep + iter_proj + occlusion + refine + linear index)
-    against the fixture made by running the REFERENCE's matching.py glue (on the host, with the
-    oracle as its two kernels): identical indices and valid flags for the identity and the
-    warm start, and the torch-glue path on the same GPU differs from it only where torch's GPU
-    normalize / conv2d round differently."""
+    against the fixture made by running the REFERENCE's matching.py glue on the HOST, with the
+    oracle as its two kernels (in each contraction convention; None = the default, the
+    reference build's): identical indices and valid flags for the identity and the warm start.
+    (The glue is bitwise the reference's host run; torch's GPU normalize / conv2d round
+    differently -- bench.py reports how many matches that changes.)"""
     import os
 
     import m3s.matching as mm
 
     gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "glue_golden.npz"))
     t = lambda k: torch.from_numpy(gold[k]).cuda()
+    sfx = "" if contract is None else f"_{contract}"
     for tag, init in (("id", None), ("warm", t("idx_init"))):
-        idx, valid = mm.match_iterative_proj(t("X11"), t("X21"), t("D11"), t("D21"), init)
+        idx, valid = mm.match_iterative_proj(t("X11"), t("X21"), t("D11"), t("D21"), init, contract=contract)
         assert idx.dtype == torch.int64 and valid.dtype == torch.bool and valid.shape[-1] == 1
-        assert np.array_equal(idx.cpu().numpy(), gold[f"match_{tag}_idx"]), (
-            tag, (idx.cpu().numpy() != gold[f"match_{tag}_idx"]).sum())
-        assert np.array_equal(valid.cpu().numpy(), gold[f"match_{tag}_valid"]), tag
+        assert np.array_equal(idx.cpu().numpy(), gold[f"match_{tag}{sfx}_idx"]), (
+            tag, (idx.cpu().numpy() != gold[f"match_{tag}{sfx}_idx"]).sum())
+        assert np.array_equal(valid.cpu().numpy(), gold[f"match_{tag}{sfx}_valid"]), tag
 
 
-@pytest.mark.parametrize("B,H,W,radius", [(1, 384, 512, 3), (2, 37, 53, 3), (1, 24, 32, 0), (2, 16, 16, 2)])
-def test_fused_pipeline_matches_oracle_pipeline(backend, oracle, B, H, W, radius):
+@pytest.mark.parametrize("B,H,W,radius,contract", [(1, 384, 512, 3, "nvcc"), (1, 384, 512, 3, "off"),
+                                                    (2, 37, 53, 3, "nvcc_right"), (1, 24, 32, 0, "nvcc"),
+                                                    (2, 16, 16, 2, "nvcc")])
+def test_fused_pipeline_matches_oracle_pipeline(backend, oracle, B, H, W, radius, contract):
     """On synthetic pairs (full size, ragged tiles, radius 0 = no refine): the fused op equals
     the oracle's whole pipeline (its C restatement of the glue, pinned to the reference's glue
-    by test_glue_golden.py, plus the oracle kernels), identity and warm start."""
+    by test_glue_golden.py, plus the oracle kernels) in the same contraction convention,
+    identity and warm start."""
     import m3s.matching as mm
     from m3s.config import config as cfg0
 
@@ -213,11 +237,12 @@ def test_fused_pipeline_matches_oracle_pipeline(backend, oracle, B, H, W, radius
     c = dict(cfg0["matching"], radius=radius)
     for init in (None, mp.idx_init):
         idx, valid = mm.match_iterative_proj(mp.X11.cuda(), mp.X21.cuda(), mp.D11.cuda(), mp.D21.cuda(),
-                                             None if init is None else init.cuda(), cfg={"matching": c})
+                                             None if init is None else init.cuda(), cfg={"matching": c},
+                                             contract=contract)
         idx_o, valid_o = oracle.match_iterative_proj(
             mp.X11.numpy(), mp.X21.numpy(), mp.D11.numpy(), mp.D21.numpy(),
             None if init is None else init.numpy(), c["max_iter"], c["lambda_init"],
-            c["convergence_thresh"], c["dist_thresh"], c["radius"], c["dilation_max"])
+            c["convergence_thresh"], c["dist_thresh"], c["radius"], c["dilation_max"], contract=contract)
         assert np.array_equal(idx.cpu().numpy(), idx_o), (idx.cpu().numpy() != idx_o).sum()
         assert np.array_equal(valid.cpu().numpy(), valid_o)
 

@@ -1,0 +1,56 @@
+#!/bin/bash
+# Round-3 GPU session: full GPU tests, smoke, bench cfg3 (default), bench cfg4 + its rocprofv3
+# kernel stats.  Every GPU step has its own limit; after a fault / abort / timeout nothing else
+# touches the GPU.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG="${TAG:-r03}"
+STEPS="${STEPS:-tests smoke bench bench4 prof4}"
+ok_or_fail() { if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "STOP after $2 (rc=$1)"; exit "$1"; fi; }
+for s in $STEPS; do
+    case "$s" in
+    tests)
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 400 \
+            --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+        rc=$?; echo "pytest gpu rc=$rc"; tail -n 5 gpurun_out/${TAG}_pytest_gpu.log; ok_or_fail $rc pytest ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
+        rc=$?; echo "smoke rc=$rc"; tail -n 2 gpurun_out/${TAG}_smoke.log; ok_or_fail $rc smoke ;;
+    bench)
+        timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+        rc=$?; echo "bench rc=$rc"; cat gpurun_out/${TAG}_bench.json; tail -n 3 gpurun_out/${TAG}_bench.err; ok_or_fail $rc bench ;;
+    gntests)
+        timeout -k 10 600 python -u -m pytest tests/test_gpu_gn.py tests/test_gpu_gn_reference_order.py -x -q \
+            -p no:cacheprovider --timeout 400 --timeout-method thread > gpurun_out/${TAG}_pytest_gn.log 2>&1
+        rc=$?; echo "pytest gn rc=$rc"; tail -n 5 gpurun_out/${TAG}_pytest_gn.log; ok_or_fail $rc pytest_gn ;;
+    qbench)
+        timeout -k 10 300 python bench.py --no-cpu-baseline --no-matching > gpurun_out/${TAG}_qbench.json 2> gpurun_out/${TAG}_qbench.err
+        rc=$?; echo "qbench rc=$rc"; cat gpurun_out/${TAG}_qbench.json; tail -n 3 gpurun_out/${TAG}_qbench.err; ok_or_fail $rc qbench ;;
+    qbench4)
+        timeout -k 10 300 python bench.py --config cfg4 --no-cpu-baseline --no-matching > gpurun_out/${TAG}_qbench4.json 2> gpurun_out/${TAG}_qbench4.err
+        rc=$?; echo "qbench4 rc=$rc"; cat gpurun_out/${TAG}_qbench4.json; tail -n 3 gpurun_out/${TAG}_qbench4.err; ok_or_fail $rc qbench4 ;;
+    bench4)
+        timeout -k 10 600 python bench.py --config cfg4 --no-matching \
+            > gpurun_out/${TAG}_bench_cfg4.json 2> gpurun_out/${TAG}_bench_cfg4.err
+        rc=$?; echo "bench cfg4 rc=$rc"; cat gpurun_out/${TAG}_bench_cfg4.json; tail -n 3 gpurun_out/${TAG}_bench_cfg4.err; ok_or_fail $rc bench4 ;;
+    prof)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof \
+            -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-matching \
+            > gpurun_out/${TAG}_prof.log 2>&1
+        rc=$?; echo "rocprof rc=$rc"; tail -n 3 gpurun_out/${TAG}_prof.log
+        rm -f gpurun_out/${TAG}_prof/*kernel_trace.csv; ok_or_fail $rc rocprof ;;
+    prof4)
+        M3S_EXIT_MAPS=gpurun_out/${TAG}_prof4_maps.txt timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof4 \
+            -o run -- python bench.py --config cfg4 --steps 3 --warmup 1 --no-cpu-baseline --no-matching \
+            > gpurun_out/${TAG}_prof4.log 2>&1
+        rc=$?; echo "rocprof cfg4 rc=$rc"; tail -n 3 gpurun_out/${TAG}_prof4.log
+        rm -f gpurun_out/${TAG}_prof4/*kernel_trace.csv; ok_or_fail $rc rocprof4 ;;
+    matching)
+        timeout -k 10 600 python -u -m pytest tests/test_gpu_matching.py -x -q -p no:cacheprovider --timeout 400 \
+            --timeout-method thread > gpurun_out/${TAG}_pytest_matching.log 2>&1
+        rc=$?; echo "pytest matching rc=$rc"; tail -n 5 gpurun_out/${TAG}_pytest_matching.log; ok_or_fail $rc pytest_matching ;;
+    esac
+done
+exit 0

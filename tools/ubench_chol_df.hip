@@ -67,6 +67,7 @@ int main(int argc, char** argv) {
         a.nt = nt;
         a.ntiles = ntiles;
         a.epoch = rep;
+        a.spin_limit = 1 << 22;
         a.trace = dtr;
         int per = 0, ncu = 0;
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)chol_df_kernel, NT, 0));
