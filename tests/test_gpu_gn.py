@@ -469,3 +469,24 @@ def test_fused_edge_reduce_is_bitwise_the_separate_launch(backend, monkeypatch, 
     T_f, dx_f = _run_gpu(backend, g, mode, 4)
     assert np.isfinite(T_f).all()
     assert np.array_equal(T_f, T_s) and np.array_equal(dx_f, dx_s)
+
+
+@pytest.mark.parametrize("dense", [True, False])
+def test_factorisation_timeout_is_an_error_not_a_singular_system(backend, monkeypatch, dense):
+    """A bounded device-side wait of the dataflow factorisation that gives up (forced here with
+    the test hook M3S_TEST_FORCE_TIMEOUT: every ready wait times out at once) raises
+    RuntimeError (M3S_ERR_TIMEOUT) instead of passing for a singular system (dx = 0, early exit);
+    the GPU drains normally and the next call without the hook is correct again."""
+    g = synth.make_graph("cfg4", H=24, W=32, seed=6)
+    if dense:
+        monkeypatch.setenv("M3S_SOLVER_DENSE", "1")
+    else:
+        monkeypatch.setenv("M3S_SOLVER", "2")
+    monkeypatch.setenv("M3S_CHOL_DF", "1")
+    T_ok, dx_ok = _run_gpu(backend, g, "rays", 2)
+    monkeypatch.setenv("M3S_TEST_FORCE_TIMEOUT", "1")
+    with pytest.raises(RuntimeError, match="timed out"):
+        _run_gpu(backend, g, "rays", 2)
+    monkeypatch.delenv("M3S_TEST_FORCE_TIMEOUT")
+    T_again, dx_again = _run_gpu(backend, g, "rays", 2)
+    assert np.array_equal(T_again, T_ok) and np.array_equal(dx_again, dx_ok)
