@@ -56,10 +56,10 @@ void m3s_shutdown(void);
  * measuring the convention's effect.
  */
 enum {
-    M3S_CONTRACT_OFF = 0,        /* IEEE multiply, then add (no fusion) */
-    M3S_CONTRACT_NVCC = 1,       /* nvcc --fmad=true, left product of a two-product sum fused */
-    M3S_CONTRACT_NVCC_RIGHT = 2, /* the same, right product fused */
-    M3S_CONTRACT_DEFAULT = M3S_CONTRACT_NVCC
+    M3S_CONTRACT_NVCC = 0,       /* nvcc --fmad=true, left product of a two-product sum fused */
+    M3S_CONTRACT_OFF = 1,        /* IEEE multiply, then add (no fusion) */
+    M3S_CONTRACT_NVCC_RIGHT = 2, /* the same as NVCC, right product fused */
+    M3S_CONTRACT_DEFAULT = M3S_CONTRACT_NVCC  /* 0: a zero-initialised argument is the default */
 };
 
 /*
@@ -178,6 +178,10 @@ typedef struct m3s_gn_args {
     const uint8_t* valid_b;
     const float* Q_b;
     int64_t E_a;
+    /* FMA-contraction convention (M3S_CONTRACT_*; 0 = the reference build's) of the
+     * reference-order accumulate and of the retraction (the fast path's reformulated sums have
+     * none to follow) */
+    int contract;
 } m3s_gn_args;
 enum {
     M3S_GN_ORDER_DEFAULT = 0,

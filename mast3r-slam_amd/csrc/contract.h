@@ -9,8 +9,9 @@
 // canonicalisation may commute the operands.  M3S_CONTRACT_OFF is plain IEEE multiply then add
 // (the round-1/2 convention, `-ffp-contract=off`).  DESIGN.md §2 records the residual ambiguity.
 //
-// Every file that includes this header must be compiled with contraction OFF (these helpers
-// are the only source of fused operations in the parity paths).
+// Each helper turns contraction off in its own body, so the OFF variant stays unfused in any
+// translation unit; code around the helpers follows its file's own -ffp-contract (the parity
+// files are compiled with contraction OFF, so these helpers are their only fused operations).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -19,9 +20,16 @@
 
 namespace m3s {
 
+// a * b + c in double (the reference's double-literal expressions), fused or not
+__device__ __forceinline__ double cmad_d(bool fused, double a, double b, double c) {
+#pragma clang fp contract(off)
+    return fused ? __builtin_fma(a, b, c) : a * b + c;
+}
+
 // a * b + c  (the product fused into the add under nvcc)
 template <int CM>
 __device__ __forceinline__ float cmad(float a, float b, float c) {
+#pragma clang fp contract(off)
     if constexpr (CM == M3S_CONTRACT_OFF) return a * b + c;
     else return __builtin_fmaf(a, b, c);
 }
@@ -29,6 +37,7 @@ __device__ __forceinline__ float cmad(float a, float b, float c) {
 // a * b + c * d
 template <int CM>
 __device__ __forceinline__ float cmm(float a, float b, float c, float d) {
+#pragma clang fp contract(off)
     if constexpr (CM == M3S_CONTRACT_OFF) return a * b + c * d;
     else if constexpr (CM == M3S_CONTRACT_NVCC) return __builtin_fmaf(a, b, c * d);
     else return __builtin_fmaf(c, d, a * b);

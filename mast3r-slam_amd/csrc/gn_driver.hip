@@ -787,6 +787,9 @@ int validate(const m3s_gn_args& a) {
                 "gauss_newton: bad summation order %d", a.order);
     M3S_REQUIRE(a.mode == M3S_GN_POINTS || a.mode == M3S_GN_RAYS || a.mode == M3S_GN_CALIB,
                 "gauss_newton: bad mode %d", a.mode);
+    M3S_REQUIRE(a.contract == M3S_CONTRACT_NVCC || a.contract == M3S_CONTRACT_OFF ||
+                    a.contract == M3S_CONTRACT_NVCC_RIGHT,
+                "gauss_newton: unknown contraction convention %d", a.contract);
     M3S_REQUIRE(a.N >= 1 && a.HW >= 1, "gauss_newton: need N >= 1 poses and HW >= 1 points");
     M3S_REQUIRE(a.E_total >= 0 && a.E_local >= 0 && a.edge_offset >= 0 &&
                     a.edge_offset + a.E_local <= a.E_total,
@@ -945,6 +948,7 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
         R.pixel_border = a.pixel_border;
         R.HW = a.HW;
         R.variant = env_int("M3S_GN_REF_VARIANT", 0);  // diagnostics
+        R.contract = a.contract;
     }
     // the workspace's plan integers (flags .. sched, one contiguous span of the layout) as an
     // image in pinned memory: the edge lists / CSR lists first (what the pack reads), then the
@@ -1137,6 +1141,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     S.delta_thresh = a.delta_thresh;
     S.flags = flags;
     S.debug = env_int("M3S_SOLVE_DEBUG", 0);
+    S.contract = a.contract;
     if (S.debug) {
         static int printed = 0;
         if (printed++ == 0) {
@@ -1306,7 +1311,7 @@ int run(const m3s_gn_args& a) {
         g_prof.mark(c.st);
         if (!c.sp.fused && !c.sp.hybrid)  // gn_solve retracts inside its launch
             M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
-                                         a.delta_thresh, flags));
+                                         a.delta_thresh, flags, a.contract));
         g_prof.mark(c.st);
     }
     // (the per-call solver buffers are released by ~Ctx on this and every error path)

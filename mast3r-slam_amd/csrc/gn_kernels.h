@@ -74,7 +74,8 @@ struct RefParams {
     float z_eps;
     int width, height, pixel_border;
     int64_t HW;
-    int variant;  // diagnostics only (env M3S_GN_REF_VARIANT): kRefVar* formula substitutions
+    int variant;   // diagnostics only (env M3S_GN_REF_VARIANT): kRefVar* formula substitutions
+    int contract;  // M3S_CONTRACT_*: FMA contraction of the reference build (contract.h)
 };
 // Formula substitutions for measuring what each deviation of the fast path's residual model
 // from the reference costs in accuracy, under the reference's own summation order.
@@ -189,6 +190,7 @@ struct SolveArgs {
     int* flags;
     int do_fwd, do_tail, do_back;  // rounds | in-kernel dense tail | back rounds + retract
     int debug;                     // M3S_SOLVE_DEBUG: printf phase times (wall clock, thread 0)
+    int contract;                  // the retraction's M3S_CONTRACT_* (m3s_gn_args.contract)
 };
 size_t solve_lds_bytes(int nmeta_lds);
 int solve_max_poses();  // x stays in LDS: the single-workgroup solve takes at most this many poses
@@ -197,6 +199,6 @@ hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
 // device address) to device memory, stream-ordered, by a kernel
 hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes);
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
-                          float delta_thresh, int* flags);
+                          float delta_thresh, int* flags, int contract);
 
 }  // namespace m3s

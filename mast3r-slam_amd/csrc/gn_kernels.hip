@@ -516,7 +516,7 @@ __global__ __launch_bounds__(256) void gn_retract_kernel(float* __restrict__ Twc
                                                          const double* __restrict__ x,
                                                          float* __restrict__ dx, int N,
                                                          float delta_thresh,
-                                                         int* __restrict__ flags) {
+                                                         int* __restrict__ flags, int contract) {
     if (flags[kFlagDone]) return;
     const int tid = threadIdx.x;
     const bool fail = flags[kFlagFail] != 0;
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256) void gn_retract_kernel(float* __restrict__ Twc
             dx[(int64_t)(p - 1) * 7 + q] = v;
             nrm += (double)v * (double)v;
         }
-        retr_sim3(xi, Twc + (int64_t)p * 8);
+        retr_sim3_cm(contract, xi, Twc + (int64_t)p * 8);
     }
     __shared__ double red[256];
     red[tid] = nrm;
@@ -653,9 +653,9 @@ hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* sl
 }
 
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
-                          float delta_thresh, int* flags) {
+                          float delta_thresh, int* flags, int contract) {
     hipLaunchKernelGGL(gn_retract_kernel, dim3(1), dim3(256), 0, st, Twc, x, dx, N, delta_thresh,
-                       flags);
+                       flags, contract);
     return hipGetLastError();
 }
 

@@ -10,21 +10,26 @@
 //     apply_Sim3_adj_inv(T_i) for EVERY point (:277-297), Ji = -Jj;
 //   * the 256 partials reduced by blockReduce's tree (256 -> 128 -> 64 -> 32 -> ... -> 1,
 //     :36-55);
-//   * no FMA contraction (file built with -ffp-contract=off, the oracle's convention).
+//   * FMA contraction as the reference's nvcc build (--fmad=true) fuses this source
+//     (m3s_gn_args.contract, default M3S_CONTRACT_NVCC; contract.h): `hij += w Jx[n] Jx[m]` is
+//     one fma of the rounded w Jx[n] per term, `u = fx x/z + cx` an fma, the Sim3 library as in
+//     sim3.h.  The file is compiled with contraction OFF; the helpers are its only fused ops.
 // Output per edge: the 7x7 chain D[n][m] = sum (w Jj[n]) Jj[m] and g[n] = sum (w e) Jj[n] in
 // f32 -- the reference's Hs/gs are exactly +-D / +-g (Ji = -Jj makes every one of the 119
-// entries a negated copy of one of these 56 chains):
+// entries a negated copy of one of these 56 chains; negation commutes with every rounding,
+// fused or not):
 //   Hs[0] = Hs[3] = lower(D) mirrored, Hs[1] = -D^T, Hs[2] = -D, gs[0] = -g, gs[1] = g.
 // gn_assemble_ref_kernel then builds the block system from the LOWER triangle of that
 // (not exactly symmetric) matrix, as SimplicialLLT reads it (gn_kernels.cu:71-113, 132-153).
 //
-// This is the parity mode: its Hs/gs match the CPU oracle's to a few ulp and its poses track
-// the reference's float rounding; the default packed path (gn_accum.hip) is ~equally exact in
-// absolute terms but sums in a different order.
+// This is the parity mode: its Hs/gs match the CPU oracle's (same convention) to a few ulp and its
+// poses track the reference's float rounding; the default packed path (gn_accum.hip) is
+// ~equally exact in absolute terms but sums in a different order.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
+#include "contract.h"
 #include "gn_kernels.h"
 #include "sim3.h"
 
@@ -47,22 +52,20 @@ __device__ __forceinline__ float inv_ref(float x, int variant) {
     return (float)(1.0 / (double)x);
 }
 
-__device__ __forceinline__ float dot3(const float* t, const float* s) {
-    return (t[0] * s[0] + t[1] * s[1]) + t[2] * s[2];
-}
-
-// gn_kernels.cu:277-297: Y = X Adj(T_i)^{-1} for a row vector X
+// gn_kernels.cu:277-297: Y = X Adj(T_i)^{-1} for a row vector X; Y[3..5] += s_inv (...) and
+// Y[6] = X[6] + s_inv dot(t, Ra) are fused multiply-adds under nvcc
+template <int CM>
 __device__ __forceinline__ void adj_inv_ref(const Sim3f& Ti, float s_inv, const float* X, float* Y) {
     float Ra[3];
-    act_so3(Ti.q, &X[0], Ra);
+    act_so3<CM>(Ti.q, &X[0], Ra);
     Y[0] = s_inv * Ra[0];
     Y[1] = s_inv * Ra[1];
     Y[2] = s_inv * Ra[2];
-    act_so3(Ti.q, &X[3], &Y[3]);
-    Y[3] += s_inv * (Ti.t[1] * Ra[2] - Ti.t[2] * Ra[1]);
-    Y[4] += s_inv * (Ti.t[2] * Ra[0] - Ti.t[0] * Ra[2]);
-    Y[5] += s_inv * (Ti.t[0] * Ra[1] - Ti.t[1] * Ra[0]);
-    Y[6] = X[6] + (s_inv * dot3(Ti.t, Ra));
+    act_so3<CM>(Ti.q, &X[3], &Y[3]);
+    Y[3] = cmad<CM>(s_inv, cmm<CM>(Ti.t[1], Ra[2], -Ti.t[2], Ra[1]), Y[3]);
+    Y[4] = cmad<CM>(s_inv, cmm<CM>(Ti.t[2], Ra[0], -Ti.t[0], Ra[2]), Y[4]);
+    Y[5] = cmad<CM>(s_inv, cmm<CM>(Ti.t[0], Ra[1], -Ti.t[1], Ra[0]), Y[5]);
+    Y[6] = cmad<CM>(s_inv, cdot3<CM>(Ti.t[0], Ra[0], Ti.t[1], Ra[1], Ti.t[2], Ra[2]), X[6]);
 }
 
 struct RefAcc {
@@ -72,42 +75,43 @@ struct RefAcc {
 
 // One residual row: Jj = J Adj^{-1}, then hij += (w Jx[n]) Jx[m], vj += (w e) Jj[n]
 // (gn_kernels.cu:999-1013 and the two loops after it) on the 49 + 7 distinct chains.
+template <int CM>
 __device__ __forceinline__ void accum_row_ref(RefAcc& a, const Sim3f& Ti, float s_inv, const float* J,
                                               float w, float err) {
     float Jj[7];
-    adj_inv_ref(Ti, s_inv, J, Jj);
+    adj_inv_ref<CM>(Ti, s_inv, J, Jj);
 #pragma unroll
     for (int n = 0; n < 7; n++) {
         const float wj = w * Jj[n];
 #pragma unroll
-        for (int m = 0; m < 7; m++) a.D[n][m] = a.D[n][m] + wj * Jj[m];
+        for (int m = 0; m < 7; m++) a.D[n][m] = cmad<CM>(wj, Jj[m], a.D[n][m]);
     }
     const float we = w * err;
 #pragma unroll
-    for (int n = 0; n < 7; n++) a.g[n] = a.g[n] + we * Jj[n];
+    for (int n = 0; n < 7; n++) a.g[n] = cmad<CM>(we, Jj[n], a.g[n]);
 }
 
-template <int MODE>
+template <int MODE, int CM>
 __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, float si_inv,
                                           const Sim3f& Tij, const float* Xi, const float* Xj,
                                           float q, float ci, float cj, bool vm, int64_t ind,
                                           RefAcc& a) {
     float Xj_Ci[3];
-    act_so3(Tij.q, Xj, Xj_Ci);  // actSim3 (:207-219)
-    Xj_Ci[0] *= Tij.s; Xj_Ci[1] *= Tij.s; Xj_Ci[2] *= Tij.s;
-    Xj_Ci[0] += Tij.t[0]; Xj_Ci[1] += Tij.t[1]; Xj_Ci[2] += Tij.t[2];
+    act_sim3<CM>(Tij, Xj, Xj_Ci);  // actSim3 (:207-219)
     float J[7];
     if constexpr (MODE == GN_RAYS) {
         // gn_kernels.cu:924-1089
-        const float norm2_i = dot3(Xi, Xi);
+        const float norm2_i = cdot3<CM>(Xi[0], Xi[0], Xi[1], Xi[1], Xi[2], Xi[2]);
         const float norm1_i = sqrtf(norm2_i);
         const float norm1_i_inv = inv_ref(norm1_i, P.variant);
-        const float ri[3] = {norm1_i_inv * Xi[0], norm1_i_inv * Xi[1], norm1_i_inv * Xi[2]};
-        const float norm2_j = dot3(Xj_Ci, Xj_Ci);
+        const float norm2_j = cdot3<CM>(Xj_Ci[0], Xj_Ci[0], Xj_Ci[1], Xj_Ci[1], Xj_Ci[2], Xj_Ci[2]);
         const float norm1_j = sqrtf(norm2_j);
         const float norm1_j_inv = inv_ref(norm1_j, P.variant);
         const float rj[3] = {norm1_j_inv * Xj_Ci[0], norm1_j_inv * Xj_Ci[1], norm1_j_inv * Xj_Ci[2]};
-        const float err[4] = {rj[0] - ri[0], rj[1] - ri[1], rj[2] - ri[2], norm1_j - norm1_i};
+        // rj - ri: a two-product difference (ri = norm1_i_inv Xi enters only here)
+        const float err[4] = {cmm<CM>(norm1_j_inv, Xj_Ci[0], -norm1_i_inv, Xi[0]),
+                              cmm<CM>(norm1_j_inv, Xj_Ci[1], -norm1_i_inv, Xi[1]),
+                              cmm<CM>(norm1_j_inv, Xj_Ci[2], -norm1_i_inv, Xi[2]), norm1_j - norm1_i};
         const bool valid = vm & (q > P.Q_thresh) & (ci > P.C_thresh) & (cj > P.C_thresh);
         const float sqrt_w_ray = valid ? P.s0_inv * sqrtf(q) : 0.0f;
         const float sqrt_w_dist = valid ? P.s1_inv * sqrtf(q) : 0.0f;
@@ -117,20 +121,20 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         const float wc_dist = sqrt_w_dist * sqrt_w_dist;
         w[0] *= wc_ray; w[1] *= wc_ray; w[2] *= wc_ray; w[3] *= wc_dist;
         const float norm3_j_inv = norm1_j_inv / norm2_j;
-        const float drx_dPx = norm1_j_inv - (Xj_Ci[0] * Xj_Ci[0]) * norm3_j_inv;
-        const float dry_dPy = norm1_j_inv - (Xj_Ci[1] * Xj_Ci[1]) * norm3_j_inv;
-        const float drz_dPz = norm1_j_inv - (Xj_Ci[2] * Xj_Ci[2]) * norm3_j_inv;
+        const float drx_dPx = cmad<CM>(-(Xj_Ci[0] * Xj_Ci[0]), norm3_j_inv, norm1_j_inv);
+        const float dry_dPy = cmad<CM>(-(Xj_Ci[1] * Xj_Ci[1]), norm3_j_inv, norm1_j_inv);
+        const float drz_dPz = cmad<CM>(-(Xj_Ci[2] * Xj_Ci[2]), norm3_j_inv, norm1_j_inv);
         const float drx_dPy = ((-Xj_Ci[0]) * Xj_Ci[1]) * norm3_j_inv;
         const float drx_dPz = ((-Xj_Ci[0]) * Xj_Ci[2]) * norm3_j_inv;
         const float dry_dPz = ((-Xj_Ci[1]) * Xj_Ci[2]) * norm3_j_inv;
         J[0] = drx_dPx; J[1] = drx_dPy; J[2] = drx_dPz; J[3] = 0.0f; J[4] = rj[2]; J[5] = -rj[1]; J[6] = 0.0f;
-        accum_row_ref(a, Ti, si_inv, J, w[0], err[0]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[0], err[0]);
         J[0] = drx_dPy; J[1] = dry_dPy; J[2] = dry_dPz; J[3] = -rj[2]; J[4] = 0.0f; J[5] = rj[0]; J[6] = 0.0f;
-        accum_row_ref(a, Ti, si_inv, J, w[1], err[1]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[1], err[1]);
         J[0] = drx_dPz; J[1] = dry_dPz; J[2] = drz_dPz; J[3] = rj[1]; J[4] = -rj[0]; J[5] = 0.0f; J[6] = 0.0f;
-        accum_row_ref(a, Ti, si_inv, J, w[2], err[2]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[2], err[2]);
         J[0] = rj[0]; J[1] = rj[1]; J[2] = rj[2]; J[3] = 0.0f; J[4] = 0.0f; J[5] = 0.0f; J[6] = norm1_j;
-        accum_row_ref(a, Ti, si_inv, J, w[3], err[3]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[3], err[3]);
     } else if constexpr (MODE == GN_CALIB) {
         // gn_kernels.cu:1360-1495
         const int u_target = (int)(ind % P.width);
@@ -146,8 +150,8 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         }
         const float x_div_z = Xj_Ci[0] * zj_inv;
         const float y_div_z = Xj_Ci[1] * zj_inv;
-        const float u = P.fx * x_div_z + P.cx;
-        const float v = P.fy * y_div_z + P.cy;
+        const float u = cmad<CM>(P.fx, x_div_z, P.cx);
+        const float v = cmad<CM>(P.fy, y_div_z, P.cy);
         const bool valid_u = (u > (float)P.pixel_border) && (u < (float)(P.width - 1 - P.pixel_border));
         const bool valid_v = (v > (float)P.pixel_border) && (v < (float)(P.height - 1 - P.pixel_border));
         const float err[3] = {u - (float)u_target, v - (float)v_target, zj_log - zi_log};
@@ -162,15 +166,15 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         w[0] *= wc_pixel; w[1] *= wc_pixel; w[2] *= wc_depth;
         const float fx = P.fx, fy = P.fy;
         J[0] = fx * zj_inv; J[1] = 0.0f; J[2] = ((-fx) * x_div_z) * zj_inv;
-        J[3] = ((-fx) * x_div_z) * y_div_z; J[4] = fx * (1.0f + x_div_z * x_div_z);
+        J[3] = ((-fx) * x_div_z) * y_div_z; J[4] = fx * cmad<CM>(x_div_z, x_div_z, 1.0f);
         J[5] = (-fx) * y_div_z; J[6] = 0.0f;
-        accum_row_ref(a, Ti, si_inv, J, w[0], err[0]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[0], err[0]);
         J[0] = 0.0f; J[1] = fy * zj_inv; J[2] = ((-fy) * y_div_z) * zj_inv;
-        J[3] = (-fy) * (1.0f + y_div_z * y_div_z); J[4] = (fy * x_div_z) * y_div_z;
+        J[3] = (-fy) * cmad<CM>(y_div_z, y_div_z, 1.0f); J[4] = (fy * x_div_z) * y_div_z;
         J[5] = fy * x_div_z; J[6] = 0.0f;
-        accum_row_ref(a, Ti, si_inv, J, w[1], err[1]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[1], err[1]);
         J[0] = 0.0f; J[1] = 0.0f; J[2] = zj_inv; J[3] = y_div_z; J[4] = -x_div_z; J[5] = 0.0f; J[6] = 1.0f;
-        accum_row_ref(a, Ti, si_inv, J, w[2], err[2]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[2], err[2]);
     } else {
         // point_align_kernel, gn_kernels.cu:564-674
         const float err[3] = {Xj_Ci[0] - Xi[0], Xj_Ci[1] - Xi[1], Xj_Ci[2] - Xi[2]};
@@ -181,11 +185,11 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         const float wc = sqrt_w_point * sqrt_w_point;
         w[0] *= wc; w[1] *= wc; w[2] *= wc;
         J[0] = 1.0f; J[1] = 0.0f; J[2] = 0.0f; J[3] = 0.0f; J[4] = Xj_Ci[2]; J[5] = -Xj_Ci[1]; J[6] = Xj_Ci[0];
-        accum_row_ref(a, Ti, si_inv, J, w[0], err[0]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[0], err[0]);
         J[0] = 0.0f; J[1] = 1.0f; J[2] = 0.0f; J[3] = -Xj_Ci[2]; J[4] = 0.0f; J[5] = Xj_Ci[0]; J[6] = Xj_Ci[1];
-        accum_row_ref(a, Ti, si_inv, J, w[1], err[1]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[1], err[1]);
         J[0] = 0.0f; J[1] = 0.0f; J[2] = 1.0f; J[3] = Xj_Ci[1]; J[4] = -Xj_Ci[0]; J[5] = 0.0f; J[6] = Xj_Ci[2];
-        accum_row_ref(a, Ti, si_inv, J, w[2], err[2]);
+        accum_row_ref<CM>(a, Ti, si_inv, J, w[2], err[2]);
     }
 }
 
@@ -193,7 +197,7 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
 
 // One workgroup per local directed edge; out[e * kRefStride + 0..48] = D (row-major),
 // out[.. + 49..55] = g, the blockReduce'd f32 sums.
-template <int MODE>
+template <int MODE, int CM>
 __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, EdgeSrc es, RefParams P,
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
     const int ix = ii_loc[e], jx = jj_loc[e];
     const Sim3f Ti = load_sim3(Twc + (int64_t)ix * 8);
     const Sim3f Tj = load_sim3(Twc + (int64_t)jx * 8);
-    const Sim3f Tij = rel_sim3(Ti, Tj);
+    const Sim3f Tij = rel_sim3<CM>(Ti, Tj);
     const float si_inv = (float)(1.0 / (double)Ti.s);  // apply_Sim3_adj_inv's s_inv
     const int64_t HW = P.HW;
     const int64_t* idx_e;
@@ -232,7 +236,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
         if ((uint64_t)ind >= (uint64_t)HW) ind = HW - 1;  // the reference reads out of bounds
         const float Xi[3] = {Xi_b[ind * 3], Xi_b[ind * 3 + 1], Xi_b[ind * 3 + 2]};
         const float Xj[3] = {Xj_b[k * 3], Xj_b[k * 3 + 1], Xj_b[k * 3 + 2]};
-        point_ref<MODE>(P, Ti, si_inv, Tij, Xi, Xj, Q[k], Ci_b[ind], Cj_b[k], vm, ind, a);
+        point_ref<MODE, CM>(P, Ti, si_inv, Tij, Xi, Xj, Q[k], Ci_b[ind], Cj_b[k], vm, ind, a);
     }
 
     // blockReduce (gn_kernels.cu:36-55) of all 56 chains at once: level o adds s[t + o] into
@@ -311,12 +315,17 @@ hipError_t launch_accum_ref(int mode, int E_local, hipStream_t st, const float* 
                             const float* Cs, const int* ii_loc, const int* jj_loc, const EdgeSrc& es,
                             const RefParams& P, float* out, const int* flags) {
     if (E_local <= 0) return hipSuccess;
-#define M3S_REF(MODE)                                                                              \
-    hipLaunchKernelGGL(gn_accum_ref_kernel<MODE>, dim3(E_local), dim3(kAccThreads), 0, st, Twc, Xs, \
+#define M3S_REF(MODE, CM)                                                                              \
+    hipLaunchKernelGGL((gn_accum_ref_kernel<MODE, CM>), dim3(E_local), dim3(kAccThreads), 0, st, Twc, Xs, \
                        Cs, ii_loc, jj_loc, es, P, out, flags)
-    if (mode == GN_RAYS) M3S_REF(GN_RAYS);
-    else if (mode == GN_CALIB) M3S_REF(GN_CALIB);
-    else M3S_REF(GN_POINTS);
+#define M3S_REF_MODES(CM)                     \
+    if (mode == GN_RAYS) M3S_REF(GN_RAYS, CM); \
+    else if (mode == GN_CALIB) M3S_REF(GN_CALIB, CM); \
+    else M3S_REF(GN_POINTS, CM)
+    if (P.contract == M3S_CONTRACT_OFF) M3S_REF_MODES(M3S_CONTRACT_OFF);
+    else if (P.contract == M3S_CONTRACT_NVCC_RIGHT) M3S_REF_MODES(M3S_CONTRACT_NVCC_RIGHT);
+    else M3S_REF_MODES(M3S_CONTRACT_NVCC);
+#undef M3S_REF_MODES
 #undef M3S_REF
     return hipGetLastError();
 }

@@ -871,7 +871,7 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
                 a.dx[(int64_t)(p - 1) * 7 + q] = v;
                 nrm += (double)v * (double)v;
             }
-            retr_sim3(xi, a.Twc + (int64_t)p * 8);
+            retr_sim3_cm(a.contract, xi, a.Twc + (int64_t)p * 8);
         }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) nrm += __shfl_xor(nrm, off, 64);

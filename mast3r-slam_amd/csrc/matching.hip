@@ -949,7 +949,7 @@ extern "C" int m3s_iter_proj_ex(const float* rays, const float* pts, const float
                                 float* p_new, uint8_t* converged, int64_t B, int64_t H, int64_t W,
                                 int64_t N, int max_iter, float lambda_init, float cost_thresh,
                                 int contract, void* stream) {
-    M3S_REQUIRE(contract >= M3S_CONTRACT_OFF && contract <= M3S_CONTRACT_NVCC_RIGHT,
+    M3S_REQUIRE(contract == M3S_CONTRACT_NVCC || contract == M3S_CONTRACT_OFF || contract == M3S_CONTRACT_NVCC_RIGHT,
                 "iter_proj: unknown contraction convention %d", contract);
     M3S_REQUIRE(B >= 0 && N >= 0, "iter_proj: negative sizes");
     M3S_REQUIRE(H >= 3 && W >= 3, "iter_proj: ray image must be at least 3x3 (got %lldx%lld)",

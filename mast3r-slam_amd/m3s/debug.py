@@ -58,6 +58,7 @@ def make_args(g, mode, L, Twc, edge_range=None, max_iter=1, delta=0.0, comm=None
     a.ws, a.ws_bytes = ws.data_ptr(), nbytes
     a.comm = comm
     a.order = mb._gn_order[0]
+    a.contract = mb._gn_contract[0]
     a.stream = torch.cuda.current_stream(torch.device(dev)).cuda_stream
     return a, keep
 

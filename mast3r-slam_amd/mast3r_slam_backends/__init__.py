@@ -30,6 +30,7 @@ __all__ = [
     "edge_confidence",
     "library_path",
     "set_gn_order",
+    "set_gn_contract",
     "lib",
 ]
 
@@ -72,7 +73,7 @@ lib.m3s_match_iterative_proj.argtypes = ([_vp] * 5 + [_c_int64] * 4 + [_i, _f, _
 # FMA-contraction convention of the parity paths (include/m3s_backend.h M3S_CONTRACT_*): the
 # reference's nvcc build fuses multiply-adds ("nvcc": the left product of a two-product sum, the
 # default); "nvcc_right" and "off" are variants for measuring the convention
-CONTRACT = {"off": 0, "nvcc": 1, "nvcc_right": 2}
+CONTRACT = {"nvcc": 0, "off": 1, "nvcc_right": 2}
 
 
 def _contract(c):
@@ -124,6 +125,7 @@ class GNArgs(ctypes.Structure):
         ("valid_b", _vp),
         ("Q_b", _vp),
         ("E_a", _c_int64),
+        ("contract", _i),
     ]
 
 
@@ -144,6 +146,17 @@ GN_POINTS, GN_RAYS, GN_CALIB = 0, 1, 2
 # reproduces the reference kernels' own float order and formulas (gn_refacc.hip).
 GN_ORDERS = {"default": 0, "fast": 1, "reference": 2}
 _gn_order = [0]
+
+
+_gn_contract = [0]
+
+
+def set_gn_contract(contract: str) -> str:
+    """Select the FMA-contraction convention (``CONTRACT``) of the reference-order GN accumulate
+    and the retraction for later gauss_newton_* calls; returns the previous."""
+    prev = [k for k, v in CONTRACT.items() if v == _gn_contract[0]][0]
+    _gn_contract[0] = _contract(contract)
+    return prev
 
 
 def set_gn_order(order: str) -> str:
@@ -396,6 +409,7 @@ def _run_gn(mode, Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q, max_iter, delt
     a.ws, a.ws_bytes = ws.data_ptr(), ws_bytes
     a.comm = comm
     a.order = _gn_order[0]
+    a.contract = _gn_contract[0]
     if second_half is not None:
         a.idx_b, a.valid_b, a.Q_b = idx_b.data_ptr(), valid_b.data_ptr(), Q_b.data_ptr()
         a.E_a = E_a

@@ -394,12 +394,16 @@ static inline float huber(float r) {
     return (double)r_abs < 1.345 ? 1.0f : (float)(1.345 / (double)r_abs);
 }
 
-/* :178-184  qi * qj, quaternion [x,y,z,w] */
+/* Below, every function follows the GN restatement's contraction convention g_contract
+ * (oracle_set_contract; default ORACLE_CONTRACT_NVCC, the reference build's): CM is it. */
+#define CM g_contract
+
+/* :178-184  qi * qj, quaternion [x,y,z,w]; each component a left-to-right sum of 4 products */
 static inline void quat_comp(const float* qi, const float* qj, float* out) {
-    float o0 = ((qi[3] * qj[0] + qi[0] * qj[3]) + qi[1] * qj[2]) - qi[2] * qj[1];
-    float o1 = ((qi[3] * qj[1] - qi[0] * qj[2]) + qi[1] * qj[3]) + qi[2] * qj[0];
-    float o2 = ((qi[3] * qj[2] + qi[0] * qj[1]) - qi[1] * qj[0]) + qi[2] * qj[3];
-    float o3 = ((qi[3] * qj[3] - qi[0] * qj[0]) - qi[1] * qj[1]) - qi[2] * qj[2];
+    float o0 = cmad(CM, -qi[2], qj[1], cmad(CM, qi[1], qj[2], cmm(CM, qi[3], qj[0], qi[0], qj[3])));
+    float o1 = cmad(CM, qi[2], qj[0], cmad(CM, qi[1], qj[3], cmm(CM, qi[3], qj[1], -qi[0], qj[2])));
+    float o2 = cmad(CM, qi[2], qj[3], cmad(CM, -qi[1], qj[0], cmm(CM, qi[3], qj[2], qi[0], qj[1])));
+    float o3 = cmad(CM, -qi[2], qj[2], cmad(CM, -qi[1], qj[1], cmm(CM, qi[3], qj[3], -qi[0], qj[0])));
     out[0] = o0; out[1] = o1; out[2] = o2; out[3] = o3;
 }
 
@@ -407,34 +411,37 @@ static inline void quat_inv(const float* q, float* out) { /* :187-193 */
     out[0] = -q[0]; out[1] = -q[1]; out[2] = -q[2]; out[3] = q[3];
 }
 
-/* :195-205; safe for X == Y (each Y[k] reads only X[k] and uv) */
+/* :195-205; safe for X == Y (each Y[k] reads only X[k] and uv).  uv = 2.0 * (...) is a double
+ * multiply of a float: exactly 2x. */
 static inline void actSO3(const float* q, const float* X, float* Y) {
-    float uv0 = (float)(2.0 * (double)(q[1] * X[2] - q[2] * X[1]));
-    float uv1 = (float)(2.0 * (double)(q[2] * X[0] - q[0] * X[2]));
-    float uv2 = (float)(2.0 * (double)(q[0] * X[1] - q[1] * X[0]));
-    float y0 = (X[0] + q[3] * uv0) + (q[1] * uv2 - q[2] * uv1);
-    float y1 = (X[1] + q[3] * uv1) + (q[2] * uv0 - q[0] * uv2);
-    float y2 = (X[2] + q[3] * uv2) + (q[0] * uv1 - q[1] * uv0);
+    float uv0 = (float)(2.0 * (double)cmm(CM, q[1], X[2], -q[2], X[1]));
+    float uv1 = (float)(2.0 * (double)cmm(CM, q[2], X[0], -q[0], X[2]));
+    float uv2 = (float)(2.0 * (double)cmm(CM, q[0], X[1], -q[1], X[0]));
+    float y0 = cmad(CM, q[3], uv0, X[0]) + cmm(CM, q[1], uv2, -q[2], uv1);
+    float y1 = cmad(CM, q[3], uv1, X[1]) + cmm(CM, q[2], uv0, -q[0], uv2);
+    float y2 = cmad(CM, q[3], uv2, X[2]) + cmm(CM, q[0], uv1, -q[1], uv0);
     Y[0] = y0; Y[1] = y1; Y[2] = y2;
 }
 
-/* :207-219 */
+/* :207-219: Y = s (R X) + t -- the scale product feeds the translation add (fused) */
 static inline void actSim3(const float* t, const float* q, const float* s, const float* X, float* Y) {
-    actSO3(q, X, Y);
-    Y[0] *= s[0]; Y[1] *= s[0]; Y[2] *= s[0];
-    Y[0] += t[0]; Y[1] += t[1]; Y[2] += t[2];
+    float r[3];
+    actSO3(q, X, r);
+    Y[0] = cmad(CM, r[0], s[0], t[0]);
+    Y[1] = cmad(CM, r[1], s[0], t[1]);
+    Y[2] = cmad(CM, r[2], s[0], t[2]);
 }
 
 /* :229-240 b <- a x b */
 static inline void crossInplace(const float* a, float* b) {
-    float x0 = a[1] * b[2] - a[2] * b[1];
-    float x1 = a[2] * b[0] - a[0] * b[2];
-    float x2 = a[0] * b[1] - a[1] * b[0];
+    float x0 = cmm(CM, a[1], b[2], -a[2], b[1]);
+    float x1 = cmm(CM, a[2], b[0], -a[0], b[2]);
+    float x2 = cmm(CM, a[0], b[1], -a[1], b[0]);
     b[0] = x0; b[1] = x1; b[2] = x2;
 }
 
-static inline float dot3(const float* t, const float* s) { return (t[0] * s[0] + t[1] * s[1]) + t[2] * s[2]; }
-static inline float squared_norm3(const float* v) { return (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]; }
+static inline float dot3(const float* t, const float* s) { return cdot3(CM, t[0], s[0], t[1], s[1], t[2], s[2]); }
+static inline float squared_norm3(const float* v) { return cdot3(CM, v[0], v[0], v[1], v[1], v[2], v[2]); }
 
 /* :252-272  T_ij = T_i^{-1} T_j */
 static void relSim3(const float* ti, const float* qi, const float* si,
@@ -452,7 +459,8 @@ static void relSim3(const float* ti, const float* qi, const float* si,
     tij[0] *= si_inv; tij[1] *= si_inv; tij[2] *= si_inv;
 }
 
-/* :277-297  Y = X * Adj(T)^{-1} for a row vector X (tangent order tau, phi, sigma) */
+/* :277-297  Y = X * Adj(T)^{-1} for a row vector X (tangent order tau, phi, sigma);
+ * Y[3..5] += s_inv * (...) and Y[6] = X[6] + s_inv * dot are fused multiply-adds */
 void oracle_apply_sim3_adj_inv(const float* t, const float* q, const float* s, const float* X, float* Y) {
     const float s_inv = (float)(1.0 / (double)s[0]);
     float Ra[3];
@@ -461,20 +469,23 @@ void oracle_apply_sim3_adj_inv(const float* t, const float* q, const float* s, c
     Y[1] = s_inv * Ra[1];
     Y[2] = s_inv * Ra[2];
     actSO3(q, &X[3], &Y[3]);
-    Y[3] += s_inv * (t[1] * Ra[2] - t[2] * Ra[1]);
-    Y[4] += s_inv * (t[2] * Ra[0] - t[0] * Ra[2]);
-    Y[5] += s_inv * (t[0] * Ra[1] - t[1] * Ra[0]);
-    Y[6] = X[6] + (s_inv * dot3(t, Ra));
+    Y[3] = cmad(CM, s_inv, cmm(CM, t[1], Ra[2], -t[2], Ra[1]), Y[3]);
+    Y[4] = cmad(CM, s_inv, cmm(CM, t[2], Ra[0], -t[0], Ra[2]), Y[4]);
+    Y[5] = cmad(CM, s_inv, cmm(CM, t[0], Ra[1], -t[1], Ra[0]), Y[5]);
+    Y[6] = cmad(CM, s_inv, dot3(t, Ra), X[6]);
 }
 
-/* :299-321 */
+/* double a*b + c, fused under every contracting convention */
+static inline double cmad_d(int cm, double a, double b, double c) { return cm != ORACLE_CONTRACT_OFF ? fma(a, b, c) : a * b + c; }
+
+/* :299-321 (the small-angle series is double arithmetic) */
 static void expSO3(const float* phi, float* q) {
-    float theta_sq = (phi[0] * phi[0] + phi[1] * phi[1]) + phi[2] * phi[2];
+    float theta_sq = squared_norm3(phi);
     float imag, real;
     if ((double)theta_sq < EPS) {
         float theta_p4 = theta_sq * theta_sq;
-        imag = (float)((0.5 - (1.0 / 48.0) * (double)theta_sq) + (1.0 / 3840.0) * (double)theta_p4);
-        real = (float)((1.0 - (1.0 / 8.0) * (double)theta_sq) + (1.0 / 384.0) * (double)theta_p4);
+        imag = (float)cmad_d(CM, 1.0 / 3840.0, (double)theta_p4, cmad_d(CM, -(1.0 / 48.0), (double)theta_sq, 0.5));
+        real = (float)cmad_d(CM, 1.0 / 384.0, (double)theta_p4, cmad_d(CM, -(1.0 / 8.0), (double)theta_sq, 1.0));
     } else {
         float theta = sqrtf(theta_sq);
         imag = sinf((float)(0.5 * (double)theta)) / theta;
@@ -494,7 +505,7 @@ void oracle_exp_sim3(const float* xi, float* t, float* q, float* s) {
     float scale = expf(sigma);
     expSO3(phi, q);
     s[0] = scale;
-    float theta_sq = (phi[0] * phi[0] + phi[1] * phi[1]) + phi[2] * phi[2];
+    float theta_sq = squared_norm3(phi);
     float theta = sqrtf(theta_sq);
     float A, B, C;
     const float one = 1.0f;
@@ -512,27 +523,27 @@ void oracle_exp_sim3(const float* xi, float* t, float* q, float* s) {
         C = (scale - one) / sigma;
         if ((double)fabsf(theta) < EPS) {
             float sigma_sq = sigma * sigma;
-            A = ((sigma - one) * scale + one) / sigma_sq;
-            B = ((((scale * half) * sigma_sq + scale) - one) - sigma * scale) / (sigma_sq * sigma);
+            A = cmad(CM, sigma - one, scale, one) / sigma_sq;
+            B = cmad(CM, -sigma, scale, cmad(CM, scale * half, sigma_sq, scale) - one) / (sigma_sq * sigma);
         } else {
             float a = scale * sinf(theta);
             float b = scale * cosf(theta);
-            float c = theta_sq + sigma * sigma;
-            A = (a * sigma + (one - b) * theta) / (theta * c);
-            B = (C - ((b - one) * sigma + a * theta) / (c)) / (theta_sq);
+            float c = cmad(CM, sigma, sigma, theta_sq);
+            A = cmm(CM, a, sigma, one - b, theta) / (theta * c);
+            B = (C - cmm(CM, b - one, sigma, a, theta) / (c)) / (theta_sq);
         }
     }
-    t[0] = C * tau[0];
-    t[1] = C * tau[1];
-    t[2] = C * tau[2];
+    /* t = C tau; t += A tau'; t += B tau'' -- the first two products are one two-product sum,
+     * the third is fused into the running sum */
+    const float tau0[3] = {tau[0], tau[1], tau[2]};
     crossInplace(phi, tau);
-    t[0] += A * tau[0];
-    t[1] += A * tau[1];
-    t[2] += A * tau[2];
+    t[0] = cmm(CM, C, tau0[0], A, tau[0]);
+    t[1] = cmm(CM, C, tau0[1], A, tau[1]);
+    t[2] = cmm(CM, C, tau0[2], A, tau[2]);
     crossInplace(phi, tau);
-    t[0] += B * tau[0];
-    t[1] += B * tau[1];
-    t[2] += B * tau[2];
+    t[0] = cmad(CM, B, tau[0], t[0]);
+    t[1] = cmad(CM, B, tau[1], t[1]);
+    t[2] = cmad(CM, B, tau[2], t[2]);
 }
 
 /* :392-413 left-composition retraction */
@@ -544,8 +555,9 @@ void oracle_retr_sim3(const float* xi, const float* t, const float* q, const flo
     oracle_exp_sim3(xi, dt, dq, ds);
     quat_comp(dq, q, q1);
     actSO3(dq, t, t1);
-    t1[0] *= ds[0]; t1[1] *= ds[0]; t1[2] *= ds[0];
-    t1[0] += dt[0]; t1[1] += dt[1]; t1[2] += dt[2];
+    t1[0] = cmad(CM, t1[0], ds[0], dt[0]);
+    t1[1] = cmad(CM, t1[1], ds[0], dt[1]);
+    t1[2] = cmad(CM, t1[2], ds[0], dt[2]);
     s1[0] = ds[0] * s[0];
 }
 
@@ -582,8 +594,13 @@ void oracle_pose_retr(float* Twc, const float* dx, int64_t N, int num_fix) {
 static int g_exact_sums = 0;
 void oracle_set_exact_sums(int on) { g_exact_sums = on != 0; }
 
-static inline double add_term(double a, float t) {
-    return g_exact_sums ? a + (double)t : (double)((float)a + t);
+/* acc += x * y: the reference's `hij[l] += w * Jx[n] * Jx[m]` / `vi[n] += w * err * Ji[n]` with
+ * x the rounded first product -- one fused multiply-add per term under nvcc (g_contract), or
+ * (exact sums) the exact product added in double */
+static inline double add_prod(double a, float x, float y) {
+    if (g_exact_sums) return a + (double)x * (double)y;
+    if (g_contract != ORACLE_CONTRACT_OFF) return (double)fmaf(x, y, (float)a);
+    return (double)((float)a + x * y);
 }
 static inline double add_acc(double a, double b) {
     return g_exact_sums ? a + b : (double)((float)a + (float)b);
@@ -614,15 +631,15 @@ static inline void accum_row(double* acc, const float* ti, const float* qi, cons
     int l = 0;
     for (int n = 0; n < 14; n++) {
         for (int m = 0; m <= n; m++) {
-            acc[l] = add_term(acc[l], (w * Jx[n]) * Jx[m]);
+            acc[l] = add_prod(acc[l], w * Jx[n], Jx[m]);
             l++;
         }
     }
     double* vi = acc + HDIM;
     double* vj = acc + HDIM + 7;
     for (int n = 0; n < 7; n++) {
-        vi[n] = add_term(vi[n], (w * err) * Ji[n]);
-        vj[n] = add_term(vj[n], (w * err) * Jj[n]);
+        vi[n] = add_prod(vi[n], w * err, Ji[n]);
+        vj[n] = add_prod(vj[n], w * err, Jj[n]);
     }
 }
 
@@ -651,16 +668,16 @@ static int point_residuals(const oracle_gn_params* P, const float* tij, const fl
         const float norm2_i = squared_norm3(Xi);
         const float norm1_i = sqrtf(norm2_i);
         const float norm1_i_inv = (float)(1.0 / (double)norm1_i);
-        float ri[3];
-        for (int i = 0; i < 3; i++) ri[i] = norm1_i_inv * Xi[i];
+        /* ri = norm1_i_inv * Xi enters only err below */
         const float norm2_j = squared_norm3(Xj_Ci);
         const float norm1_j = sqrtf(norm2_j);
         const float norm1_j_inv = (float)(1.0 / (double)norm1_j);
         float rj[3];
         for (int i = 0; i < 3; i++) rj[i] = norm1_j_inv * Xj_Ci[i];
-        err[0] = rj[0] - ri[0];
-        err[1] = rj[1] - ri[1];
-        err[2] = rj[2] - ri[2];
+        /* rj - ri: a two-product difference (each ray a product with its inverse norm) */
+        err[0] = cmm(CM, norm1_j_inv, Xj_Ci[0], -norm1_i_inv, Xi[0]);
+        err[1] = cmm(CM, norm1_j_inv, Xj_Ci[1], -norm1_i_inv, Xi[1]);
+        err[2] = cmm(CM, norm1_j_inv, Xj_Ci[2], -norm1_i_inv, Xi[2]);
         err[3] = norm1_j - norm1_i;
         const int valid = valid_match_ind & (q > P->Q_thresh) & (ci > P->C_thresh) & (cj > P->C_thresh);
         R->valid = valid;
@@ -677,9 +694,9 @@ static int point_residuals(const oracle_gn_params* P, const float* tij, const fl
         w[2] *= w_const_ray;
         w[3] *= w_const_dist;
         const float norm3_j_inv = norm1_j_inv / norm2_j;
-        const float drx_dPx = norm1_j_inv - (Xj_Ci[0] * Xj_Ci[0]) * norm3_j_inv;
-        const float dry_dPy = norm1_j_inv - (Xj_Ci[1] * Xj_Ci[1]) * norm3_j_inv;
-        const float drz_dPz = norm1_j_inv - (Xj_Ci[2] * Xj_Ci[2]) * norm3_j_inv;
+        const float drx_dPx = cmad(CM, -(Xj_Ci[0] * Xj_Ci[0]), norm3_j_inv, norm1_j_inv);
+        const float dry_dPy = cmad(CM, -(Xj_Ci[1] * Xj_Ci[1]), norm3_j_inv, norm1_j_inv);
+        const float drz_dPz = cmad(CM, -(Xj_Ci[2] * Xj_Ci[2]), norm3_j_inv, norm1_j_inv);
         const float drx_dPy = ((-Xj_Ci[0]) * Xj_Ci[1]) * norm3_j_inv;
         const float drx_dPz = ((-Xj_Ci[0]) * Xj_Ci[2]) * norm3_j_inv;
         const float dry_dPz = ((-Xj_Ci[1]) * Xj_Ci[2]) * norm3_j_inv;
@@ -709,8 +726,8 @@ static int point_residuals(const oracle_gn_params* P, const float* tij, const fl
         const float zi_log = valid_z ? logf(Xi[2]) : 0.0f;
         const float x_div_z = Xj_Ci[0] * zj_inv;
         const float y_div_z = Xj_Ci[1] * zj_inv;
-        const float u = fx * x_div_z + cx;
-        const float v = fy * y_div_z + cy;
+        const float u = cmad(CM, fx, x_div_z, cx);
+        const float v = cmad(CM, fy, y_div_z, cy);
         const int valid_u = (u > (float)P->pixel_border) && (u < (float)(P->width - 1 - P->pixel_border));
         const int valid_v = (v > (float)P->pixel_border) && (v < (float)(P->height - 1 - P->pixel_border));
         err[0] = u - (float)u_target;
@@ -733,10 +750,10 @@ static int point_residuals(const oracle_gn_params* P, const float* tij, const fl
         float* J1 = R->J[1];
         float* J2 = R->J[2];
         J0[0] = fx * zj_inv; J0[1] = 0.0f; J0[2] = ((-fx) * x_div_z) * zj_inv;
-        J0[3] = ((-fx) * x_div_z) * y_div_z; J0[4] = fx * (1.0f + x_div_z * x_div_z);
+        J0[3] = ((-fx) * x_div_z) * y_div_z; J0[4] = fx * cmad(CM, x_div_z, x_div_z, 1.0f);
         J0[5] = (-fx) * y_div_z; J0[6] = 0.0f;
         J1[0] = 0.0f; J1[1] = fy * zj_inv; J1[2] = ((-fy) * y_div_z) * zj_inv;
-        J1[3] = (-fy) * (1.0f + y_div_z * y_div_z); J1[4] = (fy * x_div_z) * y_div_z;
+        J1[3] = (-fy) * cmad(CM, y_div_z, y_div_z, 1.0f); J1[4] = (fy * x_div_z) * y_div_z;
         J1[5] = fy * x_div_z; J1[6] = 0.0f;
         J2[0] = 0.0f; J2[1] = 0.0f; J2[2] = zj_inv;
         J2[3] = y_div_z; J2[4] = -x_div_z; J2[5] = 0.0f; J2[6] = 1.0f;

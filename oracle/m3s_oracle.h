@@ -36,7 +36,7 @@ extern "C" {
 #endif
 
 /* FMA contraction conventions (mast3r-slam_amd/csrc/contract.h) */
-enum { ORACLE_CONTRACT_OFF = 0, ORACLE_CONTRACT_NVCC = 1, ORACLE_CONTRACT_NVCC_RIGHT = 2 };
+enum { ORACLE_CONTRACT_NVCC = 0, ORACLE_CONTRACT_OFF = 1, ORACLE_CONTRACT_NVCC_RIGHT = 2 };
 /* the GN restatement's convention (alignment kernels, Sim3 library, retraction); default NVCC */
 void oracle_set_contract(int cm);
 int oracle_get_contract(void);

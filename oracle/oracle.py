@@ -79,7 +79,7 @@ MODES = {"points": 0, "rays": 1, "calib": 2}
 # FMA contraction conventions (m3s_oracle.h / mast3r-slam_amd/csrc/contract.h): the reference's nvcc
 # build fuses multiply-adds (NVCC, left product of a two-product sum; the default), NVCC_RIGHT the
 # right product, OFF multiply-then-add
-CONTRACT = {"off": 0, "nvcc": 1, "nvcc_right": 2}
+CONTRACT = {"nvcc": 0, "off": 1, "nvcc_right": 2}
 CONTRACT_DEFAULT = "nvcc"
 
 

@@ -3,10 +3,12 @@
 That path accumulates every directed edge exactly as the reference's align kernels do
 (one 256-thread workgroup per edge, thread t owning points t, t+256, ..., 768-long fp32
 chains per thread, the blockReduce tree, IEEE 1/x, logf(zj) - logf(zi), the double-literal
-Huber, apply_Sim3_adj_inv per point; gn_kernels.cu:31-55, 455-723, 813-1138, 1231-1543) and
-reads the assembled matrix from its lower triangle like SimplicialLLT.  So it must reproduce
-the oracle -- the reference restated in C -- not only within the pose tolerance but term for
-term:
+Huber, apply_Sim3_adj_inv per point; gn_kernels.cu:31-55, 455-723, 813-1138, 1231-1543), with
+the FMA contraction of the reference's nvcc build (--fmad=true, setup.py:29-37; every test runs
+under each convention: "nvcc" -- the default --, "nvcc_right", "off"), and reads the assembled
+matrix from its lower triangle like SimplicialLLT.  So it must reproduce the oracle -- the
+reference restated in C, in the same convention -- not only within the pose tolerance but term
+for term:
 
 * Hs / gs (the reference kernels' own output tensors) within 4 ulp of the largest entry of
   their 7x7 block (GPU logf / glibc logf may differ by an ulp; everything else is IEEE);
@@ -26,11 +28,15 @@ LOCAL = dict(sigma_ray=0.003, sigma_dist=10.0, sigma_pixel=1.0, sigma_depth=10.0
              sigma_point=0.05, C_conf=0.0, Q_conf=1.5, pixel_border=-10, depth_eps=1e-6)
 
 
-@pytest.fixture
-def ref_order(backend):
+@pytest.fixture(params=["nvcc", "nvcc_right", "off"])
+def ref_order(request, backend, oracle):
+    """The reference-order path and the oracle in one contraction convention."""
     prev = backend.set_gn_order("reference")
-    yield
+    prev_c = backend.set_gn_contract(request.param)
+    with oracle.contract(request.param):
+        yield request.param
     backend.set_gn_order(prev)
+    backend.set_gn_contract(prev_c)
 
 
 def _graph(mode, cfg=None, N=6, E=8, H=48, W=64, seed=5):
