@@ -21,6 +21,19 @@
 #include "gn_kernels.h"
 #include "sim3.h"
 
+// Scheduling of the 4 points of a lane's step (AccStage::compute): 0 (default; what every
+// measurement so far ran -- the old default of 1 sat below its first use and never applied) lets
+// the compiler interleave the points freely, 1 fences after every point (one point's temporaries
+// live at a time), 2 after every second point.
+#ifndef M3S_ACC_SCHED_BARRIER
+#define M3S_ACC_SCHED_BARRIER 0
+#endif
+// Diagnostics builds only (tools/build_variants.sh; the results are NOT the normal equations):
+// 1 = the packed accumulate's compute alone, 2 = its memory traffic alone.
+#ifndef M3S_ACC_DIAG
+#define M3S_ACC_DIAG 0
+#endif
+
 namespace m3s {
 
 // ---------------------------------------------------------------------------
@@ -415,8 +428,11 @@ struct AccStage {
             p.valid = codes[s] >= 0;
             p.sq = __int_as_float(sqb[s]);
             point_body<M, float>(p, T, P, acc);
-#if M3S_ACC_SCHED_BARRIER
+#if M3S_ACC_SCHED_BARRIER == 1
             __builtin_amdgcn_sched_barrier(0);  // one point's temporaries live at a time
+#elif M3S_ACC_SCHED_BARRIER == 2
+            // two points' temporaries at a time: their dependent residual chains interleave
+            if (s & 1) __builtin_amdgcn_sched_barrier(0);
 #endif
         }
     }
@@ -729,6 +745,31 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
         nb = pk_b[k / 2 + 1];
     }
     for (; k < k1; k += S) {
+#if M3S_ACC_DIAG == 1
+        // diagnostics: compute only (the first step's data, re-used: no memory after it)
+        if (k == k0 + 4 * (int)threadIdx.x) {
+            cur.ka = na;
+            cur.kb = nb;
+            cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
+        }
+        cur.template compute<MODE>(T, P, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+#elif M3S_ACC_DIAG == 2
+        // diagnostics: memory only (the loads of every step, a trivial use of each value)
+        cur.ka = na;
+        cur.kb = nb;
+        if (k + S < k1) {
+            na = pk_b[(k + S) / 2];
+            nb = pk_b[(k + S) / 2 + 1];
+        }
+        cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
+        acc[0] += __int_as_float(cur.ka.x) + __int_as_float(cur.ka.z) + __int_as_float(cur.kb.x) +
+                  __int_as_float(cur.kb.z) + cur.xa.x + cur.xa.y + cur.xa.z + cur.xa.w + cur.xb.x + cur.xb.y +
+                  cur.xb.z + cur.xb.w + cur.xc.x + cur.xc.y + cur.xc.z + cur.xc.w + cur.g[0][2] + cur.g[1][2] +
+                  cur.g[2][2] + cur.g[3][2] + cur.g[0][0] + cur.g[1][0] + cur.g[2][0] + cur.g[3][0];
+        continue;
+#endif
         cur.ka = na;
         cur.kb = nb;
         if (k + S < k1) {
@@ -742,9 +783,6 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
 
 // Per-iteration accumulate over the packed stream: 8 B {code, sqrt q} + Xj 12 B + the gather
 // of the matched point (calib: its depth from Zs; rays/points: Xi) per point-edge.
-#ifndef M3S_ACC_SCHED_BARRIER
-#define M3S_ACC_SCHED_BARRIER 1
-#endif
 
 #ifndef M3S_ACC_PIPE
 #define M3S_ACC_PIPE 1

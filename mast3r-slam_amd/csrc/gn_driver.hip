@@ -215,7 +215,10 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     Layout L{};
     const int64_t npose = std::max<int64_t>(N - 1, 0);
     const int64_t n = 7 * npose;
-    L.nchunks = choose_nchunks(HW, E_local);
+    // from the TOTAL edge count: every rank of a sharded call then chunks its edges exactly as one
+    // GPU would, so the per-edge f32 partial sums (and the poses, up to the f64 all-reduce order)
+    // do not depend on the number of ranks
+    L.nchunks = choose_nchunks(HW, E_total);
     L.npad = (int)std::max<int64_t>(kCholTile, align_up((size_t)n, kCholTile));
     L.nblk_max = (int)(npose + E_total);
     size_t off = 0;

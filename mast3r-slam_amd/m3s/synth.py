@@ -202,9 +202,15 @@ def raycast_keyframe(pose, Kn, H, W, phase, device, iters=12):
 
 
 def make_graph(cfg="cfg1", H=384, W=512, device="cpu", seed=None, mode=None, edges_only=None,
-               edge_range=None) -> Graph:
+               edge_range=None, init_perturb=None, outlier_frac=0.0) -> Graph:
     """Build a synthetic graph.  ``edge_range=(lo, hi)`` materialises idx/valid/Q only for the
-    directed edges lo..hi-1 (a rank's shard); ii/jj always cover all 2E directed edges."""
+    directed edges lo..hi-1 (a rank's shard); ii/jj always cover all 2E directed edges.
+
+    Stress options (a graph the GN is NOT converged on after 10 iterations): ``init_perturb =
+    (rot_deg, t, log_scale)`` replaces the (0.5 deg, 1 cm, 0.01) start perturbation;
+    ``outlier_frac`` of the valid matches of every directed edge point at a uniformly random
+    pixel instead (gross outliers: the Huber weights and, for calib, the image-border validity
+    become active).  Both draw from their own generators, so the rest of the graph is unchanged."""
     spec = dict(CONFIGS[cfg]) if isinstance(cfg, str) else dict(cfg)
     if seed is None:
         seed = {"cfg1": 1, "cfg2": 2, "cfg3": 3, "cfg4": 4}.get(cfg, 0) if isinstance(cfg, str) else 0
@@ -217,7 +223,8 @@ def make_graph(cfg="cfg1", H=384, W=512, device="cpu", seed=None, mode=None, edg
     K = torch.tensor(Kn, dtype=torch.float32, device=device)
 
     gt = make_poses(N, seed)
-    init = perturb(gt, seed)
+    init = perturb(gt, seed) if init_perturb is None else perturb(gt, seed, *init_perturb)
+    gen_out = torch.Generator(device=device).manual_seed(seed + 5000)
     phase = np.random.default_rng(seed + 3000).uniform(0, 2 * math.pi, 2)
     Xs = torch.stack([raycast_keyframe(gt[k], Kn, H, W, phase, device) for k in range(N)])
     Xs = Xs + 0.003 * torch.randn(Xs.shape, generator=gen, device=device)
@@ -246,6 +253,10 @@ def make_graph(cfg="cfg1", H=384, W=512, device="cpu", seed=None, mode=None, edg
         idx[e - lo] = torch.where(ok, lin, torch.zeros_like(lin))
         valid[e - lo, :, 0] = ok
         Q[e - lo, :, 0] = torch.exp(1.0 + 0.5 * torch.randn((HW,), generator=gen, device=device))
+        if outlier_frac > 0:
+            bad = ok & (torch.rand((HW,), generator=gen_out, device=device) < outlier_frac)
+            wrong = torch.randint(0, HW, (HW,), generator=gen_out, device=device)
+            idx[e - lo] = torch.where(bad, wrong, idx[e - lo])
 
     to_t = lambda ps: torch.tensor(np.stack([sim3_to_vec(p) for p in ps]), dtype=torch.float32, device=device)
     return Graph(

@@ -51,6 +51,20 @@ for s in $STEPS; do
         timeout -k 10 600 python -u -m pytest tests/test_gpu_matching.py -x -q -p no:cacheprovider --timeout 400 \
             --timeout-method thread > gpurun_out/${TAG}_pytest_matching.log 2>&1
         rc=$?; echo "pytest matching rc=$rc"; tail -n 5 gpurun_out/${TAG}_pytest_matching.log; ok_or_fail $rc pytest_matching ;;
+    repro0)  # diagnostics of the exit-time SIGSEGV: no cooperative launch
+        timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_repro0 -o run \
+            -- tools/bin/repro_coop_exit 0 > gpurun_out/${TAG}_repro0.log 2>&1
+        rc=$?; echo "repro coop=0 rc=$rc"; tail -n 2 gpurun_out/${TAG}_repro0.log; ok_or_fail $rc repro0 ;;
+    repro1)  # ... one cooperative launch (may fault at exit: run it last)
+        timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_repro1 -o run \
+            -- tools/bin/repro_coop_exit 1 > gpurun_out/${TAG}_repro1.log 2>&1
+        rc=$?; echo "repro coop=1 rc=$rc"; tail -n 2 gpurun_out/${TAG}_repro1.log; ok_or_fail $rc repro1 ;;
+    prof4nocoop)  # cfg4 with the per-panel factorisation (no cooperative launch)
+        M3S_CHOL_DF=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof4nc \
+            -o run -- python bench.py --config cfg4 --steps 3 --warmup 1 --no-cpu-baseline --no-matching \
+            > gpurun_out/${TAG}_prof4nc.log 2>&1
+        rc=$?; echo "rocprof cfg4 (no coop) rc=$rc"; tail -n 3 gpurun_out/${TAG}_prof4nc.log
+        rm -f gpurun_out/${TAG}_prof4nc/*kernel_trace.csv; ok_or_fail $rc rocprof4nc ;;
     esac
 done
 exit 0
