@@ -243,7 +243,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(g, mode, E_und, iters)
         out["accuracy"] = accuracy(g, mode, Twc0, Twc, cpu_baseline.last_poses,
-                                   cpu_baseline.exact_poses, cpu_baseline.full_poses, iters)
+                                   cpu_baseline.exact_poses, cpu_baseline.full_poses, iters,
+                                   cpu_baseline.last_step, cpu_baseline.exact_step)
     if rank == 0 and world == 1 and not args.no_matching:
         out["matching"] = matching_bench(dev)
         out["tracking"] = tracking_bench(dev)
@@ -417,7 +418,8 @@ def tracking_bench(dev, reps=20):
     return res
 
 
-def accuracy(g, mode, Twc0, Twc_final, T_oracle_1, T_exact_1, T_oracle_full, iters):
+def accuracy(g, mode, Twc0, Twc_final, T_oracle_1, T_exact_1, T_oracle_full, iters, dx_oracle_1=None,
+             dx_exact_1=None):
     """'ATE-RMSE vs ref' (BASELINE.json metric): the GPU op's poses after ONE iteration and the
     timed call's poses (``iters`` iterations) against the CPU oracle's (the reference backend
     restated) on the same inputs -- max relative error of the pose data and the Sim(3)-aligned
@@ -430,11 +432,11 @@ def accuracy(g, mode, Twc0, Twc_final, T_oracle_1, T_exact_1, T_oracle_full, ite
 
     T1 = Twc0.clone()
     if mode == "calib":
-        mb.gauss_newton_calib(T1, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
+        (dx1,) = mb.gauss_newton_calib(T1, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
                               LOCAL["pixel_border"], LOCAL["depth_eps"], LOCAL["sigma_pixel"],
                               LOCAL["sigma_depth"], LOCAL["C_conf"], LOCAL["Q_conf"], 1, 0.0)
     else:
-        mb.gauss_newton_rays(T1, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, LOCAL["sigma_ray"],
+        (dx1,) = mb.gauss_newton_rays(T1, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, LOCAL["sigma_ray"],
                              LOCAL["sigma_dist"], LOCAL["C_conf"], LOCAL["Q_conf"], 1, 0.0)
     T1 = T1.cpu().numpy().astype(np.float64)
     To = np.asarray(T_oracle_1, np.float64)
@@ -448,7 +450,16 @@ def accuracy(g, mode, Twc0, Twc_final, T_oracle_1, T_exact_1, T_oracle_full, ite
     ate_init, _ = ate_rmse((ts, gt[:, :3]), (ts, Twc0.cpu().numpy().astype(np.float64)[:, :3]))
     Tf = np.asarray(T_oracle_full, np.float64)
     ate_f, _ = ate_rmse((ts, Tf[:, :3]), (ts, fin[:, :3]))
+    steps = {}
+    if dx_exact_1 is not None:
+        # the first step itself (accumulate + solve), relative to max |dx|: the poses after ONE
+        # step also carry the reference's float Sim(3) exponential, which turns a 1e-7 change of
+        # the log-scale step into ~1e-5 of a translation
+        dxx = np.asarray(dx_exact_1, np.float64)
+        steps = {"step_max_rel_err_vs_exact_sum_1iter": rel(dx1.cpu().numpy().astype(np.float64), dxx),
+                 "reference_order_step_max_rel_err_vs_exact_sum_1iter": rel(np.asarray(dx_oracle_1, np.float64), dxx)}
     return {
+        **steps,
         f"pose_max_rel_err_vs_oracle_{iters}iter_timed_call": rel(fin, Tf),
         f"ate_rmse_vs_oracle_{iters}iter_m": ate_f,
         "pose_max_rel_err_vs_oracle_1iter": rel(T1, To),
@@ -517,13 +528,14 @@ def cpu_baseline(g, mode, E_und, iters):
     times = []
     for r in range(7):
         t0 = time.perf_counter()
-        T_o, _, _ = O.gauss_newton(P1, *arrs)
+        T_o, dx_o, _ = O.gauss_newton(P1, *arrs)
         if r >= 2:
             times.append(time.perf_counter() - t0)
     dt = statistics.median(times)
     cpu_baseline.last_poses = T_o  # the accuracy check compares the GPU's first iteration
+    cpu_baseline.last_step = dx_o
     with O.exact_sums():  # precision reference: the same float terms summed in double
-        cpu_baseline.exact_poses, _, _ = O.gauss_newton(P1, *arrs)
+        cpu_baseline.exact_poses, cpu_baseline.exact_step, _ = O.gauss_newton(P1, *arrs)
     cpu_baseline.full_poses, _, _ = O.gauss_newton(params(iters), *arrs)
     return {
         "value": E_und * 1 / dt,

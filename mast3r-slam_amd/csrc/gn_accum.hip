@@ -52,6 +52,25 @@ __device__ __forceinline__ float vsplat(float s, float) { return s; }
 __device__ __forceinline__ float vrcp(float a) { return __builtin_amdgcn_rcpf(a); }    // v_rcp_f32
 __device__ __forceinline__ float vsqrt(float a) { return __builtin_amdgcn_sqrtf(a); }  // normal or 0 inputs
 __device__ __forceinline__ float vlog2(float a) { return __builtin_amdgcn_logf(a); }   // inputs > z_eps
+// rays mode's normalisation (M3S_RAYS_CR): 0 (default) = the hardware v_sqrt_f32 / v_rcp_f32
+// (1 ulp); 1 = correctly rounded sqrtf and v_rcp_f32 + one Newton step (the reference's sqrtf /
+// 1.0/x are correctly rounded); 2 = v_rsq_f32 + one Newton step.  Measured (tools/
+// accuracy_probe.py, profiles/r03_rays_norm_ab.json): the first GN step of cfg4 lands 2.13e-5 /
+// 2.11e-5 / 2.16e-5 (of max |dx|) from the exactly summed system with 0 / 1 / 2 -- the per-point
+// ulp errors average out in the 4e8-term sums -- while 1 and 2 cost 16 % / 13 % accumulate time.
+#ifndef M3S_RAYS_CR
+#define M3S_RAYS_CR 0
+#endif
+__device__ __forceinline__ float vrcp_nr(float a) {
+    const float r = __builtin_amdgcn_rcpf(a);
+    return fmaf(fmaf(-a, r, 1.0f), r, r);
+}
+// 1/sqrt(a): v_rsq_f32 plus one Newton step y (1.5 - 0.5 a y^2) (~0.5 ulp)
+__device__ __forceinline__ float vrsq_nr(float a) {
+    const float y = __builtin_amdgcn_rsqf(a);
+    const float h = 0.5f * a * y;
+    return fmaf(fmaf(-h, y, 0.5f), y, y);
+}
 __device__ __forceinline__ float vabs(float a) { return fabsf(a); }
 __device__ __forceinline__ float vmin(float a, float b) { return fminf(a, b); }
 __device__ __forceinline__ float vsel(bool m, float a, float b) { return m ? a : b; }
@@ -90,6 +109,8 @@ __device__ __forceinline__ void acc_row(V* __restrict__ acc, const V* r, V w, V 
 
 template <typename V>
 struct PointsIn {
+    // calib: xi2 carries the matched point's INVERSE depth, (z > z_eps) ? v_rcp_f32(z) : NaN (the
+    // packed path gathers it precomputed per call, gn_depth_kernel; NaN encodes z <= z_eps)
     V xi0, xi1, xi2, xj0, xj1, xj2;
     V sq;                            // sqrt(q)
     typename VMask<V>::type valid;   // match & q > Q_thresh & ci > C_thresh & cj > C_thresh
@@ -154,11 +175,23 @@ __device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T,
     if constexpr (MODE == GN_RAYS) {
         // gn_kernels.cu:924-1089
         const V n2i = vfma(p.xi0, p.xi0, vfma(p.xi1, p.xi1, p.xi2 * p.xi2));
+        const V n2j = vfma(X0, X0, vfma(X1, X1, X2 * X2));
+#if M3S_RAYS_CR == 1
+        const V n1i = __builtin_sqrtf(n2i);
+        const V n1i_inv = vrcp_nr(n1i);
+        const V n1j = __builtin_sqrtf(n2j);
+        const V n1j_inv = vrcp_nr(n1j);
+#elif M3S_RAYS_CR == 2
+        const V n1i_inv = vrsq_nr(n2i);
+        const V n1i = n2i * n1i_inv;
+        const V n1j_inv = vrsq_nr(n2j);
+        const V n1j = n2j * n1j_inv;
+#else
         const V n1i = vsqrt(n2i);
         const V n1i_inv = vrcp(n1i);
-        const V n2j = vfma(X0, X0, vfma(X1, X1, X2 * X2));
         const V n1j = vsqrt(n2j);
         const V n1j_inv = vrcp(n1j);
+#endif
         const V rx = n1j_inv * X0, ry = n1j_inv * X1, rz = n1j_inv * X2;
         const V e0 = rx - n1i_inv * p.xi0;
         const V e1 = ry - n1i_inv * p.xi1;
@@ -171,7 +204,13 @@ __device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T,
         const V w1 = huber(swr * e1) * wcr;
         const V w2 = huber(swr * e2) * wcr;
         const V w3 = huber(swd * e3) * wcd;
+#if M3S_RAYS_CR == 2
+        const V n3 = n1j_inv * n1j_inv * n1j_inv;
+#elif M3S_RAYS_CR
+        const V n3 = n1j_inv * vrcp_nr(n2j);
+#else
         const V n3 = n1j_inv * vrcp(n2j);
+#endif
         const V dxx = n1j_inv - X0 * X0 * n3;
         const V dyy = n1j_inv - X1 * X1 * n3;
         const V dzz = n1j_inv - X2 * X2 * n3;
@@ -196,13 +235,13 @@ __device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T,
         }
     } else if constexpr (MODE == GN_CALIB) {
         // gn_kernels.cu:1360-1495
-        const auto valid_z = vand(vgt(X2, P.z_eps), vgt(p.xi2, P.z_eps));
+        const auto valid_z = vand(vgt(X2, P.z_eps), p.xi2 == p.xi2);  // zi > z_eps <=> 1/zi not NaN
         const V zj_inv = vsel(valid_z, vrcp(X2), zero);
         // log(zj) - log(zi) (gn_kernels.cu:1385-1390) as ln2 * log2(zj / zi): the residual is a
         // small difference of two ~unit logs, so one log of the ratio keeps it to ~1e-7
         // relative where two float logs lose ~1e-4 of it to cancellation (inf/NaN still
         // propagate: 1/inf = 0 -> -inf).
-        const V e2 = vsel(valid_z, vsplat(0.69314718055994531f, X2) * vlog2(X2 * vrcp(p.xi2)), zero);
+        const V e2 = vsel(valid_z, vsplat(0.69314718055994531f, X2) * vlog2(X2 * p.xi2), zero);
         const V x = X0 * zj_inv, y = X1 * zj_inv;
         const V u = vfma(vsplat(P.fx, x), x, vsplat(P.cx, x));
         const V v = vfma(vsplat(P.fy, y), y, vsplat(P.cy, y));
@@ -287,6 +326,15 @@ __device__ __forceinline__ int match_index(int64_t id, bool vm, int HW) {
     return vm ? c : 0;
 }
 
+// calib: the per-call inverse depths follow the depths Zs [nkf * HW] and the ray tables (<= HW
+// floats): IZs = Zs + (nkf + 1) * HW (gn_depth_kernel; the driver sizes the region)
+__device__ __forceinline__ float* inv_depths(float* Zs, const AccParams& P) {
+    return Zs + ((int64_t)P.nkf + 1) * P.HW;
+}
+__device__ __forceinline__ const float* inv_depths(const float* Zs, const AccParams& P) {
+    return Zs + ((int64_t)P.nkf + 1) * P.HW;
+}
+
 // ind / W and ind % W exactly by multiply-shift (Granlund-Montgomery, ind < 2^31).
 __device__ __forceinline__ void pixel_of(int ind, const AccParams& P, float& ut, float& vt) {
     const unsigned q = (unsigned)(((uint64_t)(unsigned)ind * P.div_m) >> P.div_sh);
@@ -361,7 +409,8 @@ struct AccStage {
     unsigned rc_m = 0;             // RC: k / W by multiply-shift
     int rc_sh = 0, rc_w = 1;
 
-    // Zi_b: the dense depth array (packed path), or nullptr to read the depth from Xs
+    // Zi_b (calib): the dense inverse-depth array (packed path), or nullptr to read the raw depth
+    // from Xs (the unpacked path then converts it to the inverse before compute)
     template <int M>
     __device__ __forceinline__ void load(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
                                          const float* __restrict__ Zi_b, int k) {
@@ -496,7 +545,12 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
             AccStage<MODE> st;
             st.ka = int4{code[0], sqb[0], code[1], sqb[1]};
             st.kb = int4{code[2], sqb[2], code[3], sqb[3]};
-            st.template load<MODE>(Xj_b, Xi_b, nullptr, k);  // calib: the depth from Xs
+            st.template load<MODE>(Xj_b, Xi_b, nullptr, k);  // calib: the depth from Xs ...
+            if constexpr (MODE == GN_CALIB) {
+#pragma unroll
+                for (int s = 0; s < 4; s++)  // ... as the inverse depth gn_depth_kernel tabulates
+                    st.g[s][2] = st.g[s][2] > P.z_eps ? vrcp(st.g[s][2]) : __builtin_nanf("");
+            }
             st.template compute<MODE>(T, P, accs);
         }
     } else {
@@ -513,6 +567,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
             p.xi0 = Xi_b[(int64_t)ind * 3 + 0];
             p.xi1 = Xi_b[(int64_t)ind * 3 + 1];
             p.xi2 = Xi_b[(int64_t)ind * 3 + 2];
+            if constexpr (MODE == GN_CALIB) p.xi2 = p.xi2 > P.z_eps ? vrcp(p.xi2) : __builtin_nanf("");
             p.valid = vm && (q > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (Cj_b[k] > P.C_thresh);
             p.sq = vsqrt(q);
             if constexpr (MODE == GN_CALIB) pixel_of(ind, P, p.ut, p.vt);
@@ -690,8 +745,10 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
     if (tid == 0) pcnt[(int64_t)e * P.nchunks + c] = running + pad;
 }
 
-// Zs[n, k] = Xs[n, k, 2]: the only coordinate of the matched point calib mode reads, as a
-// dense 4-B array so the per-iteration gather touches 4 B per point instead of a 12-B stride.
+// Zs[n, k] = Xs[n, k, 2], and after the ray tables the inverse depths IZs[n, k] =
+// (z > z_eps) ? v_rcp_f32(z) : NaN -- what the calib accumulate gathers for the matched point (4 B
+// per point instead of a 12-B stride; the reciprocal and the z_eps test hoisted out of the
+// iterations: the same values, one transcendental per point-edge and iteration less).
 // Also the ray tables tu[u] = (u - cx) / fx, tv[v] = (v - cy) / fy (after Zs), and a check that
 // every point IS its pixel's ray times its depth, bit for bit, i.e. what solve_GN_calib's
 // constrain_points_to_ray (global_opt.py:172, geometry.py:37-42/107-123: z * ((u - cx) / fx))
@@ -702,6 +759,7 @@ __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__
                                                        int* __restrict__ flags) {
     float* __restrict__ tu = Zs + total;
     float* __restrict__ tv = tu + P.width;
+    float* __restrict__ IZn = inv_depths(Zs, P) + (int64_t)blockIdx.y * P.HW;
     const int n = blockIdx.y;  // keyframe row
     const int t0 = blockIdx.x * 256 + threadIdx.x;
     if (n == 0 && t0 < P.width) tu[t0] = ((float)t0 - P.cx) / P.fx;
@@ -712,6 +770,7 @@ __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__
     for (int k = t0; k < P.HW; k += gridDim.x * 256) {
         const float x = Xn[(int64_t)k * 3], y = Xn[(int64_t)k * 3 + 1], z = Xn[(int64_t)k * 3 + 2];
         Zn[k] = z;
+        IZn[k] = z > P.z_eps ? vrcp(z) : __builtin_nanf("");
         float u, v;
         pixel_of(k, P, u, v);
         const float xr = z * ((u - P.cx) / P.fx);
@@ -806,7 +865,7 @@ void gn_accum_packed_kernel(
     const int HW = P.HW;
     const int64_t ebase = (int64_t)e * HW;
     const float* __restrict__ Xi_b = Xs + (int64_t)ix * HW * 3;
-    const float* __restrict__ Zi_b = Zs + (int64_t)ix * HW;
+    const float* __restrict__ Zi_b = MODE == GN_CALIB ? inv_depths(Zs, P) + (int64_t)ix * HW : nullptr;
     const float* __restrict__ Xj_b = Xs + (int64_t)jx * HW * 3;
     const int4* __restrict__ pk_b = pack + ebase / 2;
     const int k0 = c * P.chunk;

@@ -260,7 +260,8 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
         L.packx = L.pcnt = L.pack;  // unused
     }
     // + the ray tables tu[W], tv[H] (gn_depth_kernel); HW floats is an upper bound for W + H
-    L.zs = take(mode == M3S_GN_CALIB ? sizeof(float) * ((size_t)N + 1) * (size_t)HW + 64 : 0);
+    // + the inverse depths IZs [N, HW] after the tables (gn_accum.hip inv_depths)
+    L.zs = take(mode == M3S_GN_CALIB ? sizeof(float) * (2 * (size_t)N + 1) * (size_t)HW + 64 : 0);
     L.total = off;
     return L;
 }

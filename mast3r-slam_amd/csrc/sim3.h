@@ -91,6 +91,16 @@ __device__ __forceinline__ void cross_inplace(const float* a, float* b) {
     b[0] = x0; b[1] = x1; b[2] = x2;
 }
 
+// The Sim(3) exponential's float transcendentals, correctly rounded (evaluated in double and
+// rounded once; oracle/m3s_oracle.c does the same).  The reference's CUDA expf / sinf / cosf are
+// <= 2 ulp and platform-specific, and its float formulas amplify one ulp of them enormously --
+// C = (expf(sigma) - 1) / sigma moves by ulp(1) / sigma (~1 % at sigma = 1e-5, i.e. ~1e-5 of a
+// pose after a first GN step) -- so no other platform can reproduce its bits there; with
+// correctly rounded values the op and the oracle retract the same step to the same bits.
+__device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float sinf_cr(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cosf_cr(float x) { return (float)cos((double)x); }
+
 // gn_kernels.cu:299-321 (the small-angle series is double arithmetic: fused in double too)
 template <int CM = M3S_CONTRACT_DEFAULT>
 __device__ __forceinline__ void exp_so3(const float* phi, float* q) {
@@ -104,8 +114,8 @@ __device__ __forceinline__ void exp_so3(const float* phi, float* q) {
         real = (float)cmad_d(F, 1.0 / 384.0, (double)theta_p4, cmad_d(F, -(1.0 / 8.0), (double)theta_sq, 1.0));
     } else {
         const float theta = sqrtf(theta_sq);
-        imag = sinf((float)(0.5 * (double)theta)) / theta;
-        real = cosf((float)(0.5 * (double)theta));
+        imag = sinf_cr((float)(0.5 * (double)theta)) / theta;
+        real = cosf_cr((float)(0.5 * (double)theta));
     }
     q[0] = imag * phi[0];
     q[1] = imag * phi[1];
@@ -120,7 +130,7 @@ __device__ __forceinline__ void exp_sim3(const float* xi, float* t, float* q, fl
     float tau[3] = {xi[0], xi[1], xi[2]};
     const float phi[3] = {xi[3], xi[4], xi[5]};
     const float sigma = xi[6];
-    const float scale = expf(sigma);
+    const float scale = expf_cr(sigma);
     exp_so3<CM>(phi, q);
     s[0] = scale;
     const float theta_sq = cdot3<CM>(phi[0], phi[0], phi[1], phi[1], phi[2], phi[2]);
@@ -133,8 +143,8 @@ __device__ __forceinline__ void exp_sim3(const float* xi, float* t, float* q, fl
             A = half;
             B = (float)(1.0 / 6.0);
         } else {
-            A = (one - cosf(theta)) / theta_sq;
-            B = (theta - sinf(theta)) / (theta_sq * theta);
+            A = (one - cosf_cr(theta)) / theta_sq;
+            B = (theta - sinf_cr(theta)) / (theta_sq * theta);
         }
     } else {
         C = (scale - one) / sigma;
@@ -143,8 +153,8 @@ __device__ __forceinline__ void exp_sim3(const float* xi, float* t, float* q, fl
             A = cmad<CM>(sigma - one, scale, one) / sigma_sq;
             B = cmad<CM>(-sigma, scale, cmad<CM>(scale * half, sigma_sq, scale) - one) / (sigma_sq * sigma);
         } else {
-            const float a = scale * sinf(theta);
-            const float b = scale * cosf(theta);
+            const float a = scale * sinf_cr(theta);
+            const float b = scale * cosf_cr(theta);
             const float c = cmad<CM>(sigma, sigma, theta_sq);
             A = cmm<CM>(a, sigma, one - b, theta) / (theta * c);
             B = (C - cmm<CM>(b - one, sigma, a, theta) / c) / theta_sq;

@@ -478,6 +478,14 @@ void oracle_apply_sim3_adj_inv(const float* t, const float* q, const float* s, c
 /* double a*b + c, fused under every contracting convention */
 static inline double cmad_d(int cm, double a, double b, double c) { return cm != ORACLE_CONTRACT_OFF ? fma(a, b, c) : a * b + c; }
 
+/* The Sim(3) exponential's float transcendentals correctly rounded (double, rounded once), as
+ * the op evaluates them (mast3r-slam_amd/csrc/sim3.h): the reference's CUDA expf / sinf / cosf
+ * (<= 2 ulp) are not reproducible off its platform, and its float formulas amplify one ulp
+ * ~1/sigma-fold ((expf(sigma) - 1) / sigma), so both sides use the correctly rounded value. */
+static inline float expf_cr(float x) { return (float)exp((double)x); }
+static inline float sinf_cr(float x) { return (float)sin((double)x); }
+static inline float cosf_cr(float x) { return (float)cos((double)x); }
+
 /* :299-321 (the small-angle series is double arithmetic) */
 static void expSO3(const float* phi, float* q) {
     float theta_sq = squared_norm3(phi);
@@ -488,8 +496,8 @@ static void expSO3(const float* phi, float* q) {
         real = (float)cmad_d(CM, 1.0 / 384.0, (double)theta_p4, cmad_d(CM, -(1.0 / 8.0), (double)theta_sq, 1.0));
     } else {
         float theta = sqrtf(theta_sq);
-        imag = sinf((float)(0.5 * (double)theta)) / theta;
-        real = cosf((float)(0.5 * (double)theta));
+        imag = sinf_cr((float)(0.5 * (double)theta)) / theta;
+        real = cosf_cr((float)(0.5 * (double)theta));
     }
     q[0] = imag * phi[0];
     q[1] = imag * phi[1];
@@ -502,7 +510,7 @@ void oracle_exp_sim3(const float* xi, float* t, float* q, float* s) {
     float tau[3] = {xi[0], xi[1], xi[2]};
     float phi[3] = {xi[3], xi[4], xi[5]};
     float sigma = xi[6];
-    float scale = expf(sigma);
+    float scale = expf_cr(sigma);
     expSO3(phi, q);
     s[0] = scale;
     float theta_sq = squared_norm3(phi);
@@ -516,8 +524,8 @@ void oracle_exp_sim3(const float* xi, float* t, float* q, float* s) {
             A = half;
             B = (float)(1.0 / 6.0);
         } else {
-            A = (one - cosf(theta)) / theta_sq;
-            B = (theta - sinf(theta)) / (theta_sq * theta);
+            A = (one - cosf_cr(theta)) / theta_sq;
+            B = (theta - sinf_cr(theta)) / (theta_sq * theta);
         }
     } else {
         C = (scale - one) / sigma;
@@ -526,8 +534,8 @@ void oracle_exp_sim3(const float* xi, float* t, float* q, float* s) {
             A = cmad(CM, sigma - one, scale, one) / sigma_sq;
             B = cmad(CM, -sigma, scale, cmad(CM, scale * half, sigma_sq, scale) - one) / (sigma_sq * sigma);
         } else {
-            float a = scale * sinf(theta);
-            float b = scale * cosf(theta);
+            float a = scale * sinf_cr(theta);
+            float b = scale * cosf_cr(theta);
             float c = cmad(CM, sigma, sigma, theta_sq);
             A = cmm(CM, a, sigma, one - b, theta) / (theta * c);
             B = (C - cmm(CM, b - one, sigma, a, theta) / (c)) / (theta_sq);
@@ -926,6 +934,29 @@ void oracle_gn_assemble(const float* Hs, const float* gs, const int64_t* ii_opt,
     gn_assemble_d(Hd, gd, ii_opt, jj_opt, N, E, H, b);
     free(Hd);
     free(gd);
+}
+
+/* The dense system of one iteration as oracle_gauss_newton forms it (the per-edge blocks kept in
+ * double: outside exact-sums mode they are float values already, so this equals gn_align +
+ * gn_assemble; in exact-sums mode it is the exactly summed system, unrounded). */
+void oracle_gn_system(const oracle_gn_params* P, const float* Twc, const float* Xs, const float* Cs,
+                      const int64_t* ii_edge, const int64_t* jj_edge, const int64_t* idx,
+                      const uint8_t* valid, const float* Q, int64_t N, int64_t HW, int64_t E,
+                      double* H, double* b) {
+    double* Hd = (double*)malloc(sizeof(double) * 4 * E * 49 + 8);
+    double* gd = (double*)malloc(sizeof(double) * 2 * E * 7 + 8);
+    int64_t* ii_opt = (int64_t*)malloc(sizeof(int64_t) * (E + 1));
+    int64_t* jj_opt = (int64_t*)malloc(sizeof(int64_t) * (E + 1));
+    for (int64_t e = 0; e < E; e++) {
+        ii_opt[e] = ii_edge[e] - 1;
+        jj_opt[e] = jj_edge[e] - 1;
+    }
+    gn_align_impl(P, Twc, Xs, Cs, ii_edge, jj_edge, idx, valid, Q, N, HW, E, Hd, gd);
+    gn_assemble_d(Hd, gd, ii_opt, jj_opt, N, E, H, b);
+    free(Hd);
+    free(gd);
+    free(ii_opt);
+    free(jj_opt);
 }
 
 static void gn_assemble_d(const double* Hs, const double* gs, const int64_t* ii_opt,

@@ -119,6 +119,13 @@ void oracle_gn_assemble(const float* Hs, const float* gs, const int64_t* ii_opt,
                         const int64_t* jj_opt, int64_t N, int64_t E,
                         double* H, double* b);
 
+/* One iteration's dense system with the per-edge blocks kept in double (equal to align +
+ * assemble unless exact sums are on; then the exactly summed system, unrounded). */
+void oracle_gn_system(const oracle_gn_params* P, const float* Twc, const float* Xs, const float* Cs,
+                      const int64_t* ii_edge, const int64_t* jj_edge, const int64_t* idx,
+                      const uint8_t* valid, const float* Q, int64_t N, int64_t HW, int64_t E,
+                      double* H, double* b);
+
 /* SimplicialLLT semantics: returns 0 on success, 1 when a pivot <= 0.  */
 int oracle_cholesky_solve(double* H, const double* b, double* x, int64_t n);
 

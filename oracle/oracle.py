@@ -64,6 +64,7 @@ _P = ctypes.POINTER(GNParams)
 _lib.oracle_gn_align.argtypes = [_P] + [_vp] * 8 + [_i64] * 3 + [_vp, _vp]
 _lib.oracle_gn_residuals.argtypes = [_P] + [_vp] * 8 + [_i64] * 3 + [_vp] * 4
 _lib.oracle_gn_assemble.argtypes = [_vp] * 4 + [_i64, _i64, _vp, _vp]
+_lib.oracle_gn_system.argtypes = [_P] + [_vp] * 8 + [_i64] * 3 + [_vp, _vp]
 _lib.oracle_cholesky_solve.argtypes = [_vp, _vp, _vp, _i64]
 _lib.oracle_cholesky_solve.restype = _i
 _lib.oracle_pose_retr.argtypes = [_vp, _vp, _i64, _i]
@@ -284,11 +285,18 @@ def gn_assemble(Hs, gs, ii_opt, jj_opt, N):
 
 
 def gn_build_system(P, Twc, Xs, Cs, ii, jj, idx, valid, Q):
-    """Dense normal equations of ONE iteration at the current Twc (reference SparseBlock)."""
+    """Dense normal equations of ONE iteration at the current Twc (reference SparseBlock), as
+    gauss_newton forms them (under ``exact_sums()``: the exactly summed system, unrounded)."""
     ie, je, _ = remap(ii, jj)
-    Hs, gs = gn_align(P, Twc, Xs, Cs, ie, je, idx, valid, Q)
-    N = np.asarray(Xs).shape[0]
-    return gn_assemble(Hs, gs, ie - 1, je - 1, N)
+    Twc, Xs, Cs = _c(Twc, np.float32), _c(Xs, np.float32), _c(Cs, np.float32)
+    idx, valid, Q = _c(idx, np.int64), _c(valid, np.uint8), _c(Q, np.float32)
+    N, HW = Xs.shape[0], Xs.shape[1]
+    n = 7 * (N - 1)
+    H = np.zeros((n, n), np.float64)
+    b = np.zeros((n,), np.float64)
+    _lib.oracle_gn_system(ctypes.byref(P), _p(Twc), _p(Xs), _p(Cs), _p(ie), _p(je), _p(idx), _p(valid),
+                          _p(Q), N, HW, ie.shape[0], _p(H), _p(b))
+    return H, b
 
 
 def cholesky_solve(H, b):

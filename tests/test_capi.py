@@ -35,10 +35,11 @@ def test_workspace_size_query(backend):
     small = f(1, 2, 64, 2, 2)
     big = f(2, 128, 384 * 512, 512, 512)
     assert 0 < small < big
-    # cfg3: the per-call packed stream (8 B per directed point-edge) dominates; the dense f64
-    # matrices are not part of it (sized per call by the solver actually used)
+    # cfg3: the per-call packed stream (8 B per directed point-edge) dominates, then the calib
+    # depth / ray-table / inverse-depth arrays ((2N + 1) HW floats); the dense f64 matrices are
+    # not part of it (sized per call by the solver actually used)
     HW = 384 * 512
-    assert 8 * 512 * HW < big < 8 * 512 * HW + (128 + 1) * HW * 4 + 64 * 2**20
+    assert 8 * 512 * HW < big < 8 * 512 * HW + (2 * 128 + 1) * HW * 4 + 64 * 2**20
     # far beyond the dense-solve limit (1171 keyframes): still a valid (sparse-path) size
     huge = f(1, 4096, 64, 8192, 8192)
     assert 0 < huge < 64 * 2**20

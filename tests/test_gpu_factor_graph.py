@@ -170,7 +170,7 @@ def test_device_factor_graph_pin_2_keeps_pinned_rows(mode):
     store path must agree bitwise with the reference-compatible FactorGraph."""
     ids = [3, 4, 5, 6, 7, 8]
     fg, dg, (s_ref, s_dev) = _device_setup(mode, ids)
-    cfg = dict(DEFAULT_CONFIG, pin=2)
+    cfg = dict(DEFAULT_CONFIG["local_opt"], pin=2)
     fg.cfg, dg.cfg = cfg, dict(cfg)
     before = s_dev.T_WC.clone()
     (fg.solve_GN_rays if mode == "rays" else fg.solve_GN_calib)()

@@ -284,25 +284,30 @@ def test_compacted_stream_keeps_nan_poisoning_and_empty_edges(backend, oracle, m
     assert np.isnan(H).any() and np.array_equal(np.isnan(H), np.isnan(H_p))
 
 
-def test_full_size_cfg3_calib_within_1e5_of_exactly_summed_system(backend, oracle):
+def test_full_size_cfg3_calib_step_closer_to_exactly_summed_system(backend, oracle):
     """BASELINE's graph (cfg3: 128 keyframes, 256 pairs, 512x384, calib), one iteration.
-    Summation order matters at this size: the reference's float order (the oracle mirrors
-    it, gn_kernels.cu:31-55) lands ~8e-5 (relative) from the poses obtained when the same
-    float terms are summed in double, so the HIP path (f32 lane partials, f64 across
-    workgroups) is pinned against that exactly summed system at the 1e-5 north-star bar,
-    and must be closer to it than the reference's own order."""
+    Summation order matters at this size: the reference's float order (the oracle mirrors it,
+    gn_kernels.cu:31-55) puts the first step 2.4e-3 (of max |dx|) from the step obtained when
+    the same float terms are summed in double; the HIP path (f32 lane partials over short
+    chunks, f64 across workgroups) must land closer to that exactly summed step than the
+    reference order does (measured: 6e-5), and its poses are the oracle's retraction of its
+    own step, bit for bit (poses after ONE step are not compared across different steps:
+    see test_cfg4_full_size_one_and_ten_iterations)."""
     g = synth.make_graph("cfg3")
     from m3s.geometry import constrain_points_to_ray
 
     g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
-    T_gpu, _ = _run_gpu(backend, g, "calib", 1)
-    T_ref, _, _ = _run_oracle(oracle, g, "calib", 1)
+    T_gpu, dx_gpu = _run_gpu(backend, g, "calib", 1)
+    _, dx_ref, _ = _run_oracle(oracle, g, "calib", 1)
     with oracle.exact_sums():
-        T_exact, _, _ = _run_oracle(oracle, g, "calib", 1)
-    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
-    assert rel(T_gpu, T_exact) < 1e-5
-    assert rel(T_gpu, T_exact) <= rel(T_ref, T_exact)
-    assert rel(T_gpu, T_ref) < 2e-4  # the reference order's own rounding (see above)
+        _, dx_x, _ = _run_oracle(oracle, g, "calib", 1)
+    step = lambda d: float(np.abs(d.astype(np.float64) - dx_x).max() / np.abs(dx_x).max())
+    print(f"cfg3 first step: op {step(dx_gpu):.2e}, reference order {step(dx_ref):.2e} (of max |dx|)")
+    assert step(dx_gpu) <= step(dx_ref)
+    assert step(dx_gpu) < 1e-3
+    T0 = g.Twc.numpy()
+    T_r = np.stack([T0[0]] + [oracle.retr_sim3(dx_gpu[i - 1], T0[i]) for i in range(1, T0.shape[0])])
+    assert np.array_equal(T_gpu, T_r), _rel(T_gpu, T_r)
 
 
 @pytest.mark.parametrize("iters", [3, 6])
@@ -376,22 +381,33 @@ def test_cfg1_keyframe_pair_matches_oracle(backend, oracle, mode):
 @pytest.mark.timeout(600)
 def test_cfg4_full_size_one_and_ten_iterations(backend, oracle):
     """BASELINE config 4 at full size on one GPU (256 keyframes, 1024 pairs = 2048 directed
-    edges, 512x384, gauss_newton_rays).  One iteration: at this size the first pose update is
-    only determined to the fp32 rounding of its ~4e8 summed terms (sigma = the distance between
-    the oracle's reference order and the same float terms summed in double: 4e-6 on this graph,
-    2.5e-5 on bench.py's), and per-point rounding differences (the op's affine-map form of
-    T_ij x, gn_accum.hip) move it by the same amount -- so the op must agree with both within
-    max(1e-5, 4 sigma).  The formula itself is pinned at 1e-5 by the reference-order mode
-    (test_gpu_gn_reference_order.py).  Ten iterations (the timed call): within the north-star
-    1e-5 of the oracle, finite, deterministic (two runs bitwise equal), converging."""
+    edges, 512x384, gauss_newton_rays).
+
+    One iteration, split into its two stages:
+      * the step dx (accumulate + solve): at this size it is only determined to the fp32
+        rounding of its ~4e8 summed terms -- sigma = the distance of the oracle's step (the
+        reference order) from the step of the same float terms summed in double (1.7e-4 of
+        max |dx| on this graph) -- so the op's step must lie within max(1e-5, 4 sigma) of the
+        exactly summed one (measured: 2e-5, eight times closer than the reference order);
+      * the retraction: the op's poses are the oracle's retraction of the op's own step, bit
+        for bit (sim3.h; both evaluate the Sim(3) exponential's transcendentals correctly
+        rounded).  Poses after one step are NOT compared across different steps: the
+        reference's float exponential turns a 1e-7 change of the log-scale into a ~1e-5 change
+        of the translation ((expf(sigma) - 1) / sigma at sigma ~ 1e-5), whichever side is right.
+    Ten iterations (the timed call): within the north-star 1e-5 of the oracle, finite,
+    deterministic (two runs bitwise equal), converging."""
     g = synth.make_graph("cfg4")
     T1, dx1 = _run_gpu(backend, g, "rays", 1)
-    T_o, _, _ = _run_oracle(oracle, g, "rays", 1)
+    _, dx_o, _ = _run_oracle(oracle, g, "rays", 1)
     with oracle.exact_sums():
-        T_exact, _, _ = _run_oracle(oracle, g, "rays", 1)
-    bound = max(1e-5, 4 * _rel(T_o, T_exact))
-    assert _rel(T1, T_o) < bound, (_rel(T1, T_o), bound)
-    assert _rel(T1, T_exact) < bound, (_rel(T1, T_exact), bound)
+        _, dx_x, _ = _run_oracle(oracle, g, "rays", 1)
+    step = lambda d: float(np.abs(d.astype(np.float64) - dx_x).max() / np.abs(dx_x).max())
+    bound = max(1e-5, 4 * step(dx_o))
+    print(f"cfg4 first step: op {step(dx1):.2e}, reference order {step(dx_o):.2e} (of max |dx|)")
+    assert step(dx1) < bound, (step(dx1), bound)
+    T0 = g.Twc.numpy()
+    T_r = np.stack([T0[0]] + [oracle.retr_sim3(dx1[i - 1], T0[i]) for i in range(1, T0.shape[0])])
+    assert np.array_equal(T1, T_r), _rel(T1, T_r)
     Ta, dxa = _run_gpu(backend, g, "rays", 10)
     Tb, dxb = _run_gpu(backend, g, "rays", 10)
     assert np.isfinite(Ta).all() and np.array_equal(Ta, Tb) and np.array_equal(dxa, dxb)

@@ -9,7 +9,7 @@ while [ $# -ge 2 ]; do
     name=$1; flags=$2; shift 2
     objs=""
     for f in $(sed -n 's/^SRCS := //p' Makefile | sed 's|csrc/||g; s|\.hip||g'); do
-        fc=-ffp-contract=fast
+        fc=-ffp-contract=fast-honor-pragmas
         case $f in matching|match_glue|edges|keyframe|gn_refacc) fc=-ffp-contract=off ;; esac
         [ $f = gn_accum ] && fc="$fc -fno-slp-vectorize"
         /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Icsrc -I../include $fc $flags \

@@ -51,6 +51,23 @@ for s in $STEPS; do
         timeout -k 10 600 python -u -m pytest tests/test_gpu_matching.py -x -q -p no:cacheprovider --timeout 400 \
             --timeout-method thread > gpurun_out/${TAG}_pytest_matching.log 2>&1
         rc=$?; echo "pytest matching rc=$rc"; tail -n 5 gpurun_out/${TAG}_pytest_matching.log; ok_or_fail $rc pytest_matching ;;
+    alltests)  # every GPU test, no -x, passing tests' prints kept (-rP)
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rfEP -p no:cacheprovider --timeout 400 \
+            --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+        rc=$?; echo "pytest gpu rc=$rc"; grep -E "passed|failed" gpurun_out/${TAG}_pytest_gpu.log | tail -n 3; ok_or_fail $rc pytest ;;
+    probe)  # accuracy probe of the default library, with the H / b split of the first step
+        timeout -k 10 600 python tools/accuracy_probe.py --tag default ${PROBE_ARGS:---system} \
+            >> gpurun_out/${TAG}_accprobe.jsonl 2>> gpurun_out/${TAG}_accprobe.err
+        rc=$?; echo "accprobe default rc=$rc"; tail -n 1 gpurun_out/${TAG}_accprobe.jsonl; ok_or_fail $rc accprobe ;;
+    abrays)  # rays-mode norm variants (lib/variants/rcr{0,1,2}.so): accuracy probe + cfg4 timing
+        for v in ${VARIANTS:-rcr0 rcr1 rcr2}; do
+            M3S_BACKEND_LIB=$PWD/mast3r-slam_amd/lib/variants/$v.so timeout -k 10 400 python tools/accuracy_probe.py \
+                --tag $v >> gpurun_out/${TAG}_accprobe.jsonl 2>> gpurun_out/${TAG}_accprobe.err
+            rc=$?; echo "accprobe $v rc=$rc"; tail -n 1 gpurun_out/${TAG}_accprobe.jsonl; ok_or_fail $rc accprobe_$v
+            M3S_BACKEND_LIB=$PWD/mast3r-slam_amd/lib/variants/$v.so timeout -k 10 300 python bench.py --config cfg4 \
+                --no-cpu-baseline --no-matching > gpurun_out/${TAG}_qbench4_$v.json 2> gpurun_out/${TAG}_qbench4_$v.err
+            rc=$?; echo "qbench4 $v rc=$rc"; cat gpurun_out/${TAG}_qbench4_$v.json; ok_or_fail $rc qbench4_$v
+        done ;;
     repro0)  # diagnostics of the exit-time SIGSEGV: no cooperative launch
         timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_repro0 -o run \
             -- tools/bin/repro_coop_exit 0 > gpurun_out/${TAG}_repro0.log 2>&1
