@@ -37,8 +37,11 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "keyframe-pair GN iters/sec @512×384, 256 edges; ATE-RMSE vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 REF_BYTES_PER_POINT_EDGE = 45  # Xj 12 + Xi 12 + Cj 4 + Ci 4 + Q 4 + idx 8 + valid 1
-# packed formulation (>= 3 iterations per call): record 8 + Xj 12 + matched point (calib: z 4; else Xi 12)
+# packed formulation (>= 3 iterations per call): record 8 + Xj 12 + matched point (calib: z 4; else Xi 12);
+# calib with ray-constrained keyframe points (solve_GN_calib's constrain_points_to_ray): Xj is read
+# as its 4-B depth (x, y from the pixel's ray), record 8 + depth 4 + matched inverse depth 4 = 16
 PACKED_BYTES_PER_POINT_EDGE = {"calib": 24, "rays": 32, "points": 32}
+RAY_BYTES_PER_POINT_EDGE = 16
 LOCAL = dict(sigma_ray=0.003, sigma_dist=10.0, sigma_pixel=1.0, sigma_depth=10.0, sigma_point=0.05,
              C_conf=0.0, Q_conf=1.5, pixel_border=-10, depth_eps=1e-6)  # base.yaml:35-50
 
@@ -167,6 +170,14 @@ def main():
     ph = (ctypes.c_double * 4)()
     nph = ctypes.c_int(0)
     mb.lib.m3s_prof_end(ph, ctypes.byref(nph))
+    # which accumulate path the op took (its device flags, read back by one more untimed call)
+    os.environ["M3S_GN_DEBUG_FLAGS"] = "2"
+    step()
+    torch.cuda.synchronize()
+    del os.environ["M3S_GN_DEBUG_FLAGS"]
+    dbg = (ctypes.c_int * 4)()
+    mb.lib.m3s_gn_debug_flags(dbg)
+    ray_path = bool(dbg[3])
     n_ph = max(nph.value, 1)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -178,7 +189,10 @@ def main():
     n_it = max(nprof.value, 1)
     acc_ms = prof[0] / n_it if acc_events else ph[0] / n_ph
     packed = iters >= 3 and os.environ.get("M3S_GN_PACK", "1") != "0"
-    bpe = PACKED_BYTES_PER_POINT_EDGE[mode] if packed else REF_BYTES_PER_POINT_EDGE
+    bpe = (RAY_BYTES_PER_POINT_EDGE if ray_path else PACKED_BYTES_PER_POINT_EDGE[mode]) if packed \
+        else REF_BYTES_PER_POINT_EDGE
+    stream = ("packed, ray-constrained Xj (depth only)" if ray_path else "packed") if packed \
+        else "reference tensors"
     bytes_launch = bpe * g.HW * (hi - lo)
     ref_bytes_launch = REF_BYTES_PER_POINT_EDGE * g.HW * (hi - lo)
     achieved = bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
@@ -187,7 +201,7 @@ def main():
         try:
             tf = json.load(open(args.traffic_file))
             if (tf.get("config") == args.config and tf.get("n_gpus", 1) == world
-                    and tf.get("packed", False) == packed):
+                    and tf.get("packed", False) == packed and tf.get("stream") == stream):
                 traffic = tf.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -233,6 +247,7 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_launch,
             "algorithmic_bytes_per_point_edge": bpe,
+            "stream": stream,
             "avg_launch_ms": acc_ms,
             "ref_formulation_bytes_per_launch": ref_bytes_launch,
             "ref_formulation_equiv_GBps": ref_bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None,
@@ -289,46 +304,26 @@ def matching_bench(dev, reps=10):
             if r >= 2:
                 t_ip += ev[0].elapsed_time(ev[1]) / reps
                 t_rf += ev[1].elapsed_time(ev[2]) / reps
-        # A/B: the LDS-tiled refine kernel (M3S_REFINE_LDS=1, opt-in) vs the default gather kernel
-        os.environ["M3S_REFINE_LDS"] = "1"
-        t_gather = 0.0
-        for r in range(reps + 2):
-            ev[1].record()
-            mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
-            ev[2].record()
-            torch.cuda.synchronize()
-            if r >= 2:
-                t_gather += ev[1].elapsed_time(ev[2]) / reps
-        del os.environ["M3S_REFINE_LDS"]
-        # A/B: the MFMA correlation path (M3S_REFINE_MFMA=1, opt-in): approximate scores on
-        # v_mfma_f32_16x16x32_f16 + exact re-scoring of the candidates within the error bound
-        os.environ["M3S_REFINE_MFMA"] = "1"
-        t_mfma = 0.0
-        for r in range(reps + 2):
-            ev[1].record()
-            mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
-            ev[2].record()
-            torch.cuda.synchronize()
-            if r >= 2:
-                t_mfma += ev[1].elapsed_time(ev[2]) / reps
-        mb.refine_mfma_stats(True)
-        mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
-        resc, cand = mb.refine_mfma_stats(False)
-        del os.environ["M3S_REFINE_MFMA"]
-        # A/B: bound-and-rescore with dot2 approximations (M3S_REFINE_DOT2=1, opt-in)
-        os.environ["M3S_REFINE_DOT2"] = "1"
-        mb.refine_mfma_stats(True)
-        mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
-        resc_d, cand_d = mb.refine_mfma_stats(False)
-        t_exact = 0.0
-        for r in range(reps + 2):
-            ev[1].record()
-            mb.refine_matches(D11, D21, p1, mc["radius"], mc["dilation_max"])
-            ev[2].record()
-            torch.cuda.synchronize()
-            if r >= 2:
-                t_exact += ev[1].elapsed_time(ev[2]) / reps
-        del os.environ["M3S_REFINE_DOT2"]
+        # A/Bs: the measurement-only refine variants (mast3r_slam_backends.variants: the LDS-tiled
+        # kernel, the MFMA correlation with exact re-scoring, the dot2 bound-and-rescore)
+        from mast3r_slam_backends import variants as mv
+
+        def variant_ms(kind):
+            t = 0.0
+            for r in range(reps + 2):
+                ev[1].record()
+                mv.refine_matches_variant(kind, D11, D21, p1, mc["radius"], mc["dilation_max"])
+                ev[2].record()
+                torch.cuda.synchronize()
+                if r >= 2:
+                    t += ev[1].elapsed_time(ev[2]) / reps
+            mv.variant_stats(True)
+            mv.refine_matches_variant(kind, D11, D21, p1, mc["radius"], mc["dilation_max"])
+            return t, mv.variant_stats(False)
+
+        t_gather, _ = variant_ms(mv.LDS)
+        t_mfma, (resc, cand) = variant_ms(mv.MFMA)
+        t_exact, (resc_d, cand_d) = variant_ms(mv.DOT2)
         def wall_ms(fused):
             for _ in range(2):
                 match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=fused)

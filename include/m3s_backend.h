@@ -116,14 +116,15 @@ int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D1
                              int radius, int dilation_max, int contract, int64_t* idx_out,
                              uint8_t* valid_out, void* ws, size_t ws_bytes, void* stream);
 
-/*
- * Diagnostics of the MFMA refine path (env M3S_REFINE_MFMA=1): out2 = {candidates re-scored
- * exactly, in-image candidates} accumulated since the previous call; enable != 0 turns the
- * counting on for later calls (it synchronises the stream after each refine), 0 off.
- */
-void m3s_refine_mfma_stats(int enable, unsigned long long* out2);
+/* The measured-slower refine_matches variants (LDS tile, MFMA correlation, dot2) are not part of
+ * this boundary: include/m3s_variants.h, lib/libm3s_variants.so. */
 
 /* ---------------- Gauss-Newton ---------------- */
+
+/* Diagnostics: with env M3S_GN_DEBUG_FLAGS set (2: silently), a GN call reads back its device
+ * flags at the end (one extra synchronisation); out4 = {early exit, pivot failure, packed stream,
+ * ray-constrained calib accumulate (Xj read as its depth)} of the last such call. */
+void m3s_gn_debug_flags(int* out4);
 
 enum { M3S_GN_POINTS = 0, M3S_GN_RAYS = 1, M3S_GN_CALIB = 2 };
 

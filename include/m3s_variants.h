@@ -1,0 +1,39 @@
+/*
+ * m3s_variants.h -- measurement-only refine_matches kernels (lib/libm3s_variants.so).
+ *
+ * NOT part of the drop-in boundary (m3s_backend.h).  Each variant is bit-exact with the
+ * reference's refine_matches (matching_kernels.cu:25-81) -- the same winner for every pixel --
+ * and was measured slower than the product kernel on the bench data; they
+ * are kept so that bench.py and the tests can A/B them.  Pointers and stream as in m3s_backend.h.
+ */
+#ifndef M3S_VARIANTS_H
+#define M3S_VARIANTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    M3S_REFINE_VARIANT_LDS = 1,  /* candidate box of a 32x16 pixel tile staged in LDS */
+    M3S_REFINE_VARIANT_MFMA = 2, /* approximate scores on v_mfma_f32_16x16x32_f16 + exact re-score */
+    M3S_REFINE_VARIANT_DOT2 = 3  /* approximate scores with v_dot2 + exact re-score */
+};
+
+/* refine_matches (fp16, F = 24, radius 3, N = H*W) with one of the variants; returns M3S_OK or an
+ * error code (message: m3s_variants_last_error()). */
+int m3s_refine_variant_f16(int variant, const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
+                           int64_t* p1_new, int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
+                           int radius, int dilation_max, void* stream);
+/* Counters of the bound-and-rescore variants (MFMA, DOT2) since the last call: out2[0] = exactly
+ * re-scored candidates, out2[1] = in-image candidates; enable != 0 turns counting on. */
+void m3s_refine_variant_stats(int enable, unsigned long long* out2);
+const char* m3s_variants_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* M3S_VARIANTS_H */

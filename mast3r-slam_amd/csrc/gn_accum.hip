@@ -342,6 +342,25 @@ __device__ __forceinline__ void pixel_of(int ind, const AccParams& P, float& ut,
     ut = (float)(ind - (int)q * P.width);
 }
 
+// The packed calib record's match (code & 0x7fffffff = v << 16 | u, AccParams::pack_uv): its
+// flat index v W + u (24-bit multiply-add) and its pixel as floats.
+__device__ __forceinline__ int uv_index(int code, int width) {
+    return (int)__umul24((unsigned)(code >> 16) & 0x7fffu, (unsigned)width) + (code & 0xffff);
+}
+__device__ __forceinline__ void uv_pixel(int code, float& ut, float& vt) {
+    ut = (float)(code & 0xffff);
+    vt = (float)((code >> 16) & 0x7fff);
+}
+// the pack's record code for match index ind (valid or not: bit 31 marks invalid)
+__device__ __forceinline__ int pack_code(int ind, bool ok, const AccParams& P) {
+    int c = ind;
+    if (P.pack_uv) {
+        const unsigned q = (unsigned)(((uint64_t)(unsigned)ind * P.div_m) >> P.div_sh);
+        c = (int)(q << 16) | (ind - (int)q * P.width);
+    }
+    return ok ? c : (int)((unsigned)c | 0x80000000u);
+}
+
 // Half exchanges of two registers (gfx950 v_permlane32_swap / v_permlane16_swap): afterwards
 // a + b holds, in the first half (row pair) of the lanes, a's partial sums and in the second
 // b's -- a reduce-scatter step that costs one swap + one add for two values.
@@ -399,38 +418,75 @@ __device__ __forceinline__ void block_partial(const float* accs, float* __restri
 
 // One pipeline stage of the packed accumulate: the records, Xj and the gathered matched points
 // of 4 consecutive points of one lane.
-template <int MODE, bool RC = false>
+// PK: the packed path's conventions (calib: the matched inverse depth gathered from Zi_b, the
+// record codes are pixels, AccParams::pack_uv); else the unpacked kernel's (raw depth from Xs,
+// codes are flat indices).  NP: consecutive points per lane and step (4, or 2 for the packed
+// path without RC: fewer loads in flight, fewer VGPRs).
+template <int MODE, bool RC = false, bool PK = true, int NP = 4>
 struct AccStage {
-    int4 ka, kb;         // {code, sqrt q} x 2 points each
-    float4 xa, xb, xc;   // Xj of the 4 points (RC: xa = their depths, xb = tu[u..u+3], xc.x = tv[v])
-    float g[4][3];       // gathered matched point (calib: depth only, in g[s][2])
+    static_assert(NP == 4 || NP == 2, "4 or 2 points per step");
+    // the records {code, sqrt q} as scalars: kept as two int4 members, the struct was not split
+    // into registers (a 16-B stack / LDS round trip per step in the ISA)
+    int cd[NP], sb[NP];
+    __device__ __forceinline__ void set(int4 a, int4 b) {
+        cd[0] = a.x; sb[0] = a.y; cd[1] = a.z; sb[1] = a.w;
+        if constexpr (NP == 4) {
+            cd[2] = b.x; sb[2] = b.y; cd[3] = b.z; sb[3] = b.w;
+        }
+    }
+    float xv[3 * NP];    // Xj of the points (RC: xv[0..NP) their depths, xv[NP..2NP) tu[u..], xv[2NP] tv[v])
+    float g[NP][3];      // gathered matched point (calib: depth only, in g[s][2])
     const float* rc_tu = nullptr;  // RC: the ray tables (after Zs)
     const float* rc_tv = nullptr;
     unsigned rc_m = 0;             // RC: k / W by multiply-shift
     int rc_sh = 0, rc_w = 1;
+    int width = 1;                 // PK calib: the image width (record pixel -> flat index)
 
-    // Zi_b (calib): the dense inverse-depth array (packed path), or nullptr to read the raw depth
-    // from Xs (the unpacked path then converts it to the inverse before compute)
     template <int M>
     __device__ __forceinline__ void load(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
                                          const float* __restrict__ Zi_b, int k) {
         if constexpr (RC) {
             // Xj_b = the depth row of keyframe j; the ray tables follow Zs (gn_depth_kernel)
-            xa = *reinterpret_cast<const float4*>(Xj_b + k);
+            // (the NP points share a row: k is a multiple of NP and W of 4)
             const unsigned q = (unsigned)(((uint64_t)(unsigned)k * rc_m) >> rc_sh);
             const int u = k - (int)q * rc_w;
-            xb = *reinterpret_cast<const float4*>(rc_tu + u);
-            xc.x = rc_tv[q];
-        } else {
-            xa = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
-            xb = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
-            xc = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
-        }
-        const int ind[4] = {ka.x & 0x7fffffff, ka.z & 0x7fffffff, kb.x & 0x7fffffff, kb.z & 0x7fffffff};
+            if constexpr (NP == 4) {
+                const float4 za = *reinterpret_cast<const float4*>(Xj_b + k);
+                const float4 ta = *reinterpret_cast<const float4*>(rc_tu + u);
+                const float t[8] = {za.x, za.y, za.z, za.w, ta.x, ta.y, ta.z, ta.w};
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
+                for (int i = 0; i < 8; i++) xv[i] = t[i];
+            } else {
+                const float2 za = *reinterpret_cast<const float2*>(Xj_b + k);
+                const float2 ta = *reinterpret_cast<const float2*>(rc_tu + u);
+                xv[0] = za.x; xv[1] = za.y; xv[2] = ta.x; xv[3] = ta.y;
+            }
+            xv[2 * NP] = rc_tv[q];
+        } else if constexpr (NP == 4) {
+            const float4 a = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3);
+            const float4 b = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 4);
+            const float4 c = *reinterpret_cast<const float4*>(Xj_b + (int64_t)k * 3 + 8);
+            const float t[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int i = 0; i < 12; i++) xv[i] = t[i];
+        } else {
+            const float2 a = *reinterpret_cast<const float2*>(Xj_b + (int64_t)k * 3);
+            const float2 b = *reinterpret_cast<const float2*>(Xj_b + (int64_t)k * 3 + 2);
+            const float2 c = *reinterpret_cast<const float2*>(Xj_b + (int64_t)k * 3 + 4);
+            const float t[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+#pragma unroll
+            for (int i = 0; i < 6; i++) xv[i] = t[i];
+        }
+        int ind[NP];
+#pragma unroll
+        for (int s = 0; s < NP; s++) ind[s] = (M == GN_CALIB && PK) ? uv_index(cd[s], width) : (cd[s] & 0x7fffffff);
+#pragma unroll
+        for (int s = 0; s < NP; s++) {
             if constexpr (M == GN_CALIB) {
-                g[s][2] = Zi_b ? Zi_b[ind[s]] : Xi_b[(int64_t)ind[s] * 3 + 2];
+                if constexpr (PK)
+                    g[s][2] = Zi_b[ind[s]];
+                else
+                    g[s][2] = Xi_b[(int64_t)ind[s] * 3 + 2];
             } else {
                 const float* xp = Xi_b + (int64_t)ind[s] * 3;
                 g[s][0] = xp[0];
@@ -440,32 +496,32 @@ struct AccStage {
         }
     }
 
-    // the 4 points one at a time on scalar accumulators
+    // the points one at a time on scalar accumulators
     template <int M>
     __device__ __forceinline__ void compute(const RelXf& T, const AccParams& P, float* __restrict__ acc) const {
-        const int codes[4] = {ka.x, ka.z, kb.x, kb.z};
-        const int sqb[4] = {ka.y, ka.w, kb.y, kb.w};
-        float xj[12];
+        const int* codes = cd;
+        const int* sqb = sb;
+        float xj[3 * NP];
         if constexpr (RC) {  // x = z * ((u - cx) / fx), y = z * ((v - cy) / fy): constrain_points_to_ray
-            const float z4[4] = {xa.x, xa.y, xa.z, xa.w};
-            const float t4[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
-            for (int s = 0; s < 4; s++) {
-                xj[3 * s] = z4[s] * t4[s];
-                xj[3 * s + 1] = z4[s] * xc.x;
-                xj[3 * s + 2] = z4[s];
+            for (int s = 0; s < NP; s++) {
+                xj[3 * s] = xv[s] * xv[NP + s];
+                xj[3 * s + 1] = xv[s] * xv[2 * NP];
+                xj[3 * s + 2] = xv[s];
             }
         } else {
-            const float t[12] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w, xc.x, xc.y, xc.z, xc.w};
 #pragma unroll
-            for (int q = 0; q < 12; q++) xj[q] = t[q];
+            for (int q = 0; q < 3 * NP; q++) xj[q] = xv[q];
         }
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
+        for (int s = 0; s < NP; s++) {
             PointsIn<float> p;
             if constexpr (M == GN_CALIB) {
                 p.xi0 = p.xi1 = 0.0f;
-                pixel_of(codes[s] & 0x7fffffff, P, p.ut, p.vt);
+                if constexpr (PK)
+                    uv_pixel(codes[s], p.ut, p.vt);
+                else
+                    pixel_of(codes[s] & 0x7fffffff, P, p.ut, p.vt);
             } else {
                 p.xi0 = g[s][0];
                 p.xi1 = g[s][1];
@@ -486,6 +542,20 @@ struct AccStage {
         }
     }
 };
+
+// Points per lane and step of the accumulate (4 or 2), per mode.  Rays / points: 2 -- 74 instead
+// of 112 VGPRs (points 61 / 75), 6 instead of 4 waves per SIMD; cfg4 accumulate 2.08 -> 1.96 ms.
+// Calib: 4, with the ray-constrained path (Xj read as its depth): 0.337 ms on cfg3 against 0.350
+// for the positional path at 2 and 0.358 for the ray-constrained one at 2 (profiles/r03_acc_ab.txt).
+// -DM3S_ACC_PPL=n forces n for every mode (A/B builds).
+template <int MODE>
+__host__ __device__ constexpr int acc_np() {
+#ifdef M3S_ACC_PPL
+    return M3S_ACC_PPL;
+#else
+    return MODE == GN_CALIB ? 4 : 2;
+#endif
+}
 
 // Reads the reference's tensors directly every iteration (used when the call runs < 3
 // iterations, or the inputs are not 16-B aligned).  1-D grid over (edge, chunk) tasks in the
@@ -523,32 +593,46 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
         // two paths produce bitwise identical partials
 #pragma unroll
         for (int q = 0; q < kNacc; q++) accs[q] = 0.0f;
-        for (int k = k0 + 4 * tid; k < k1; k += 4 * kAccThreads) {
-            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + k);
-            const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + k);
-            const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + k + 2);
-            const float4 q4 = *reinterpret_cast<const float4*>(Q + k);
-            const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
-            const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
-            const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
-            const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
-            const float cjs[4] = {cj4.x, cj4.y, cj4.z, cj4.w};
-            int code[4], sqb[4];
+        constexpr int NP = acc_np<MODE>();  // the packed path's points per step: the same sums
+        for (int k = k0 + NP * tid; k < k1; k += NP * kAccThreads) {
+            bool vm[4];
+            int64_t ids[4];
+            float qs[4], cjs[4];
+            if constexpr (NP == 4) {
+                const uchar4 vm4 = *reinterpret_cast<const uchar4*>(valid + k);
+                const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + k);
+                const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + k + 2);
+                const float4 q4 = *reinterpret_cast<const float4*>(Q + k);
+                const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
+                vm[0] = vm4.x != 0; vm[1] = vm4.y != 0; vm[2] = vm4.z != 0; vm[3] = vm4.w != 0;
+                ids[0] = id01.x; ids[1] = id01.y; ids[2] = id23.x; ids[3] = id23.y;
+                qs[0] = q4.x; qs[1] = q4.y; qs[2] = q4.z; qs[3] = q4.w;
+                cjs[0] = cj4.x; cjs[1] = cj4.y; cjs[2] = cj4.z; cjs[3] = cj4.w;
+            } else {
+                const uchar2 vm2 = *reinterpret_cast<const uchar2*>(valid + k);
+                const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + k);
+                const float2 q2 = *reinterpret_cast<const float2*>(Q + k);
+                const float2 cj2 = *reinterpret_cast<const float2*>(Cj_b + k);
+                vm[0] = vm2.x != 0; vm[1] = vm2.y != 0;
+                ids[0] = id01.x; ids[1] = id01.y;
+                qs[0] = q2.x; qs[1] = q2.y;
+                cjs[0] = cj2.x; cjs[1] = cj2.y;
+            }
+            int code[4] = {0, 0, 0, 0}, sqb[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int s = 0; s < 4; s++) {
+            for (int s = 0; s < NP; s++) {
                 const int ind = match_index(ids[s], vm[s], HW);
                 const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) &&
                                 (cjs[s] > P.C_thresh);
                 code[s] = ok ? ind : (int)((unsigned)ind | 0x80000000u);
                 sqb[s] = __float_as_int(vsqrt(qs[s]));
             }
-            AccStage<MODE> st;
-            st.ka = int4{code[0], sqb[0], code[1], sqb[1]};
-            st.kb = int4{code[2], sqb[2], code[3], sqb[3]};
+            AccStage<MODE, false, false, NP> st;
+            st.set(int4{code[0], sqb[0], code[1], sqb[1]}, int4{code[2], sqb[2], code[3], sqb[3]});
             st.template load<MODE>(Xj_b, Xi_b, nullptr, k);  // calib: the depth from Xs ...
             if constexpr (MODE == GN_CALIB) {
 #pragma unroll
-                for (int s = 0; s < 4; s++)  // ... as the inverse depth gn_depth_kernel tabulates
+                for (int s = 0; s < NP; s++)  // ... as the inverse depth gn_depth_kernel tabulates
                     st.g[s][2] = st.g[s][2] > P.z_eps ? vrcp(st.g[s][2]) : __builtin_nanf("");
             }
             st.template compute<MODE>(T, P, accs);
@@ -617,7 +701,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
     for (int s = 0; s < 4; s++) {
         const int ind = match_index(ids[s], vm[s], HW);
         const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (cjs[s] > P.C_thresh);
-        code[s] = ok ? ind : (int)((unsigned)ind | 0x80000000u);
+        code[s] = pack_code(ind, ok, P);
         sqb[s] = __float_as_int(vsqrt(qs[s]));
     }
     int4* dst = pack + (ebase + k) / 2;
@@ -690,7 +774,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
             for (int s = 0; s < 4; s++) {
                 const int ind = match_index(ids[s], vm[s], HW);
                 const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (cjs[s] > P.C_thresh);
-                code[s] = ok ? ind : (int)((unsigned)ind | 0x80000000u);
+                code[s] = pack_code(ind, ok, P);
                 sqb[s] = __float_as_int(vsqrt(qs[s]));
                 const float* xi = Xi_b + (int64_t)ind * 3;
                 const bool fin = finite3(&xj[3 * s]) &&
@@ -736,7 +820,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
         const int kd = s_dead;  // pad > 0 implies a dead point exists (chunks are multiples of 4)
         const int64_t id = idx_e[kd];
         const int ind = match_index(id, valid_e[kd] != 0, HW);
-        pk[obase + running + tid] = make_int2((int)((unsigned)ind | 0x80000000u), __float_as_int(vsqrt(Q_e[kd])));
+        pk[obase + running + tid] = make_int2(pack_code(ind, false, P), __float_as_int(vsqrt(Q_e[kd])));
         float* o = px + (obase + running + tid) * 3;
         o[0] = Xj_b[(int64_t)kd * 3];
         o[1] = Xj_b[(int64_t)kd * 3 + 1];
@@ -780,16 +864,17 @@ __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__
     if (!ray) flags[kFlagNotRay] = 1;  // benign race: every writer stores 1
 }
 
-// One lane's steps of the packed accumulate (4 points per step); the records of the next step
+// One lane's steps of the packed accumulate (NP points per step); the records of the next step
 // are loaded one step ahead.  RC: Xj_b is keyframe j's depth row and x, y come from the ray
 // tables that follow Zs (total = N * HW floats of depth).
-template <int MODE, bool RC>
+template <int MODE, bool RC, int NP = 4>
 __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
                                             const float* __restrict__ Zi_b, const int4* __restrict__ pk_b,
                                             int k0, int k1, const RelXf& T, const AccParams& P,
                                             const float* __restrict__ Zs, float* __restrict__ acc) {
-    constexpr int S = 4 * kAccThreads;
-    AccStage<MODE, RC> cur;
+    constexpr int S = NP * kAccThreads;
+    AccStage<MODE, RC, true, NP> cur;
+    cur.width = P.width;
     if constexpr (RC) {
         cur.rc_tu = Zs + (int64_t)P.nkf * P.HW;
         cur.rc_tv = cur.rc_tu + P.width;
@@ -797,44 +882,42 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
         cur.rc_sh = P.div_sh;
         cur.rc_w = P.width;
     }
+    // the records of NP points: one int4 per two
+    auto records = [&](int kk, int4& a, int4& b) {
+        a = pk_b[kk / 2];
+        if constexpr (NP == 4) b = pk_b[kk / 2 + 1];
+    };
     int4 na = int4{0, 0, 0, 0}, nb = int4{0, 0, 0, 0};
-    int k = k0 + 4 * threadIdx.x;
-    if (k < k1) {
-        na = pk_b[k / 2];
-        nb = pk_b[k / 2 + 1];
-    }
+    int k = k0 + NP * threadIdx.x;
+    if (k < k1) records(k, na, nb);
     for (; k < k1; k += S) {
 #if M3S_ACC_DIAG == 1
         // diagnostics: compute only (the first step's data, re-used: no memory after it)
-        if (k == k0 + 4 * (int)threadIdx.x) {
-            cur.ka = na;
-            cur.kb = nb;
+        if (k == k0 + NP * (int)threadIdx.x) {
+            cur.set(na, nb);
             cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
         }
         cur.template compute<MODE>(T, P, acc);
         __builtin_amdgcn_sched_barrier(0);
         continue;
 #elif M3S_ACC_DIAG == 2
-        // diagnostics: memory only (the loads of every step, a trivial use of each value)
-        cur.ka = na;
-        cur.kb = nb;
-        if (k + S < k1) {
-            na = pk_b[(k + S) / 2];
-            nb = pk_b[(k + S) / 2 + 1];
-        }
+        // diagnostics: memory only -- the first step computed (so the system stays solvable and
+        // the iterations keep running), then every step's loads with each value merely consumed
+        cur.set(na, nb);
+        if (k + S < k1) records(k + S, na, nb);
         cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
-        acc[0] += __int_as_float(cur.ka.x) + __int_as_float(cur.ka.z) + __int_as_float(cur.kb.x) +
-                  __int_as_float(cur.kb.z) + cur.xa.x + cur.xa.y + cur.xa.z + cur.xa.w + cur.xb.x + cur.xb.y +
-                  cur.xb.z + cur.xb.w + cur.xc.x + cur.xc.y + cur.xc.z + cur.xc.w + cur.g[0][2] + cur.g[1][2] +
-                  cur.g[2][2] + cur.g[3][2] + cur.g[0][0] + cur.g[1][0] + cur.g[2][0] + cur.g[3][0];
+        if (k == k0 + NP * (int)threadIdx.x) {
+            cur.template compute<MODE>(T, P, acc);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 3 * NP; q++) asm volatile("" ::"v"(cur.xv[q]));
+#pragma unroll
+            for (int q = 0; q < NP; q++) asm volatile("" ::"v"(cur.g[q][2]), "v"(cur.g[q][0]), "v"(cur.cd[q]), "v"(cur.sb[q]));
+        }
         continue;
 #endif
-        cur.ka = na;
-        cur.kb = nb;
-        if (k + S < k1) {
-            na = pk_b[(k + S) / 2];
-            nb = pk_b[(k + S) / 2 + 1];
-        }
+        cur.set(na, nb);
+        if (k + S < k1) records(k + S, na, nb);
         cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
         cur.template compute<MODE>(T, P, acc);
     }
@@ -849,7 +932,7 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
 #ifndef M3S_ACC_WAVES
 #define M3S_ACC_WAVES 1
 #endif
-template <int MODE, bool COMPACT>
+template <int MODE, bool COMPACT, bool RCOK = false>
 __global__ __launch_bounds__(kAccThreads) __attribute__((amdgpu_waves_per_eu(M3S_ACC_WAVES)))
 void gn_accum_packed_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Zs,
@@ -884,16 +967,15 @@ void gn_accum_packed_kernel(
     // two-deep: the gathers + Xj of step s+1 and the records of step s+2 are in flight while
     // step s is computed
     AccStage<MODE> cur, nxt;
+    cur.width = nxt.width = P.width;
     int4 pa2 = int4{0, 0, 0, 0}, pb2 = int4{0, 0, 0, 0};
     int k = k0 + 4 * tid;
     if (k < k1) {
-        cur.ka = pk_b[k / 2];
-        cur.kb = pk_b[k / 2 + 1];
+        cur.set(pk_b[k / 2], pk_b[k / 2 + 1]);
         cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
     }
     if (k + S < k1) {
-        nxt.ka = pk_b[(k + S) / 2];
-        nxt.kb = pk_b[(k + S) / 2 + 1];
+        nxt.set(pk_b[(k + S) / 2], pk_b[(k + S) / 2 + 1]);
     }
     for (; k < k1; k += S) {
         if (k + S < k1) nxt.template load<MODE>(Xj_b, Xi_b, Zi_b, k + S);
@@ -903,20 +985,19 @@ void gn_accum_packed_kernel(
         }
         cur.template compute<MODE>(T, P, acc);
         cur = nxt;
-        nxt.ka = pa2;
-        nxt.kb = pb2;
+        nxt.set(pa2, pb2);
     }
 #else
     if constexpr (COMPACT) {
         // compacted stream: the chunk's live points, Xj copied alongside the records
         const int64_t cb = ((int64_t)e * P.nchunks + c) * P.chunk;
-        accum_steps<MODE, false>(px + cb * 3, Xi_b, Zi_b, pack + cb / 2, 0, pcnt[(int64_t)e * P.nchunks + c], T, P,
+        accum_steps<MODE, false, acc_np<MODE>()>(px + cb * 3, Xi_b, Zi_b, pack + cb / 2, 0, pcnt[(int64_t)e * P.nchunks + c], T, P,
                                  Zs, acc);
-    } else if (MODE == GN_CALIB && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
+    } else if (RCOK && MODE == GN_CALIB && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
         // calib with ray-constrained keyframe points (gn_depth_kernel's check): Xj from its depth
-        accum_steps<MODE, true>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
+        accum_steps<MODE, true, acc_np<MODE>()>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
     else
-        accum_steps<MODE, false>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
+        accum_steps<MODE, false, acc_np<MODE>()>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
 #endif
     block_partial(acc, partials + ((int64_t)e * P.nchunks + c) * kNaccPad, ecnt != nullptr);
     if (ecnt != nullptr) {
@@ -990,17 +1071,21 @@ hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float*
                                const int* jj_loc, const int4* pack, const AccParams& P,
                                const int4* sched, float* partials, const int* flags, const float* px,
                                const int* pcnt, int* ecnt, double* edgeblk) {
-#define M3S_ACCP(MODE, CP)                                                                       \
-    hipLaunchKernelGGL((gn_accum_packed_kernel<MODE, CP>), grid, dim3(kAccThreads), 0, st, Twc, Xs, Zs, \
+#define M3S_ACCP(MODE, CP, RC)                                                                       \
+    hipLaunchKernelGGL((gn_accum_packed_kernel<MODE, CP, RC>), grid, dim3(kAccThreads), 0, st, Twc, Xs, Zs, \
                        ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt, edgeblk)
+#define M3S_ACCP2(MODE, CP) M3S_ACCP(MODE, CP, false)
     const bool cp = px != nullptr;
     if (mode == GN_RAYS) {
-        if (cp) M3S_ACCP(GN_RAYS, true); else M3S_ACCP(GN_RAYS, false);
+        if (cp) M3S_ACCP2(GN_RAYS, true); else M3S_ACCP2(GN_RAYS, false);
     } else if (mode == GN_CALIB) {
-        if (cp) M3S_ACCP(GN_CALIB, true); else M3S_ACCP(GN_CALIB, false);
+        if (cp) M3S_ACCP2(GN_CALIB, true);
+        else if (P.raycheck) M3S_ACCP(GN_CALIB, false, true);
+        else M3S_ACCP2(GN_CALIB, false);
     } else {
-        if (cp) M3S_ACCP(GN_POINTS, true); else M3S_ACCP(GN_POINTS, false);
+        if (cp) M3S_ACCP2(GN_POINTS, true); else M3S_ACCP2(GN_POINTS, false);
     }
+#undef M3S_ACCP2
 #undef M3S_ACCP
     return hipGetLastError();
 }

@@ -62,6 +62,8 @@ struct Prof {
 Prof g_prof;
 }  // namespace
 
+int g_dbg_flags[4] = {0, 0, 0, 0};  // done, fail, packed, ray-constrained accumulate (last call)
+
 void set_error(const char* fmt, ...) {
     char buf[1024];
     va_list ap;
@@ -933,6 +935,14 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     // (cfg3) / 13 % (cfg4), and the compacting pack (Xj copies, finiteness gathers) costs more
     // per call than the 10 iterations save
     c.compact = c.packed && env_int("M3S_GN_COMPACT", 0) != 0;
+    // calib: the packed records carry the match as its pixel (v << 16 | u), decoded with a mask, a
+    // bit-field extract and one 24-bit multiply-add instead of a 64-bit division by W per point
+    if (a.mode == M3S_GN_CALIB && (a.width >= 65536 || a.height >= 32768)) c.packed = c.compact = false;
+    P.pack_uv = c.packed && a.mode == M3S_GN_CALIB;
+    // calib: the packed accumulate reads Xj as its 4-B depth when gn_depth_kernel finds every point
+    // on its pixel's ray bit for bit (solve_GN_calib's constrain_points_to_ray; bitwise the same
+    // result): 16 instead of 24 B per point-edge.  M3S_GN_RAYCHECK=0 keeps the positional path only.
+    P.raycheck = c.packed && !c.compact && a.mode == M3S_GN_CALIB && env_int("M3S_GN_RAYCHECK", 1) != 0;
 
     c.ref_order = gn_order(a) == M3S_GN_ORDER_REFERENCE;
     if (c.ref_order) {
@@ -967,11 +977,7 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     char* h = stagings().ws.get(hi - lo + sizeof(int) * nslot);
     M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
     std::memset(h, 0, L.ii_loc - lo);  // flags
-    // M3S_GN_RAYCHECK=1: let the packed calib accumulate take the ray-constrained path
-    // (Xj read as its depth, 16 instead of 24 B per point-edge) when every point passes the
-    // check.  Off by default: bitwise the same result, but only ~3 % faster on cfg3 -- the
-    // kernel is latency-bound, not HBM-bound.
-    if (env_int("M3S_GN_RAYCHECK", 0) == 0) reinterpret_cast<int*>(h)[kFlagNotRay] = 1;
+    if (!c.P.raycheck) reinterpret_cast<int*>(h)[kFlagNotRay] = 1;
     auto put = [&](size_t off, const std::vector<int>& v) {
         if (!v.empty()) std::memcpy(h + (off - lo), v.data(), sizeof(int) * v.size());
     };
@@ -1332,12 +1338,18 @@ int run(const m3s_gn_args& a) {
             return M3S_ERR_TIMEOUT;
         }
     }
-    if (env_int("M3S_GN_DEBUG_FLAGS", 0)) {  // diagnostics: the device flags after the call
+    if (const int dbg = env_int("M3S_GN_DEBUG_FLAGS", 0)) {  // diagnostics: the device flags after the call
         int hf[kNumFlags];
         M3S_HIP_CHECK(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, c.st));
         M3S_HIP_CHECK(hipStreamSynchronize(c.st));
-        fprintf(stderr, "gn flags: done %d fail %d not_ray %d timeout %d packed %d\n", hf[kFlagDone],
-                hf[kFlagFail], hf[kFlagNotRay], hf[kFlagTimeout], (int)c.packed);
+        // m3s_gn_debug_flags: which accumulate path the call took (bench.py prices its bytes)
+        g_dbg_flags[0] = hf[kFlagDone];
+        g_dbg_flags[1] = hf[kFlagFail];
+        g_dbg_flags[2] = c.packed ? 1 : 0;
+        g_dbg_flags[3] = (c.packed && c.P.raycheck && hf[kFlagNotRay] == 0) ? 1 : 0;
+        if (dbg != 2)
+            fprintf(stderr, "gn flags: done %d fail %d not_ray %d timeout %d packed %d\n", hf[kFlagDone],
+                    hf[kFlagFail], hf[kFlagNotRay], hf[kFlagTimeout], (int)c.packed);
     }
     return M3S_OK;
 }
@@ -1348,6 +1360,10 @@ int run(const m3s_gn_args& a) {
 using namespace m3s;
 
 extern "C" const char* m3s_last_error(void) { return m3s::get_error(); }
+
+extern "C" void m3s_gn_debug_flags(int* out4) {
+    for (int k = 0; k < 4; k++) out4[k] = m3s::g_dbg_flags[k];
+}
 
 extern "C" const char* m3s_version(void) { return "m3s 0.1.0 gfx950"; }
 

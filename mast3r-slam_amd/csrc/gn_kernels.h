@@ -62,6 +62,9 @@ struct AccParams {
     int chunk;    // points per workgroup (multiple of 4)
     int nchunks;  // chunks per directed edge
     int nkf;      // keyframes (rows of Xs / Zs)
+    int pack_uv;  // packed calib stream: code = v << 16 | u of the match (W < 2^16, H < 2^15)
+    int raycheck; // M3S_GN_RAYCHECK=1: launch the packed calib kernel that can take the
+                  // ray-constrained path (a separate instantiation: its VGPRs do not burden the default)
 };
 
 // Reference-order ("parity") accumulate, gn_refacc.hip

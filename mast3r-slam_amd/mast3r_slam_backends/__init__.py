@@ -63,8 +63,6 @@ lib.m3s_iter_proj_ex.argtypes = [_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _i, _v
 lib.m3s_refine_matches_f16.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_refine_matches_f32.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
 lib.m3s_refine_matches_f64.argtypes = [_vp] * 4 + [_c_int64] * 5 + [_i, _i, _vp]
-lib.m3s_refine_mfma_stats.argtypes = [_i, _vp]
-lib.m3s_refine_mfma_stats.restype = None
 lib.m3s_match_workspace_bytes.argtypes = [_c_int64] * 4
 lib.m3s_match_workspace_bytes.restype = ctypes.c_size_t
 lib.m3s_match_iterative_proj.argtypes = ([_vp] * 5 + [_c_int64] * 4 + [_i, _f, _f, _f, _i, _i, _i]
@@ -285,14 +283,6 @@ def refine_matches(D11, D21, p1, window_size, dilation_max):
         )
     _raise(rc, "refine_matches")
     return [p1_new]
-
-
-def refine_mfma_stats(enable=True):
-    """Counters of the MFMA refine path (M3S_REFINE_MFMA=1): (re-scored, in-image candidates) since
-    the previous call; ``enable`` switches the counting for later calls."""
-    out = (ctypes.c_ulonglong * 2)()
-    lib.m3s_refine_mfma_stats(int(bool(enable)), ctypes.cast(out, ctypes.c_void_p))
-    return int(out[0]), int(out[1])
 
 
 def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init, max_iter, lambda_init, cost_thresh,

@@ -80,31 +80,36 @@ def test_iter_proj_empty(backend):
     assert p_new.shape == (0, 64, 2) and conv.shape == (0, 64)
 
 
-def _refine_both(backend, oracle, D11, D21, p1, radius=3, dmax=5):
-    (out_g,) = backend.refine_matches(D11.cuda(), D21.cuda(), p1.cuda(), radius, dmax)
+def _refine_both(backend, oracle, D11, D21, p1, radius=3, dmax=5, variant=None):
+    """The product op (variant None) or a measurement-only variant (mast3r_slam_backends.variants)
+    against the oracle."""
+    if variant is None:
+        (out_g,) = backend.refine_matches(D11.cuda(), D21.cuda(), p1.cuda(), radius, dmax)
+    else:
+        from mast3r_slam_backends import variants
+        (out_g,) = variants.refine_matches_variant(variant, D11.cuda(), D21.cuda(), p1.cuda(), radius, dmax)
     out_o = oracle.refine_matches(D11.numpy(), D21.numpy(), p1.numpy(), radius, dmax)
     return out_g.cpu().numpy(), out_o
 
 
-@pytest.mark.parametrize("dot2", ["0", "1"])
+@pytest.mark.parametrize("dot2", [False, True])
 @pytest.mark.parametrize("B,H,W", [(1, 384, 512), (2, 24, 32)])
-def test_refine_matches_f16_bit_exact(backend, oracle, monkeypatch, B, H, W, dot2):
-    """Default fp16 path (every candidate's fp16 chain) and M3S_REFINE_DOT2=1 (bound-and-rescore:
+def test_refine_matches_f16_bit_exact(backend, oracle, B, H, W, dot2):
+    """Default fp16 path (every candidate's fp16 chain) and the DOT2 variant (bound-and-rescore:
     dot2 approximations, exact fp16 chains for the shortlist): both bit-exact."""
-    monkeypatch.setenv("M3S_REFINE_DOT2", dot2)
     mp = synth.make_match_pair(B=B, H=H, W=W, seed=11)
     p1 = torch.stack((mp.idx_init % W, mp.idx_init // W), -1).long()
     D11 = mp.D11.half()
     D21 = mp.D21.reshape(B, H * W, -1).half()
-    out_g, out_o = _refine_both(backend, oracle, D11, D21, p1)
+    out_g, out_o = _refine_both(backend, oracle, D11, D21, p1, variant=3 if dot2 else None)
     assert out_g.dtype == np.int64
     assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
 
 
 @pytest.mark.parametrize("scatter", [0, 3, 40, 10**6])
-def test_refine_lds_tile_and_fallback(backend, oracle, monkeypatch, scatter):
-    """The LDS-tiled kernel (M3S_REFINE_LDS=1) against the oracle and against the default
-    candidate-gather kernel (M3S_REFINE_LDS=0), bitwise.  ``scatter`` spreads the starting
+def test_refine_lds_tile_and_fallback(backend, oracle, scatter):
+    """The LDS-tiled variant against the oracle and against the product candidate-gather
+    kernel, bitwise.  ``scatter`` spreads the starting
     matches: 0/3 px keeps every tile's candidate box in LDS; 40 px makes the large-dilation
     boxes exceed the LDS budget (those levels gather from global memory); 10**6 puts most
     starts far outside the image (clipped windows, many empty)."""
@@ -116,9 +121,7 @@ def test_refine_lds_tile_and_fallback(backend, oracle, monkeypatch, scatter):
         p1 = p1 + torch.randint(-scatter, scatter + 1, p1.shape, generator=g)
     D11 = mp.D11.half()
     D21 = mp.D21.reshape(B, H * W, -1).half()
-    monkeypatch.setenv("M3S_REFINE_LDS", "1")
-    out_l, out_o = _refine_both(backend, oracle, D11, D21, p1)
-    monkeypatch.setenv("M3S_REFINE_LDS", "0")
+    out_l, out_o = _refine_both(backend, oracle, D11, D21, p1, variant=1)
     (out_gth,) = backend.refine_matches(D11.cuda(), D21.cuda(), p1.cuda(), 3, 5)
     assert np.array_equal(out_l, out_o), f"{(out_l != out_o).any(-1).sum()} matches differ"
     assert np.array_equal(out_l, out_gth.cpu().numpy())
@@ -248,8 +251,8 @@ def test_fused_pipeline_matches_oracle_pipeline(backend, oracle, B, H, W, radius
 
 
 @pytest.mark.parametrize("warm", [False, True])
-def test_refine_mfma_path_bit_exact(backend, oracle, monkeypatch, warm):
-    """The MFMA correlation path (M3S_REFINE_MFMA=1: approximate scores on
+def test_refine_mfma_path_bit_exact(backend, oracle, warm):
+    """The MFMA correlation variant (approximate scores on
     v_mfma_f32_16x16x32_f16, exact c10::Half re-scoring of every candidate within the error
     bound of the best) gives the oracle's indices bit for bit at 512x384, and re-scores only a
     fraction of the candidates."""
@@ -259,20 +262,19 @@ def test_refine_mfma_path_bit_exact(backend, oracle, monkeypatch, warm):
     p1 = torch.from_numpy(p).long()
     D11 = mp.D11.half()
     D21 = mp.D21.view(1, -1, 24).half()
-    monkeypatch.setenv("M3S_REFINE_MFMA", "1")
-    backend.refine_mfma_stats(True)
-    out_g, out_o = _refine_both(backend, oracle, D11, D21, p1, 3, 5)
-    resc, total = backend.refine_mfma_stats(False)
+    from mast3r_slam_backends import variants
+    variants.variant_stats(True)
+    out_g, out_o = _refine_both(backend, oracle, D11, D21, p1, 3, 5, variant=variants.MFMA)
+    resc, total = variants.variant_stats(False)
     assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
     assert 0 < resc < total, (resc, total)
 
 
-@pytest.mark.parametrize("path", ["M3S_REFINE_MFMA", "M3S_REFINE_DOT2"])
-def test_refine_mfma_path_edge_cases(backend, oracle, monkeypatch, path):
+@pytest.mark.parametrize("path", [2, 3])  # variants.MFMA, variants.DOT2
+def test_refine_mfma_path_edge_cases(backend, oracle, path):
     """Ties everywhere, all-negative scores, out-of-image starts, huge values (bound beyond fp16
     range: every candidate re-scored) and NaN descriptors, all bit-exact on the MFMA and the dot2
     bound-and-rescore paths."""
-    monkeypatch.setenv(path, "1")
     g = torch.Generator().manual_seed(4)
     B, H, W, F = 1, 40, 36, 24
     p1 = torch.stack((torch.randint(-5, W + 5, (B, H * W), generator=g),
@@ -287,5 +289,5 @@ def test_refine_mfma_path_edge_cases(backend, oracle, monkeypatch, path):
     nan11[0, 7, 9, 3] = float("nan")
     cases["nan"] = (nan11, torch.randn((B, H * W, F), generator=g))
     for name, (D11, D21) in cases.items():
-        out_g, out_o = _refine_both(backend, oracle, D11.half(), D21.half(), p1, 3, 5)
+        out_g, out_o = _refine_both(backend, oracle, D11.half(), D21.half(), p1, 3, 5, variant=path)
         assert np.array_equal(out_g, out_o), name

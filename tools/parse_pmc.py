@@ -39,8 +39,14 @@ fetch_kb = sum(bf[name]) / len(bf[name])
 write_kb = sum(bw[name]) / len(bw[name])
 read_b = fetch_kb * 1024 * k_fetch
 write_b = write_kb * 1024 * k_write
+# the accumulate path the profiled bench run took (its JSON line's roofline.stream)
+stream = None
+for line in open(os.path.join(root, "bench_FETCH_SIZE.log")):
+    if line.startswith("{"):
+        stream = json.loads(line).get("roofline", {}).get("stream")
 res = {
     "config": cfg,
+    "stream": stream,
     "n_gpus": 1,
     "kernel": name,
     "packed": "packed" in name,

@@ -19,4 +19,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
     rc=$?; echo "pmc $c calib rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 python tools/pmc_filter.py $OUT
+python tools/parse_pmc.py $OUT gpurun_out/accum_traffic_$CFG.json $CFG
 exit 0

@@ -1,5 +1,6 @@
 """Runs refine_matches at 512x384 (B=8, base.yaml radius 3 / dilation 5) a few times, for PMC
-profiling of the matching kernels (tools/pmc_refine.sh).  M3S_REFINE_LDS selects the kernel."""
+profiling of the matching kernels (tools/pmc_refine.sh).  VARIANT=1|2|3 runs a measurement-only
+variant (mast3r_slam_backends.variants) instead of the product kernel."""
 import os
 import sys
 
@@ -17,7 +18,12 @@ W = 512
 p1 = torch.stack((mp.idx_init % W, mp.idx_init // W), -1).long()
 D11 = mp.D11.half()
 D21 = mp.D21.view(B, 384 * 512, -1).half()
+kind = int(os.environ.get("VARIANT", "0"))
 for _ in range(int(os.environ.get("REPS", "5"))):
-    mb.refine_matches(D11, D21, p1, 3, 5)
+    if kind:
+        from mast3r_slam_backends import variants
+        variants.refine_matches_variant(kind, D11, D21, p1, 3, 5)
+    else:
+        mb.refine_matches(D11, D21, p1, 3, 5)
 torch.cuda.synchronize()
 print("done")
