@@ -324,6 +324,8 @@ def matching_bench(dev, reps=10):
         t_gather, _ = variant_ms(mv.LDS)
         t_mfma, (resc, cand) = variant_ms(mv.MFMA)
         t_exact, (resc_d, cand_d) = variant_ms(mv.DOT2)
+        t_lat, (resc_l, cand_l) = variant_ms(mv.LATTICE)
+        n_mfma_l = mv.mfma_issued()
         def wall_ms(fused):
             for _ in range(2):
                 match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=fused)
@@ -359,6 +361,17 @@ def matching_bench(dev, reps=10):
                 "useful_TFLOPs": 245 * 48 * npx / (t_mfma * 1e-3) / 1e12,
                 "mfma_util_vs_2500TF": 245 * 16384 / 16 * npx / (t_mfma * 1e-3) / 2.5e15,
                 "useful_util_vs_2500TF": 245 * 48 * npx / (t_mfma * 1e-3) / 2.5e15,
+            },
+            "refine_mfma_lattice": {
+                # MFMA over per-level lattice buckets (refine_variants.hip): issued = the kernel's
+                # count of 16x16x32 f16 MFMAs (16384 FLOP each); useful = the reference's MACs
+                "ms": t_lat,
+                "rescored_fraction": resc_l / max(cand_l, 1),
+                "mfma_issued": n_mfma_l,
+                "mfma_issued_TFLOPs": n_mfma_l * 16384 / (t_lat * 1e-3) / 1e12,
+                "mfma_util_vs_2500TF": n_mfma_l * 16384 / (t_lat * 1e-3) / 2.5e15,
+                "useful_TFLOPs": 245 * 48 * npx / (t_lat * 1e-3) / 1e12,
+                "useful_util_vs_2500TF": 245 * 48 * npx / (t_lat * 1e-3) / 2.5e15,
             },
             "match_iterative_proj_ms": t_glue,
             "match_iterative_proj_torch_glue_ms": t_torch_glue,

@@ -19,7 +19,9 @@ extern "C" {
 enum {
     M3S_REFINE_VARIANT_LDS = 1,  /* candidate box of a 32x16 pixel tile staged in LDS */
     M3S_REFINE_VARIANT_MFMA = 2, /* approximate scores on v_mfma_f32_16x16x32_f16 + exact re-score */
-    M3S_REFINE_VARIANT_DOT2 = 3  /* approximate scores with v_dot2 + exact re-score */
+    M3S_REFINE_VARIANT_DOT2 = 3, /* approximate scores with v_dot2 + exact re-score */
+    M3S_REFINE_VARIANT_LATTICE = 4 /* MFMA over per-level lattice buckets of the tile + exact re-score
+                                      (dilation_max <= 5) */
 };
 
 /* refine_matches (fp16, F = 24, radius 3, N = H*W) with one of the variants; returns M3S_OK or an
@@ -27,9 +29,10 @@ enum {
 int m3s_refine_variant_f16(int variant, const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
                            int64_t* p1_new, int64_t B, int64_t H, int64_t W, int64_t N, int64_t F,
                            int radius, int dilation_max, void* stream);
-/* Counters of the bound-and-rescore variants (MFMA, DOT2) since the last call: out2[0] = exactly
- * re-scored candidates, out2[1] = in-image candidates; enable != 0 turns counting on. */
-void m3s_refine_variant_stats(int enable, unsigned long long* out2);
+/* Counters of the bound-and-rescore variants (MFMA, DOT2, LATTICE) since the last call: out3[0] =
+ * exactly re-scored candidates, out3[1] = in-image candidates, out3[2] = 16x16x32 MFMAs issued by
+ * the lattice kernel; enable != 0 turns counting on. */
+void m3s_refine_variant_stats(int enable, unsigned long long* out3);
 const char* m3s_variants_last_error(void);
 
 #ifdef __cplusplus

@@ -98,27 +98,36 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
 
     float lambda = lambda_init;
     uint8_t conv = 0;
-    for (int it = 0; it < max_iter; it++) {
+    // The state at (u, v): residual e, cost, and the normal-equation terms without lambda.  A
+    // rejected step leaves (u, v) and so all of it unchanged, and an accepted one moves to the
+    // trial point whose ray channels, residual and cost were just evaluated (the same operations
+    // on the same texels, so the same values) -- each iteration gathers the trial point's 3 ray
+    // channels and, after an accepted step, its 6 gradient channels: 12 or 36 dwords per pixel
+    // and iteration instead of the reference's 48, bitwise the same arithmetic.
+    float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, cost = 0.0f;
+    float A00b = 0.0f, A01 = 0.0f, A11b = 0.0f, b0 = 0.0f, b1 = 0.0f;
+    auto normal_terms = [&](const Bilin& bb) {  // :202-210 from the gradients at bb and e
+        const float gx0 = interp<CM>(bb, 3), gx1 = interp<CM>(bb, 4), gx2 = interp<CM>(bb, 5);
+        const float gy0 = interp<CM>(bb, 6), gy1 = interp<CM>(bb, 7), gy2 = interp<CM>(bb, 8);
+        A00b = cdot3<CM>(gx0, gx0, gx1, gx1, gx2, gx2);
+        A01 = cdot3<CM>(gx0, gy0, gx1, gy1, gx2, gy2);
+        A11b = cdot3<CM>(gy0, gy0, gy1, gy1, gy2, gy2);
+        b0 = -cdot3<CM>(e0, gx0, e1, gx1, e2, gx2);
+        b1 = -cdot3<CM>(e0, gy0, e1, gy1, e2, gy2);
+    };
+    if (max_iter > 0) {
         const Bilin bl = make_bilin(img, W, u, v);
         const float r0 = interp<CM>(bl, 0), r1 = interp<CM>(bl, 1), r2 = interp<CM>(bl, 2);
-        const float gx0 = interp<CM>(bl, 3), gx1 = interp<CM>(bl, 4), gx2 = interp<CM>(bl, 5);
-        const float gy0 = interp<CM>(bl, 6), gy1 = interp<CM>(bl, 7), gy2 = interp<CM>(bl, 8);
-
         // :186-198: r *= 1/|r| then err = r - pts (the scaled ray feeds only the subtraction: fused)
         const float r_norm_inv = inv_f(sqrtf(cdot3<CM>(r0, r0, r1, r1, r2, r2)));
-        const float e0 = cmad<CM>(r0, r_norm_inv, -px), e1 = cmad<CM>(r1, r_norm_inv, -py),
-                    e2 = cmad<CM>(r2, r_norm_inv, -pz);
-        const float cost = cdot3<CM>(e0, e0, e1, e1, e2, e2);
-
-        // :202-210
-        float A00 = cdot3<CM>(gx0, gx0, gx1, gx1, gx2, gx2);
-        const float A01 = cdot3<CM>(gx0, gy0, gx1, gy1, gx2, gy2);
-        float A11 = cdot3<CM>(gy0, gy0, gy1, gy1, gy2, gy2);
-        const float b0 = -cdot3<CM>(e0, gx0, e1, gx1, e2, gx2);
-        const float b1 = -cdot3<CM>(e0, gy0, e1, gy1, e2, gy2);
-        A00 += lambda;
-        A11 += lambda;
-
+        e0 = cmad<CM>(r0, r_norm_inv, -px);
+        e1 = cmad<CM>(r1, r_norm_inv, -py);
+        e2 = cmad<CM>(r2, r_norm_inv, -pz);
+        cost = cdot3<CM>(e0, e0, e1, e1, e2, e2);
+        normal_terms(bl);
+    }
+    for (int it = 0; it < max_iter; it++) {
+        const float A00 = A00b + lambda, A11 = A11b + lambda;
         // :213-219: u + det_inv * (...) is a fused multiply-add under nvcc
         const float det_inv = inv_f(cmm<CM>(A00, A11, -A01, A01));
         const float u_new = clamp_ref(cmad<CM>(det_inv, cmm<CM>(A11, b0, -A01, b1), u), 1.0f, umax);
@@ -137,6 +146,11 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
             v = v_new;
             lambda = (float)((double)lambda * 0.1);  // `lambda *= 0.1` is a double multiply
             conv = new_cost < cost_thresh;
+            e0 = f0;
+            e1 = f1;
+            e2 = f2;
+            cost = new_cost;
+            if (it + 1 < max_iter) normal_terms(bn);
         } else {
             lambda = (float)((double)lambda * 10.0);
             conv = cost < cost_thresh;
@@ -144,145 +158,6 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
     }
     *reinterpret_cast<float2*>(p_new + g * 2) = make_float2(u, v);
     converged[g] = conv;
-}
-
-// ---------------------------------------------------------------------------------
-// iter_proj on the fused op's ray image: texels of 3 float4 {ray, 0 | d/du, 0 | d/dv, 0} (48 B,
-// 16-B aligned: a bilinear tap is 3 x dwordx4 -- the second evaluation only the first --
-// instead of 9 dword loads of the reference's 36-B texels), PPT pixels per thread (independent
-// chains interleaved: ILP when the launch is small), and the caller's post-processing fused
-// (matching.py:66-76: p.long(), the occlusion test ||X11[p1] - X21|| < dist_thresh on the
-// pre-refine pixel, valid = converged & that; p1 as (u, v) for refine, or u + W v without it).
-// The arithmetic is iter_proj_kernel's, operation for operation (bitwise the same p_new).
-// ---------------------------------------------------------------------------------
-struct Bilin4 {
-    float w11, w12, w21, w22;
-    const float4 *r11, *r12, *r21, *r22;
-};
-
-__device__ __forceinline__ Bilin4 make_bilin4(const float4* __restrict__ img, int W, float u, float v) {
-    Bilin4 b;
-    const int u11 = (int)floorf(u);
-    const int v11 = (int)floorf(v);
-    const float du = u - (float)u11;
-    const float dv = v - (float)v11;
-    b.w11 = du * dv;
-    b.w12 = (float)((1.0 - (double)du) * (double)dv);
-    b.w21 = (float)((double)du * (1.0 - (double)dv));
-    b.w22 = (float)((1.0 - (double)du) * (1.0 - (double)dv));
-    const int64_t row0 = (int64_t)v11 * W;
-    const int64_t row1 = (int64_t)(v11 + 1) * W;
-    b.r11 = img + (row1 + u11 + 1) * 3;
-    b.r12 = img + (row1 + u11) * 3;
-    b.r21 = img + (row0 + u11 + 1) * 3;
-    b.r22 = img + (row0 + u11) * 3;
-    return b;
-}
-
-template <int CM>
-__device__ __forceinline__ float3 interp4(const Bilin4& b, int c) {
-    const float4 t11 = b.r11[c], t12 = b.r12[c], t21 = b.r21[c], t22 = b.r22[c];
-    float3 o;
-    o.x = cmad<CM>(b.w22, t22.x, cmad<CM>(b.w21, t21.x, cmm<CM>(b.w11, t11.x, b.w12, t12.x)));
-    o.y = cmad<CM>(b.w22, t22.y, cmad<CM>(b.w21, t21.y, cmm<CM>(b.w11, t11.y, b.w12, t12.y)));
-    o.z = cmad<CM>(b.w22, t22.z, cmad<CM>(b.w21, t21.z, cmm<CM>(b.w11, t11.z, b.w12, t12.z)));
-    return o;
-}
-
-struct IpState {
-    float u, v, lambda, px, py, pz;
-    uint8_t conv;
-};
-
-// one LM iteration of one pixel (matching_kernels.cu:153-268; iter_proj_kernel's arithmetic)
-template <int CM>
-__device__ __forceinline__ void ip_step(IpState& s, const float4* __restrict__ img, int W, float umax, float vmax,
-                                        float cost_thresh) {
-    const Bilin4 bl = make_bilin4(img, W, s.u, s.v);
-    const float3 r = interp4<CM>(bl, 0), gx = interp4<CM>(bl, 1), gy = interp4<CM>(bl, 2);
-    const float r_norm_inv = inv_f(sqrtf(cdot3<CM>(r.x, r.x, r.y, r.y, r.z, r.z)));
-    const float e0 = cmad<CM>(r.x, r_norm_inv, -s.px), e1 = cmad<CM>(r.y, r_norm_inv, -s.py),
-                e2 = cmad<CM>(r.z, r_norm_inv, -s.pz);
-    const float cost = cdot3<CM>(e0, e0, e1, e1, e2, e2);
-    float A00 = cdot3<CM>(gx.x, gx.x, gx.y, gx.y, gx.z, gx.z);
-    const float A01 = cdot3<CM>(gx.x, gy.x, gx.y, gy.y, gx.z, gy.z);
-    float A11 = cdot3<CM>(gy.x, gy.x, gy.y, gy.y, gy.z, gy.z);
-    const float b0 = -cdot3<CM>(e0, gx.x, e1, gx.y, e2, gx.z);
-    const float b1 = -cdot3<CM>(e0, gy.x, e1, gy.y, e2, gy.z);
-    A00 += s.lambda;
-    A11 += s.lambda;
-    const float det_inv = inv_f(cmm<CM>(A00, A11, -A01, A01));
-    const float u_new = clamp_ref(cmad<CM>(det_inv, cmm<CM>(A11, b0, -A01, b1), s.u), 1.0f, umax);
-    const float v_new = clamp_ref(cmad<CM>(det_inv, cmm<CM>(-A01, b0, A00, b1), s.v), 1.0f, vmax);
-    const Bilin4 bn = make_bilin4(img, W, u_new, v_new);
-    const float3 t = interp4<CM>(bn, 0);
-    const float n2_inv = inv_f(sqrtf(cdot3<CM>(t.x, t.x, t.y, t.y, t.z, t.z)));
-    const float f0 = cmad<CM>(t.x, n2_inv, -s.px), f1 = cmad<CM>(t.y, n2_inv, -s.py),
-                f2 = cmad<CM>(t.z, n2_inv, -s.pz);
-    const float new_cost = cdot3<CM>(f0, f0, f1, f1, f2, f2);
-    if (new_cost < cost) {
-        s.u = u_new;
-        s.v = v_new;
-        s.lambda = (float)((double)s.lambda * 0.1);
-        s.conv = new_cost < cost_thresh;
-    } else {
-        s.lambda = (float)((double)s.lambda * 10.0);
-        s.conv = cost < cost_thresh;
-    }
-}
-
-template <int CM, int PPT>
-__global__ __launch_bounds__(kBlock) void iter_proj_t4_kernel(
-    const float4* __restrict__ rays4, const float* __restrict__ pts, const float* __restrict__ p_init,
-    const float* __restrict__ X11, const float* __restrict__ X21, int H, int W, int64_t N, int64_t total,
-    int64_t span, int max_iter, float lambda_init, float cost_thresh, float dist_thresh,
-    int64_t* __restrict__ p1, int64_t* __restrict__ lin, uint8_t* __restrict__ valid) {
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const float umax = (float)(W - 2), vmax = (float)(H - 2);
-    IpState st[PPT];
-    const float4* img[PPT];
-    int64_t gs[PPT];
-    bool live[PPT];
-#pragma unroll
-    for (int q = 0; q < PPT; q++) {
-        const int64_t g = t + q * span;  // pixel sets one span apart: each wave's lanes stay contiguous
-        live[q] = g < total;
-        gs[q] = live[q] ? g : 0;
-        const int64_t b = gs[q] / N;
-        img[q] = rays4 + b * (int64_t)H * W * 3;
-        const float2 pi = *reinterpret_cast<const float2*>(p_init + gs[q] * 2);
-        st[q].u = clamp_ref(pi.x, 1.0f, umax);
-        st[q].v = clamp_ref(pi.y, 1.0f, vmax);
-        st[q].px = pts[gs[q] * 3 + 0];
-        st[q].py = pts[gs[q] * 3 + 1];
-        st[q].pz = pts[gs[q] * 3 + 2];
-        st[q].lambda = lambda_init;
-        st[q].conv = 0;
-    }
-    for (int it = 0; it < max_iter; it++) {
-#pragma unroll
-        for (int q = 0; q < PPT; q++) ip_step<CM>(st[q], img[q], W, umax, vmax, cost_thresh);
-    }
-    const int64_t HW = (int64_t)H * W;
-#pragma unroll
-    for (int q = 0; q < PPT; q++) {
-        if (!live[q]) continue;
-        const int64_t g = gs[q];
-        const int64_t b = g / HW;
-        // p.long() (truncation); iter_proj keeps p inside [1, W-2] x [1, H-2]
-        const int64_t u = (int64_t)st[q].u, v = (int64_t)st[q].v;
-        const float* a = X11 + (b * HW + v * W + u) * 3;
-        const float* x2 = X21 + g * 3;
-        const float d0 = a[0] - x2[0], d1 = a[1] - x2[1], d2 = a[2] - x2[2];
-        const float dist = __builtin_sqrtf(__builtin_fmaf(d2, d2, __builtin_fmaf(d1, d1, d0 * d0)));
-        valid[g] = (st[q].conv != 0) && (dist < dist_thresh);
-        if (lin) {
-            lin[g] = u + (int64_t)W * v;
-        } else {
-            p1[g * 2] = u;
-            p1[g * 2 + 1] = v;
-        }
-    }
 }
 
 template <int F, int R>
@@ -460,40 +335,6 @@ extern "C" int m3s_iter_proj_ex(const float* rays, const float* pts, const float
 }
 
 namespace m3s {
-// iter_proj + the caller's post-processing on the fused op's float4-texel ray image (above)
-int iter_proj_t4_launch(const float* rays4, const float* pts, const float* p_init, const float* X11,
-                        const float* X21, int64_t B, int64_t H, int64_t W, int max_iter, float lambda_init,
-                        float cost_thresh, float dist_thresh, int contract, int64_t* p1, int64_t* lin,
-                        uint8_t* valid, hipStream_t st) {
-    M3S_REQUIRE(contract == M3S_CONTRACT_NVCC || contract == M3S_CONTRACT_OFF || contract == M3S_CONTRACT_NVCC_RIGHT,
-                "iter_proj: unknown contraction convention %d", contract);
-    const int64_t N = H * W, total = B * N;
-    if (total == 0) return M3S_OK;
-    // two pixels per thread while that still leaves >= ~2 waves per SIMD (small launches:
-    // their chains interleave); one otherwise.  M3S_IP_PPT=1|2 forces it.
-    static const int ppt_env = [] {
-        const char* e = getenv("M3S_IP_PPT");
-        return e ? atoi(e) : 0;
-    }();
-    const int ppt = ppt_env == 1 || ppt_env == 2 ? ppt_env : (total <= 262144 ? 2 : 1);
-    const int64_t span = (total + ppt - 1) / ppt;
-    const float4* r4 = reinterpret_cast<const float4*>(rays4);
-#define M3S_IPT(CM, P)                                                                                          \
-    hipLaunchKernelGGL((iter_proj_t4_kernel<CM, P>), dim3(grid_for(span)), dim3(kBlock), 0, st, r4, pts, p_init, \
-                       X11, X21, (int)H, (int)W, N, total, span, max_iter, lambda_init, cost_thresh, dist_thresh,  \
-                       p1, lin, valid)
-#define M3S_IPT_P(CM)      \
-    if (ppt == 2) M3S_IPT(CM, 2); \
-    else M3S_IPT(CM, 1)
-    if (contract == M3S_CONTRACT_OFF) M3S_IPT_P(M3S_CONTRACT_OFF);
-    else if (contract == M3S_CONTRACT_NVCC_RIGHT) M3S_IPT_P(M3S_CONTRACT_NVCC_RIGHT);
-    else M3S_IPT_P(M3S_CONTRACT_NVCC);
-#undef M3S_IPT_P
-#undef M3S_IPT
-    M3S_LAUNCH_CHECK();
-    return M3S_OK;
-}
-
 // refine_matches on fp16 descriptors; lin != nullptr writes u + W v per pixel instead of (u, v)
 int refine_f16_launch(const uint16_t* D11, const uint16_t* D21, const int64_t* p1, int64_t* p1_new,
                       int64_t* lin, int64_t B, int64_t H, int64_t W, int64_t N, int64_t F, int radius,

@@ -225,6 +225,286 @@ __global__ __launch_bounds__(kBlock) void refine_mfma_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// refine_matches with the correlation on MFMA over LATTICE BUCKETS (variant LATTICE).
+//
+// At dilation d a pixel's 49 candidates are the lattice points c_p + d (i, j), |i|, |j| <= R, of
+// ITS centre c_p.  Two pixels share candidates only when their centres are congruent mod d, so
+// per level the tile's pixels are bucketed by class (u0 mod d, v0 mod d) -- d^2 classes, members
+// kept in pixel order -- and cut into groups of 16.  A group's windows, in lattice coordinates
+// (U, V) = floor(c / d), all lie in its box [Umin - R, Umax + R] x [Vmin - R, Vmax + R]; one
+// v_mfma_f32_16x16x32_f16 scores the group's 16 descriptors (A, K = 24 zero-padded to 32) against
+// 16 box cells (B, one 16-B piece per lane gathered from D11), and each of the 16 x 16 outputs that
+// lies in its pixel's window goes to the pixel's score table in LDS.  On smooth matches the boxes
+// are small (about (16/d + 6)^2 cells at d >= 4, (16 + 6) x (1 + 6) at d = 1), so every D11 row is
+// loaded once per group instead of once per candidate, and 25-45 % of the MFMA outputs are used
+// (the diagonal formulation above: 1/16).  Then per pixel the bound-and-rescore of
+// refine_mfma_kernel (same bound E, same shortlist rule) re-scores the possible winners exactly
+// in candidate order.  A group whose box exceeds kLatCellLimit cells (a discontinuity, far
+// starts) and pixels whose bound is not finite score every candidate exactly instead.
+// ---------------------------------------------------------------------------------
+constexpr int kLatCellLimit = 512;
+constexpr int kLatBatch = 8;  // box chunks (16 cells) whose gathers are in flight together
+// diagnostics builds only: 1 = no MFMA phase (every pixel scored exactly), 2 = no exact phase
+// (the results are then NOT refine_matches'), 3 = neither (bucketing alone)
+#ifndef M3S_LAT_DIAG
+#define M3S_LAT_DIAG 0
+#endif
+constexpr int kLatMaxD = 5;  // dilation levels with <= 25 classes; larger dilation_max: the caller falls back
+constexpr int kLatMaxCls = kLatMaxD * kLatMaxD;
+constexpr int kLatMaxItems = kBlock / 16 + kLatMaxCls;
+
+__device__ __forceinline__ int floordiv(int a, int d) { return a >= 0 ? a / d : -((-a + d - 1) / d); }
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void refine_lattice_kernel(
+    const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21, const int64_t* __restrict__ p1,
+    int64_t* __restrict__ p1_new, int64_t* __restrict__ lin, int H, int W, int64_t N, int64_t B, TileMap tm,
+    int dilation_max, const unsigned* __restrict__ hmax2, unsigned long long* __restrict__ stats) {
+    constexpr int F = 24;
+    constexpr int S = 2 * R + 1;
+    constexpr int NC = S * S;
+    static_assert(NC <= 64, "candidate mask is 64 bits");
+    // approximate scores [candidate][pixel of the tile], rows padded by one: the 16 lanes that
+    // write one pixel's scores (different candidates) hit 16 different banks
+    __shared__ float sS[NC][kBlock + 1];
+    __shared__ int sU[kBlock], sV[kBlock];   // lattice centre of each pixel at this level
+    __shared__ unsigned char sMem[kBlock];   // the tile's pixels sorted by class, pixel order within
+    __shared__ unsigned char sFall[kBlock];  // 1: score every candidate exactly at this level
+    __shared__ int sCnt[kBlock / 64][kLatMaxCls];
+    __shared__ int sBase[kBlock / 64][kLatMaxCls];
+    __shared__ int sOff[kLatMaxCls + 1];
+    __shared__ int sItem[kLatMaxItems];
+    __shared__ int sNItems;
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // the tile (the XCD-banded order of tile_pixel), every thread stays for the MFMAs
+    const int64_t nblk = (int64_t)gridDim.x, blk = blockIdx.x;
+    const int64_t per = (nblk + 7) / 8;
+    const int64_t lb = (blk % 8) * per + blk / 8;
+    if (lb >= (int64_t)tm.ntiles * B) return;  // uniform over the workgroup
+    const int64_t b = lb / tm.ntiles;
+    const int tt = (int)(lb - b * tm.ntiles);
+    const int ty = tt / tm.tiles_x, tx = tt - ty * tm.tiles_x;
+    auto pix_g = [&](int p) { return b * N + (int64_t)(ty * kTile + (p >> 4)) * W + tx * kTile + (p & 15); };
+    const bool active = tx * kTile + (t & 15) < W && ty * kTile + (t >> 4) < H;
+    const int64_t g = active ? pix_g(t) : 0;
+    const uint16_t* __restrict__ img = D11 + b * (int64_t)H * W * F;
+
+    half2_t q2[F / 2];
+    float qn2 = 0.0f;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
+#pragma unroll
+        for (int c = 0; c < F / 8; c++) {
+            uint4 w = src[c];
+            const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                q2[c * 4 + k] = hp[k];
+                qn2 = fmaf((float)hp[k].x, (float)hp[k].x, fmaf((float)hp[k].y, (float)hp[k].y, qn2));
+            }
+        }
+    }
+    const float hmax = sqrtf(__uint_as_float(hmax2[b])) * 1.00001f;
+    const float pbound = (sqrtf(qn2) * 1.00001f) * hmax;  // >= sum_k |q_k h_k| for every candidate
+    const float E = kRefineBoundRel * pbound + kRefineBoundAbs;
+    const bool score_all = !(pbound <= kRefineBoundMax);  // NaN / inf / fp16 overflow possible
+
+    int64_t u0 = active ? p1[g * 2 + 0] : 0;
+    int64_t v0 = active ? p1[g * 2 + 1] : 0;
+    half_t max_score = (half_t)kRefineHalfMaxInit;
+    int64_t u_new = u0, v_new = v0;
+    unsigned nresc = 0, ntotal = 0, nmfma = 0;
+    const int m = lane & 15, kc = lane >> 4;
+    for (int d = dilation_max; d > 0; d--) {
+        const int64_t rd = (int64_t)R * d;
+        const int ncls = d * d;
+        // 1. class and lattice centre (int32 lattice math while the centre is within 2^20 px)
+        const bool near = u0 >= -(1 << 20) && u0 <= (1 << 20) && v0 >= -(1 << 20) && v0 <= (1 << 20);
+        int cls = -1;
+        if (active && near) {
+            const int uu = (int)u0, vv = (int)v0;
+            const int U = floordiv(uu, d), V = floordiv(vv, d);
+            sU[t] = U;
+            sV[t] = V;
+            cls = (uu - U * d) * d + (vv - V * d);
+        }
+        sFall[t] = (active && (!near || score_all)) ? 1 : 0;
+        if (!(active && near && !score_all)) cls = -1;
+        // 2. rank within the class (pixel order), per wave
+        int rank = 0;
+        for (int c = 0; c < ncls; c++) {
+            const uint64_t mk = __ballot(cls == c);
+            if (cls == c) rank = __popcll(mk & ((1ull << lane) - 1ull));
+            if (lane == 0) sCnt[wave][c] = __popcll(mk);
+        }
+        __syncthreads();
+        // 3. class offsets, per-wave bases and the work items (class, group of 16): wave 0
+        if (wave == 0) {
+            int tot = 0;
+            if (lane < ncls) {
+#pragma unroll
+                for (int w = 0; w < kBlock / 64; w++) tot += sCnt[w][lane];
+            }
+            int inc = tot, ng = (tot + 15) / 16, ginc = ng;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(inc, off, 64), z = __shfl_up(ginc, off, 64);
+                if (lane >= off) {
+                    inc += y;
+                    ginc += z;
+                }
+            }
+            if (lane < ncls) {
+                int run = inc - tot;
+                sOff[lane] = run;
+#pragma unroll
+                for (int w = 0; w < kBlock / 64; w++) {
+                    sBase[w][lane] = run;
+                    run += sCnt[w][lane];
+                }
+                for (int q = 0; q < ng; q++) sItem[ginc - ng + q] = (lane << 8) | q;
+            }
+            if (lane == ncls - 1) sOff[ncls] = inc;
+            if (lane == 63) sNItems = ginc;
+        }
+        __syncthreads();
+        if (cls >= 0) sMem[sBase[wave][cls] + rank] = (unsigned char)t;
+        __syncthreads();
+        // 4. approximate scores over each group's lattice box
+        const int nitems = (M3S_LAT_DIAG & 1) ? 0 : sNItems;
+        if ((M3S_LAT_DIAG & 1) && active) sFall[t] = 1;
+        for (int it = wave; it < nitems; it += kBlock / 64) {
+            const int code = sItem[it];
+            const int c = code >> 8, grp = code & 255;
+            const int base = sOff[c] + 16 * grp, cnt = min(16, sOff[c + 1] - base);
+            const int pm = m < cnt ? (int)sMem[base + m] : -1;
+            const int Um = pm >= 0 ? sU[pm] : 0, Vm = pm >= 0 ? sV[pm] : 0;
+            int umin = pm >= 0 ? Um : INT_MAX, umax = pm >= 0 ? Um : INT_MIN;
+            int vmin = pm >= 0 ? Vm : INT_MAX, vmax = pm >= 0 ? Vm : INT_MIN;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {  // over the 16 members (each 16-lane row holds all)
+                umin = min(umin, __shfl_xor(umin, off, 64));
+                umax = max(umax, __shfl_xor(umax, off, 64));
+                vmin = min(vmin, __shfl_xor(vmin, off, 64));
+                vmax = max(vmax, __shfl_xor(vmax, off, 64));
+            }
+            const int bu = umax - umin + 2 * R + 1, bv = vmax - vmin + 2 * R + 1;
+            if (bu > kLatCellLimit || bv > kLatCellLimit || bu * bv > kLatCellLimit) {
+                if (lane < cnt) sFall[sMem[base + lane]] = 1;  // this group scores exactly
+                continue;
+            }
+            const int cells = bu * bv;
+            nmfma += (cells + 15) / 16;  // wave-uniform: counted by every lane, reported by lane 0
+            uint4 wa = make_uint4(0, 0, 0, 0);
+            if (pm >= 0 && kc < 3) wa = reinterpret_cast<const uint4*>(D21 + pix_g(pm) * F)[kc];
+            const half8_t A = __builtin_bit_cast(half8_t, wa);
+            // this lane's 4 output rows: members 4 kc + e
+            int pe[4], Ue[4], Ve[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                pe[e] = __shfl(pm, 4 * kc + e, 64);
+                Ue[e] = __shfl(Um, 4 * kc + e, 64);
+                Ve[e] = __shfl(Vm, 4 * kc + e, 64);
+            }
+            const int cu = c / d, cv = c - cu * d;  // the class's residues
+            // kLatBatch chunks at a time: their B gathers are issued together, then the MFMAs
+            for (int ch0 = 0; ch0 < cells; ch0 += 16 * kLatBatch) {
+                uint4 wb[kLatBatch];
+                int Ucs[kLatBatch], Vcs[kLatBatch];
+#pragma unroll
+                for (int q = 0; q < kLatBatch; q++) {
+                    const int ci = ch0 + 16 * q + m;
+                    const int qv = ci / bu;
+                    Ucs[q] = umin - R + (ci - qv * bu);
+                    Vcs[q] = vmin - R + qv;
+                    const int64_t u = (int64_t)cu + (int64_t)d * Ucs[q], v = (int64_t)cv + (int64_t)d * Vcs[q];
+                    wb[q] = make_uint4(0, 0, 0, 0);
+                    if (ci < cells && kc < 3 && inside_image(u, v, W, H))
+                        wb[q] = reinterpret_cast<const uint4*>(img + (v * W + u) * F)[kc];
+                    if (ci >= cells) Ucs[q] = INT_MIN / 2;  // no pixel's window
+                }
+#pragma unroll
+                for (int q = 0; q < kLatBatch; q++) {
+                    if (ch0 + 16 * q >= cells) break;  // wave-uniform
+                    float4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, __builtin_bit_cast(half8_t, wb[q]), acc, 0, 0, 0);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const unsigned di = (unsigned)(Ucs[q] - Ue[e] + R), dj = (unsigned)(Vcs[q] - Ve[e] + R);
+                        if (pe[e] >= 0 && di < (unsigned)S && dj < (unsigned)S) sS[di * S + dj][pe[e]] = acc[e];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // 5. per pixel: the shortlist of possible winners, re-scored exactly in candidate order
+        if (active && !(M3S_LAT_DIAG & 2)) {
+            const bool all = sFall[t] != 0;
+            uint64_t mask = 0;
+            float lo = -__int_as_float(0x7f800000);
+            if (!all) {
+#pragma unroll
+                for (int c = 0; c < NC; c++) {
+                    const int64_t u = u0 - rd + (int64_t)(c / S) * d, v = v0 - rd + (int64_t)(c % S) * d;
+                    if (inside_image(u, v, W, H)) lo = fmaxf(lo, sS[c][t] - E);
+                }
+            }
+            const float beat = (float)max_score;
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const int64_t u = u0 - rd + (int64_t)(c / S) * d, v = v0 - rd + (int64_t)(c % S) * d;
+                const bool in = inside_image(u, v, W, H);
+                ntotal += in;
+                if (in && (all || (sS[c][t] + E >= lo && sS[c][t] + E > beat))) mask |= 1ull << c;
+            }
+            nresc += __builtin_popcountll(mask);
+            while (mask) {  // up to 4 shortlisted rows in flight, then scored in candidate order
+                int cs[4];
+                uint4 rows[4][F / 8];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    cs[q] = mask ? __builtin_ctzll(mask) : -1;
+                    mask &= mask - 1;
+                    if (cs[q] >= 0) {
+                        const int64_t u = u0 - rd + (int64_t)(cs[q] / S) * d, v = v0 - rd + (int64_t)(cs[q] % S) * d;
+                        const uint4* src = reinterpret_cast<const uint4*>(img + (v * W + u) * F);
+#pragma unroll
+                        for (int k = 0; k < F / 8; k++) rows[q][k] = src[k];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (cs[q] < 0) break;
+                    const half_t score = score_f16<F>(q2, rows[q]);
+                    if (score > max_score) {
+                        max_score = score;
+                        u_new = u0 - rd + (int64_t)(cs[q] / S) * d;
+                        v_new = v0 - rd + (int64_t)(cs[q] % S) * d;
+                    }
+                }
+            }
+            u0 = u_new;
+            v0 = v_new;
+        }
+        __syncthreads();  // the next level rewrites the tables
+    }
+    if (active) store_match(p1_new, lin, g, W, u_new, v_new);
+    if (stats) {  // diagnostics: candidates re-scored exactly / in-image candidates
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            nresc += __shfl_xor(nresc, off, 64);
+            ntotal += __shfl_xor(ntotal, off, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(stats, (unsigned long long)nresc);
+            atomicAdd(stats + 1, (unsigned long long)ntotal);
+            atomicAdd(stats + 2, (unsigned long long)nmfma);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // refine_matches, bound-and-rescore on the VALU (opt-in M3S_REFINE_DOT2=1).  The same
 // exactness argument as refine_mfma_kernel, with the approximate scores from v_dot2c_f32_f16
 // (12 per candidate: fp16 products exact in fp32, fp32 sums) instead of 48 half-precision ops:
@@ -590,15 +870,14 @@ __global__ __launch_bounds__(kLdsThreads) void refine_lds_kernel(
 
 // exactly re-scored / in-image candidates of the bound-and-rescore variants
 static bool g_refine_stats_enabled = false;
-static unsigned long long g_refine_stats[2] = {0, 0};
+static unsigned long long g_refine_stats[3] = {0, 0, 0};
 
-extern "C" void m3s_refine_variant_stats(int enable, unsigned long long* out2) {
-    if (out2) {
-        out2[0] = g_refine_stats[0];
-        out2[1] = g_refine_stats[1];
+extern "C" void m3s_refine_variant_stats(int enable, unsigned long long* out3) {
+    if (out3) {
+        for (int k = 0; k < 3; k++) out3[k] = g_refine_stats[k];
     }
     g_refine_stats_enabled = enable != 0;
-    g_refine_stats[0] = g_refine_stats[1] = 0;
+    g_refine_stats[0] = g_refine_stats[1] = g_refine_stats[2] = 0;
 }
 
 extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
@@ -612,8 +891,10 @@ extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const ui
     M3S_REQUIRE(F == 24 && aligned && N == H * W && radius == 3,
                 "refine variant: needs F = 24, 16-B aligned descriptors, N = H*W and radius 3");
     M3S_REQUIRE(variant == M3S_REFINE_VARIANT_LDS || variant == M3S_REFINE_VARIANT_MFMA ||
-                    variant == M3S_REFINE_VARIANT_DOT2,
+                    variant == M3S_REFINE_VARIANT_DOT2 || variant == M3S_REFINE_VARIANT_LATTICE,
                 "refine variant: unknown kind %d", variant);
+    M3S_REQUIRE(variant != M3S_REFINE_VARIANT_LATTICE || dilation_max <= kLatMaxD,
+                "refine variant: the lattice kernel handles dilation_max <= %d", kLatMaxD);
     hipStream_t st = (hipStream_t)stream;
     int64_t* lin = nullptr;
     if (variant != M3S_REFINE_VARIANT_LDS) {
@@ -625,7 +906,7 @@ extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const ui
         const int64_t grid = (nblk + 7) / 8 * 8;
         // per-image max ||h||^2 (+ the optional re-score counters), stream-ordered scratch
         unsigned* scratch = nullptr;
-        const size_t sbytes = sizeof(unsigned) * (size_t)B + 2 * sizeof(unsigned long long) + 16;
+        const size_t sbytes = sizeof(unsigned) * (size_t)B + 3 * sizeof(unsigned long long) + 16;
         M3S_HIP_CHECK(hipMallocAsync((void**)&scratch, sbytes, st));
         M3S_HIP_CHECK(hipMemsetAsync(scratch, 0, sbytes, st));
         unsigned long long* stats = reinterpret_cast<unsigned long long*>(
@@ -634,7 +915,10 @@ extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const ui
         const int64_t HW = H * W;
         const unsigned hb = (unsigned)std::min<int64_t>((HW + kBlock - 1) / kBlock, 1024);
         hipLaunchKernelGGL(refine_hmax_kernel, dim3(hb, (unsigned)B), dim3(kBlock), 0, st, D11, HW, scratch);
-        if (variant == M3S_REFINE_VARIANT_MFMA)
+        if (variant == M3S_REFINE_VARIANT_LATTICE)
+            hipLaunchKernelGGL((refine_lattice_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
+                               p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, scratch, st_arg);
+        else if (variant == M3S_REFINE_VARIANT_MFMA)
             hipLaunchKernelGGL((refine_mfma_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
                                p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, scratch, st_arg);
         else
@@ -642,11 +926,10 @@ extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const ui
                                p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, scratch, st_arg);
         M3S_LAUNCH_CHECK();
         if (g_refine_stats_enabled) {
-            unsigned long long h[2];
+            unsigned long long h[3];
             M3S_HIP_CHECK(hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, st));
             M3S_HIP_CHECK(hipStreamSynchronize(st));
-            g_refine_stats[0] += h[0];
-            g_refine_stats[1] += h[1];
+            for (int k = 0; k < 3; k++) g_refine_stats[k] += h[k];
         }
         M3S_HIP_CHECK(hipFreeAsync(scratch, st));
     } else {

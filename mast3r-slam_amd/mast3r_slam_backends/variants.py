@@ -10,10 +10,10 @@ import torch
 
 from . import _check, _on_device, _ptr, _stream
 
-LDS, MFMA, DOT2 = 1, 2, 3  # M3S_REFINE_VARIANT_*
+LDS, MFMA, DOT2, LATTICE = 1, 2, 3, 4  # M3S_REFINE_VARIANT_*
 
-library_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
-                            "libm3s_variants.so")
+library_path = os.environ.get("M3S_VARIANTS_LIB", os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libm3s_variants.so"))
 if not os.path.exists(library_path):
     raise ImportError(f"refine variants library not found at {library_path}; build with `make -C mast3r-slam_amd`")
 lib = ctypes.CDLL(library_path)
@@ -42,8 +42,14 @@ def refine_matches_variant(kind, D11, D21, p1, window_size, dilation_max):
 
 
 def variant_stats(enable=True):
-    """Counters of the bound-and-rescore variants (MFMA, DOT2): (exactly re-scored, in-image
-    candidates) since the previous call; ``enable`` switches the counting for later calls."""
-    out = (ctypes.c_ulonglong * 2)()
+    """Counters of the bound-and-rescore variants (MFMA, DOT2, LATTICE): (exactly re-scored, in-image
+    candidates) since the previous call; ``enable`` switches the counting for later calls.
+    ``mfma_issued()`` gives the lattice kernel's MFMA count of the same interval."""
+    out = (ctypes.c_ulonglong * 3)()
     lib.m3s_refine_variant_stats(int(bool(enable)), ctypes.cast(out, ctypes.c_void_p))
+    variant_stats.mfma = int(out[2])
     return int(out[0]), int(out[1])
+
+
+def mfma_issued():
+    return getattr(variant_stats, "mfma", 0)

@@ -106,10 +106,12 @@ def test_refine_matches_f16_bit_exact(backend, oracle, B, H, W, dot2):
     assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
 
 
+@pytest.mark.parametrize("variant", [1, 4])  # variants.LDS, variants.LATTICE
 @pytest.mark.parametrize("scatter", [0, 3, 40, 10**6])
-def test_refine_lds_tile_and_fallback(backend, oracle, scatter):
-    """The LDS-tiled variant against the oracle and against the product candidate-gather
-    kernel, bitwise.  ``scatter`` spreads the starting
+def test_refine_lds_tile_and_fallback(backend, oracle, scatter, variant):
+    """The LDS-tiled and the lattice-bucket MFMA variants against the oracle and against the
+    product candidate-gather kernel, bitwise (for the lattice kernel, 40 px scatter overflows the
+    group boxes -> exact scoring of those groups).  ``scatter`` spreads the starting
     matches: 0/3 px keeps every tile's candidate box in LDS; 40 px makes the large-dilation
     boxes exceed the LDS budget (those levels gather from global memory); 10**6 puts most
     starts far outside the image (clipped windows, many empty)."""
@@ -121,7 +123,7 @@ def test_refine_lds_tile_and_fallback(backend, oracle, scatter):
         p1 = p1 + torch.randint(-scatter, scatter + 1, p1.shape, generator=g)
     D11 = mp.D11.half()
     D21 = mp.D21.reshape(B, H * W, -1).half()
-    out_l, out_o = _refine_both(backend, oracle, D11, D21, p1, variant=1)
+    out_l, out_o = _refine_both(backend, oracle, D11, D21, p1, variant=variant)
     (out_gth,) = backend.refine_matches(D11.cuda(), D21.cuda(), p1.cuda(), 3, 5)
     assert np.array_equal(out_l, out_o), f"{(out_l != out_o).any(-1).sum()} matches differ"
     assert np.array_equal(out_l, out_gth.cpu().numpy())
@@ -250,8 +252,9 @@ def test_fused_pipeline_matches_oracle_pipeline(backend, oracle, B, H, W, radius
         assert np.array_equal(valid.cpu().numpy(), valid_o)
 
 
+@pytest.mark.parametrize("variant", [2, 4])  # variants.MFMA, variants.LATTICE
 @pytest.mark.parametrize("warm", [False, True])
-def test_refine_mfma_path_bit_exact(backend, oracle, warm):
+def test_refine_mfma_path_bit_exact(backend, oracle, warm, variant):
     """The MFMA correlation variant (approximate scores on
     v_mfma_f32_16x16x32_f16, exact c10::Half re-scoring of every candidate within the error
     bound of the best) gives the oracle's indices bit for bit at 512x384, and re-scores only a
@@ -264,13 +267,13 @@ def test_refine_mfma_path_bit_exact(backend, oracle, warm):
     D21 = mp.D21.view(1, -1, 24).half()
     from mast3r_slam_backends import variants
     variants.variant_stats(True)
-    out_g, out_o = _refine_both(backend, oracle, D11, D21, p1, 3, 5, variant=variants.MFMA)
+    out_g, out_o = _refine_both(backend, oracle, D11, D21, p1, 3, 5, variant=variant)
     resc, total = variants.variant_stats(False)
     assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
     assert 0 < resc < total, (resc, total)
 
 
-@pytest.mark.parametrize("path", [2, 3])  # variants.MFMA, variants.DOT2
+@pytest.mark.parametrize("path", [2, 3, 4])  # variants.MFMA, variants.DOT2, variants.LATTICE
 def test_refine_mfma_path_edge_cases(backend, oracle, path):
     """Ties everywhere, all-negative scores, out-of-image starts, huge values (bound beyond fp16
     range: every candidate re-scored) and NaN descriptors, all bit-exact on the MFMA and the dot2

@@ -3,6 +3,6 @@
 set -e
 cd "$(dirname "$0")"
 mkdir -p bin
-for f in ubench_chol ubench_fp64 ubench_lat; do
+for f in ubench_chol ubench_fp64 ubench_lat repro_coop_exit; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -o bin/$f $f.hip
 done
