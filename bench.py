@@ -103,7 +103,13 @@ def main():
         return
     if os.environ.get("M3S_EXIT_MAPS"):
         _dump_maps_at_exit(os.environ["M3S_EXIT_MAPS"])
-    if world > 1:
+    # M3S_BENCH_COMM=host: a rehearsal of the N-rank flow on fewer GPUs (ranks may share one):
+    # gloo process group and the op's host-callback all-reduce instead of RCCL over xGMI
+    rehearse = world > 1 and os.environ.get("M3S_BENCH_COMM", "rccl") == "host"
+    if rehearse:
+        local_rank = local_rank % max(torch.cuda.device_count(), 1)
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
@@ -111,7 +117,7 @@ def main():
 
     import mast3r_slam_backends as mb
     from m3s import synth
-    from m3s.dist import RcclComm, gauss_newton_sharded, shard_range
+    from m3s.dist import HostComm, RcclComm, gauss_newton_sharded, shard_range
     from m3s.geometry import constrain_points_to_ray
 
     spec = synth.CONFIGS[args.config]
@@ -123,7 +129,7 @@ def main():
     g = synth.make_graph(args.config, device=dev, edge_range=(lo, hi))
     if mode == "calib":  # solve_GN_calib does this before the op (global_opt.py:172)
         g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
-    comm = RcclComm(rank, world, device=dev) if world > 1 else None
+    comm = (HostComm() if rehearse else RcclComm(rank, world, device=dev)) if world > 1 else None
     Twc0 = g.Twc.clone()
     Twc = g.Twc.clone()
     L = dict(LOCAL, K=g.K, height=g.H, width=g.W)
@@ -180,7 +186,7 @@ def main():
     ray_path = bool(dbg[3])
     n_ph = max(nph.value, 1)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -229,7 +235,8 @@ def main():
             "H": g.H,
             "W": g.W,
             "gn_iters_per_step": iters,
-            "parallelism": f"edge-sharded x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+            "parallelism": f"edge-sharded x{world}" + ((" + host all-reduce (rehearsal: ranks share GPUs)"
+                                                         if rehearse else " + RCCL all-reduce") if world > 1 else ""),
         },
         "phase_ms_per_iter": {
             "accumulate": acc_ms,

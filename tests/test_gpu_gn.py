@@ -336,6 +336,26 @@ def test_ray_constrained_calib_path_is_identical(backend, oracle, monkeypatch, i
     assert np.array_equal(T_fb, T_fb_gen)
 
 
+@pytest.mark.parametrize("W", [100, 102, 126])
+def test_pixel_coded_calib_records_at_odd_widths(backend, oracle, monkeypatch, W):
+    """The packed calib records carry the match as its pixel (v << 16 | u, decoded with a 24-bit
+    multiply-add): at widths that are not powers of two, with W % 4 == 0 (the ray-constrained
+    path) and W % 4 == 2 (positional Xj), the packed call is bitwise the unpacked one (which
+    decodes flat indices by division) and within 1e-5 of the oracle."""
+    from m3s.geometry import constrain_points_to_ray
+
+    g = synth.make_graph("cfg2", H=48, W=W, mode="calib")
+    g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    monkeypatch.setenv("M3S_GN_PACK", "2")
+    T_p, _ = _run_gpu(backend, g, "calib", 3)
+    monkeypatch.setenv("M3S_GN_PACK", "0")
+    T_u, _ = _run_gpu(backend, g, "calib", 3)
+    monkeypatch.setenv("M3S_GN_PACK", "1")
+    assert np.array_equal(T_p, T_u)
+    T_o, _, _ = _run_oracle(oracle, g, "calib", 3)
+    assert np.abs(T_p - T_o).max() / np.abs(T_o).max() < 1e-5
+
+
 def _cfg3_calib_graph():
     from m3s.geometry import constrain_points_to_ray
 

@@ -68,6 +68,10 @@ for s in $STEPS; do
                 --no-cpu-baseline --no-matching > gpurun_out/${TAG}_qbench4_$v.json 2> gpurun_out/${TAG}_qbench4_$v.err
             rc=$?; echo "qbench4 $v rc=$rc"; cat gpurun_out/${TAG}_qbench4_$v.json; ok_or_fail $rc qbench4_$v
         done ;;
+    rehearse2)  # the 2-rank bench flow on this one GPU (gloo + host all-reduce instead of RCCL)
+        M3S_BENCH_COMM=host timeout -k 10 400 python bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline \
+            --no-matching > gpurun_out/${TAG}_rehearse2.json 2> gpurun_out/${TAG}_rehearse2.err
+        rc=$?; echo "rehearse2 rc=$rc"; cat gpurun_out/${TAG}_rehearse2.json; tail -n 3 gpurun_out/${TAG}_rehearse2.err; ok_or_fail $rc rehearse2 ;;
     repro0)  # diagnostics of the exit-time SIGSEGV: no cooperative launch
         timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_repro0 -o run \
             -- tools/bin/repro_coop_exit 0 > gpurun_out/${TAG}_repro0.log 2>&1
