@@ -179,17 +179,21 @@ Stagings& stagings() {
     return *t_stagings;
 }
 
-// Number of point chunks per directed edge: chunks of ~kChunkTarget points (the per-XCD
-// working set of a chunk-major schedule is ~16 keyframes x chunk x 16 B), and at least
-// ~4096 workgroups overall when the edge count is small.
+// Points per accumulate task (edge x chunk).  16384 (round 3): the chunks amortise the task
+// prologue (pose loads, the affine map) and the workgroup reduction over twice the points of the
+// former 8192 -- cfg3 accumulate 0.342 -> 0.331 ms, cfg4 1.98 -> 1.94 ms; flat up to ~49k
+// (profiles/r03_chunk_ab.txt)
 int chunk_target() {
     static int t = [] {
         const char* e = getenv("M3S_ACC_CHUNK");
-        return e ? std::max(1024, atoi(e)) : 8192;
+        return e ? std::max(1024, atoi(e)) : 16384;
     }();
     return t;
 }
 
+// Number of point chunks per directed edge: chunks of ~chunk_target() points (the per-XCD
+// working set of a chunk-major schedule is ~16 keyframes x chunk x 16 B), and at least
+// ~4096 workgroups overall when the edge count is small.
 int choose_nchunks(int64_t HW, int64_t E_local) {
     int64_t nc = (HW + chunk_target() - 1) / chunk_target();
     const int64_t want = (4096 + std::max<int64_t>(E_local, 1) - 1) / std::max<int64_t>(E_local, 1);
