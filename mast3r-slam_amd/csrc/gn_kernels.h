@@ -9,7 +9,10 @@ namespace m3s {
 
 enum { GN_POINTS = 0, GN_RAYS = 1, GN_CALIB = 2 };
 
-constexpr int kAccThreads = 256;
+#ifndef M3S_ACC_THREADS
+#define M3S_ACC_THREADS 256
+#endif
+constexpr int kAccThreads = M3S_ACC_THREADS;  // accumulate / pack workgroup size
 constexpr int kNacc = 35;      // 28 (sym 7x7) + 7 (gradient)
 constexpr int kNaccPad = 36;   // partial record stride (floats)
 constexpr int kEdgeBlk = 36;   // per-edge record (doubles): Hjj packed 28 + vj 7 + pad
