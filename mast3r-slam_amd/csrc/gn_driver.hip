@@ -1112,6 +1112,25 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
     return M3S_OK;
 }
 
+// M3S_SOLVE_DEBUG: gn_solve_kernel writes its phase clocks to a device buffer; the driver
+// waits for the launch and prints them (debug runs only: the wait serialises the call)
+constexpr int kSolveDbgWords = kSolveDbgCycles + 1;
+unsigned long long* solve_dbg_buffer() {
+    static unsigned long long* p = nullptr;
+    if (p == nullptr && hipMalloc(&p, sizeof(unsigned long long) * kSolveDbgWords) != hipSuccess) p = nullptr;
+    if (p != nullptr) (void)hipMemset(p, 0, sizeof(unsigned long long) * kSolveDbgWords);
+    return p;
+}
+hipError_t launch_gn_solve_dbg(hipStream_t st, const SolveArgs& S) {
+    hipError_t e = launch_gn_solve(st, S);
+    if (e != hipSuccess || !S.debug || S.dbg == nullptr) return e;
+    unsigned long long h[kSolveDbgWords];
+    e = hipMemcpyAsync(h, S.dbg, sizeof(h), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) print_solve_debug(h);
+    return e;
+}
+
 int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     const Layout& L = c.L;
     const int npose = (int)(a.N - 1);
@@ -1155,6 +1174,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     S.delta_thresh = a.delta_thresh;
     S.flags = flags;
     S.debug = env_int("M3S_SOLVE_DEBUG", 0);
+    S.dbg = S.debug ? solve_dbg_buffer() : nullptr;
     S.contract = a.contract;
     if (S.debug) {
         static int printed = 0;
@@ -1182,14 +1202,14 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
             // the in-register tail + back-substitution + retraction
             S.do_fwd = 1;
             S.do_tail = S.do_back = 0;
-            M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+            M3S_HIP_CHECK(launch_gn_solve_dbg(c.st, S));
             S.do_fwd = 0;
             S.do_tail = S.do_back = 1;
-            M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+            M3S_HIP_CHECK(launch_gn_solve_dbg(c.st, S));
             return M3S_OK;
         }
         S.do_fwd = S.do_tail = S.do_back = 1;
-        M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+        M3S_HIP_CHECK(launch_gn_solve_dbg(c.st, S));
         return M3S_OK;
     }
     // multi-launch: one launch per round phase, the tail by the tiled dense Cholesky
@@ -1247,7 +1267,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         S.meta_lds = 1;
         S.do_fwd = 0;
         S.do_tail = S.do_back = 1;
-        M3S_HIP_CHECK(launch_gn_solve(c.st, S));
+        M3S_HIP_CHECK(launch_gn_solve_dbg(c.st, S));
         return M3S_OK;
     }
     if (sp.ntail > 0) c.may_timeout = true;  // the core's dataflow factorisation (chol_df)

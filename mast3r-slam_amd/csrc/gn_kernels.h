@@ -195,11 +195,16 @@ struct SolveArgs {
     float delta_thresh;
     int* flags;
     int do_fwd, do_tail, do_back;  // rounds | in-kernel dense tail | back rounds + retract
-    int debug;                     // M3S_SOLVE_DEBUG: printf phase times (wall clock, thread 0)
+    int debug;                     // M3S_SOLVE_DEBUG: phase times (wall clock, thread 0) ...
+    unsigned long long* dbg;       // ... written here ({n, entry, exit, (code, time) x n}); the
+                                   // driver prints them (no printf call in the kernel: a call
+                                   // gives it a stack frame)
     int contract;                  // the retraction's M3S_CONTRACT_* (m3s_gn_args.contract)
 };
 size_t solve_lds_bytes(int nmeta_lds);
 int solve_max_poses();  // x stays in LDS: the single-workgroup solve takes at most this many poses
+constexpr int kSolveDbgCycles = 3 + 2 * 96;  // SolveArgs::dbg word: shader cycles over the launch
+void print_solve_debug(const unsigned long long* host_copy);  // of SolveArgs::dbg
 hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
 // copy `bytes` (a multiple of 4; both addresses 16-B aligned) from pinned host memory (its
 // device address) to device memory, stream-ordered, by a kernel

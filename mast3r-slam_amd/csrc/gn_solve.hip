@@ -43,6 +43,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 
 #include "gn_kernels.h"
 #include "sim3.h"
@@ -52,6 +53,11 @@
 // a barrier, then a matvec per panel row
 #ifndef M3S_TAIL_FUSED_A
 #define M3S_TAIL_FUSED_A 1
+#endif
+// Diagnostic builds only (timing; the results are wrong): bit 1 = no L row stores to global in
+// the tail's phase A, bit 2 = no rank-7 MFMA update, bit 4 = no next-panel extraction
+#ifndef M3S_TAIL_DIAG
+#define M3S_TAIL_DIAG 0
 #endif
 
 namespace m3s {
@@ -68,8 +74,12 @@ constexpr int kMaxTicks = 96;
 constexpr int kSchurBatch = 4;  // Schur targets per 7-lane group with their loads in flight together
 
 // dynamic LDS (doubles): a union of the tail buffers and the round staging, then the plan ints
+// The extracted panel is a strip of two whole tile columns (J0, J0 + 1: every pose's 7 columns
+// lie in them), written branch-free from the accumulators -- the per-lane row / column tests
+// of extracting only the 7 columns cost ~1 us per pose step; row stride 33: one pad double.
+constexpr int kSS = 33;
 constexpr int kOffPn = 0;
-constexpr int kOffPop = kOffPn + kTailMax * kPS;
+constexpr int kOffPop = kOffPn + kTailMax * kSS;
 constexpr int kOffZ = kOffPop + kTailMax * kPS;
 constexpr int kOffL = kOffZ + kTailMax;
 constexpr int kTailDoubles = kOffL + kTailPoseMax * kLRec;
@@ -77,7 +87,9 @@ constexpr int kOffX = kTailDoubles;  // x (7 per pose) after the tail buffers: l
 constexpr int kOffWst = 0;                                   // round: W blocks of the round
 constexpr int kOffYst = kOffWst + kSolveWStage;              // round: y of the round's poses
 constexpr int kRoundDoubles = kOffYst + 7 * kSolveRoundPoses;
-constexpr int kRegionDoubles = kTailDoubles > kRoundDoubles ? kTailDoubles : kRoundDoubles;
+constexpr int kSolvePosesX = 312;  // poses whose x fits after the tail buffers
+constexpr int kRegionDoubles =
+    kTailDoubles + 7 * kSolvePosesX > kRoundDoubles ? kTailDoubles + 7 * kSolvePosesX : kRoundDoubles;
 
 __host__ __device__ constexpr int pk(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower
 
@@ -206,7 +218,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
                                            bool& bad, Tick& tick) {
     constexpr SlotMap SM = make_slot_map(T, W);
     constexpr int NS = SM.n;
-    double* __restrict__ sPn = smem + kOffPn;    // extracted panel (7 columns used)
+    double* __restrict__ sPn = smem + kOffPn;    // extracted strip: tile columns J0, J0 + 1
     double* __restrict__ sPop = smem + kOffPop;  // MFMA operand: L panel rows (0 outside live rows)
     double* __restrict__ sZ = smem + kOffZ;      // tail RHS -> y -> (back) partial sums
     double* __restrict__ sL = smem + kOffL;      // per tail pose: packed L_KK^-1
@@ -250,23 +262,16 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
     }
     for (int i = tid; i < kTailMax * kPS; i += kThreads) sPop[i] = 0.0;
     for (int i = tid; i < n; i += kThreads) sZ[i] = a.b[(int64_t)Mtail[i / 7] * 7 + i % 7];
-    // the panel of pose 0 (tile column 0)
+    // the strip of pose 0 (tile column 0)
 #pragma unroll
     for (int k = 0; k < NS; k++) {
         if (SM.J[k] == 0) {
-            const int col = lane & 15;
-            if (col < 7) {
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int row = 16 * SM.I[k] + (lane >> 4) + 4 * e;
-                    if (row >= col && row < n) sPn[row * kPS + col] = -acc[k][e];
-                }
-            }
+            for (int e = 0; e < 4; e++) sPn[(16 * SM.I[k] + (lane >> 4) + 4 * e) * kSS + (lane & 15)] = -acc[k][e];
         }
     }
     lds_barrier();
     tick(6);
-
 #if M3S_TAIL_FUSED_A
     double yprev[7];  // y of the previous pose, written to sZ by one thread a phase later
 #endif
@@ -288,14 +293,15 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
             const bool prow = tid < nrows;
             const int m = tid - nrows;  // diagonal-column role: 0 <= m < 7
             const int i = c0 + 7 + tid;
+            const int so = c0 & 15;  // the pose's first column in the strip
 #pragma unroll
             for (int r = 0; r < 7; r++) {
 #pragma unroll
-                for (int j = 0; j <= r; j++) L[pk(r, j)] = sPn[(c0 + r) * kPS + j];
+                for (int j = 0; j <= r; j++) L[pk(r, j)] = sPn[(c0 + r) * kSS + so + j];
                 z[r] = sZ[c0 + r];
             }
 #pragma unroll
-            for (int c = 0; c < 7; c++) in[c] = prow ? sPn[i * kPS + c] : (c == m ? 1.0 : 0.0);
+            for (int c = 0; c < 7; c++) in[c] = prow ? sPn[i * kSS + so + c] : (c == m ? 1.0 : 0.0);
             const double zr0 = prow ? sZ[i] : 0.0;
             chol7(L, inv, bad);
             fwd7(L, inv, z, yK);
@@ -306,7 +312,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
 #pragma unroll
                 for (int c = 0; c < 7; c++) {
                     sPop[i * kPS + c] = out[c];
-                    Lg[c] = out[c];
+                    if (!(M3S_TAIL_DIAG & 1)) Lg[c] = out[c];
                     zr = fma(-out[c], yK[c], zr);
                 }
                 sZ[i] = zr;
@@ -329,7 +335,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
 #pragma unroll
             for (int i = 0; i < 7; i++) {
 #pragma unroll
-                for (int j = 0; j <= i; j++) L[pk(i, j)] = sPn[(c0 + i) * kPS + j];
+                for (int j = 0; j <= i; j++) L[pk(i, j)] = sPn[(c0 + i) * kSS + (c0 & 15) + j];
                 z[i] = sZ[c0 + i];
             }
             chol7(L, inv, bad);
@@ -360,7 +366,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
                 double in[7], out[7], y[7];
 #pragma unroll
                 for (int c = 0; c < 7; c++) {
-                    in[c] = sPn[i * kPS + c];
+                    in[c] = sPn[i * kSS + (c0 & 15) + c];
                     y[c] = sZ[c0 + c];
                 }
                 double zr = sZ[i];
@@ -409,7 +415,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
             for (int k = 0; k < NS; k++) kf += SM.J[k] < Jmin;
 #define M3S_MF(k)                                                                                 \
     case k:                                                                                       \
-        if constexpr (k < NS) {                                                                   \
+        if constexpr (k < NS && !(M3S_TAIL_DIAG & 2)) {                                           \
             acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(P0[SM.I[k]], P0[SM.J[k]], acc[k], 0, 0, 0); \
             acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(P1[SM.I[k]], P1[SM.J[k]], acc[k], 0, 0, 0); \
         }                                                                                         \
@@ -424,39 +430,19 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
             }
 #undef M3S_MF
             static_assert(NS <= 32, "tail slot map exceeds the unrolled MFMA switch");
-            if (K + 1 < nt) {
+            if (K + 1 < nt && !(M3S_TAIL_DIAG & 4)) {
+                // the next pose's strip: its tile columns J0 and J1 (= J0 or J0 + 1), whole tiles
                 const int c1 = c0 + 7;
                 const int J0 = c1 >> 4, J1 = (c1 + 6) >> 4;
-                int klo = 0, khi = 0;
 #pragma unroll
                 for (int k = 0; k < NS; k++) {
-                    klo += SM.J[k] < J0;
-                    khi += SM.J[k] <= J1;
+                    if (SM.J[k] == J0 || SM.J[k] == J1) {
+                        const int cl = 16 * (SM.J[k] - J0) + (lane & 15);
+#pragma unroll
+                        for (int e = 0; e < 4; e++)
+                            sPn[(16 * SM.I[k] + (lane >> 4) + 4 * e) * kSS + cl] = -acc[k][e];
+                    }
                 }
-                const int col_l = (lane & 15);
-                const int rbase = (lane >> 4);
-#define M3S_EX(k)                                                                                 \
-    case k:                                                                                       \
-        if constexpr (k < NS) {                                                                   \
-            if (k >= khi) break;                                                                  \
-            const int col = 16 * SM.J[k] + col_l;                                                 \
-            if (col >= c1 && col < c1 + 7) {                                                      \
-                _Pragma("unroll") for (int e = 0; e < 4; e++) {                                    \
-                    const int row = 16 * SM.I[k] + rbase + 4 * e;                                 \
-                    if (row >= col && row < n) sPn[row * kPS + (col - c1)] = -acc[k][e];          \
-                }                                                                                 \
-            }                                                                                     \
-        }                                                                                         \
-        [[fallthrough]];
-                switch (klo) {
-                    M3S_EX(0) M3S_EX(1) M3S_EX(2) M3S_EX(3) M3S_EX(4) M3S_EX(5) M3S_EX(6) M3S_EX(7)
-                    M3S_EX(8) M3S_EX(9) M3S_EX(10) M3S_EX(11) M3S_EX(12) M3S_EX(13) M3S_EX(14)
-                    M3S_EX(15) M3S_EX(16) M3S_EX(17) M3S_EX(18) M3S_EX(19) M3S_EX(20) M3S_EX(21)
-                    M3S_EX(22) M3S_EX(23) M3S_EX(24) M3S_EX(25) M3S_EX(26) M3S_EX(27) M3S_EX(28)
-                    M3S_EX(29) M3S_EX(30) M3S_EX(31)
-                    default: break;
-                }
-#undef M3S_EX
             }
             if (K >= 3 && K < 5) {
                 if (NS > 0) asm volatile("s_nop 0" :: "v"(acc[NS - 1][0]));
@@ -465,6 +451,7 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
         }
         lds_barrier();
         if (K >= 3 && K < 5) tick(11);
+        else tick(15);  // a whole pose step
     }
     tick(2);
 #if M3S_TAIL_FUSED_A
@@ -476,15 +463,15 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
 
     __syncthreads();  // the L rows (global, written by every wave) are read below
     // back-substitution L^T x = y over the tail, right-looking: x_K = L_KK^-T z_K, then every
-    // z_j (j < 7K) drops its L[7K + c][j] x_K[c] terms.  The L entries a thread needs for the
-    // next pose are prefetched before the barrier.
-    double lp[7];
-    {
-        const int c0 = 7 * (nt - 1);
+    // z_j (j < 7K) drops its L[7K + c][j] x_K[c] terms.  The L entries a thread needs are
+    // prefetched three poses ahead (an L2 round trip is longer than one pose step) into three
+    // buffers used in rotation by a loop unrolled by 3, so no register copy waits on a load.
+    auto load_lp = [&](int K, double (&dst)[7]) {
+        const int c0 = 7 * K;
 #pragma unroll
-        for (int c = 0; c < 7; c++) lp[c] = tid < c0 ? a.Lg[(int64_t)(c0 + c) * n + tid] : 0.0;
-    }
-    for (int K = nt - 1; K >= 0; K--) {
+        for (int c = 0; c < 7; c++) dst[c] = (K >= 0 && tid < c0) ? a.Lg[(int64_t)(c0 + c) * n + tid] : 0.0;
+    };
+    auto back_step = [&](int K, double (&lp)[7]) {
         const int c0 = 7 * K;
         double Li[28], z[7], xk[7];
 #pragma unroll
@@ -509,12 +496,17 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
             for (int c = 0; c < 7; c++) s2 = fma(-lp[c], xk[c], s2);
             sZ[tid] = s2;
         }
-        if (K > 0) {
-            const int c1 = c0 - 7;
-#pragma unroll
-            for (int c = 0; c < 7; c++) lp[c] = tid < c1 ? a.Lg[(int64_t)(c1 + c) * n + tid] : 0.0;
-        }
+        if (K >= 3) load_lp(K - 3, lp);  // this buffer's next pose
         lds_barrier();
+    };
+    double lp0[7], lp1[7], lp2[7];
+    load_lp(nt - 1, lp0);
+    load_lp(nt - 2, lp1);
+    load_lp(nt - 3, lp2);
+    for (int K = nt - 1; K >= 0; K -= 3) {
+        back_step(K, lp0);
+        if (K >= 1) back_step(K - 1, lp1);
+        if (K >= 2) back_step(K - 2, lp2);
     }
     lds_barrier();  // x of the tail (LDS) is read by the back rounds
     tick(3);
@@ -525,6 +517,11 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
 template <int T, int NT>
 __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
     constexpr int NW = NT / 64;
+    __shared__ uint64_t sEntry, sEntryCyc;  // M3S_SOLVE_DEBUG: the clocks before the flag's round trip
+    if (a.debug && threadIdx.x == 0) {
+        sEntry = wall_clock64();
+        sEntryCyc = __builtin_amdgcn_s_memtime();  // shader clock: the effective frequency
+    }
     if (a.flags[kFlagDone]) return;
     extern __shared__ double smem[];
     __shared__ double sRed[NW];
@@ -551,8 +548,25 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
     // the plan integers, staged in LDS in one coalesced pass (the host only selects this solver
     // when they fit).  M must be a known-LDS pointer: a generic pointer compiles to FLAT loads,
     // and waiting on a FLAT load also waits for every outstanding global store (~1 us each).
+    // Batches of 8 loads per thread in flight before their LDS stores (a plain loop waited for
+    // each load in turn: ~14 dependent L2 round trips for cfg3's plan).
     int* __restrict__ M = reinterpret_cast<int*>(smem + kRegionDoubles);
-    for (int i = tid; i < a.nmeta; i += NT) M[i] = a.meta[i];
+    {
+        constexpr int kB = 8;
+        for (int i0 = 0; i0 < a.nmeta; i0 += kB * NT) {
+            int v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; u++) {
+                const int i = i0 + u * NT + tid;
+                v[u] = i < a.nmeta ? a.meta[i] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kB; u++) {
+                const int i = i0 + u * NT + tid;
+                if (i < a.nmeta) M[i] = v[u];
+            }
+        }
+    }
     lds_barrier();
     tick(14);
     const int* __restrict__ Mrounds = M + a.o_rounds;
@@ -892,26 +906,55 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
         __syncthreads();
         if (tid == 0 && sFail) a.flags[kFlagFail] = 1;
     }
-    if (a.debug && tid == 0) {
-        for (int k = 1; k < nticks; k++) {
-            const double us = (double)(sT[k] - sT[k - 1]) * 0.01;
-            switch (sTk[k]) {
-                case 1: printf("gn_solve  R: schur+barrier %8.2f us\n", us); break;
-                case 2: printf("gn_solve tail factor %8.2f us\n", us); break;
-                case 3: printf("gn_solve tail back   %8.2f us\n", us); break;
-                case 4: printf("gn_solve back rounds %8.2f us\n", us); break;
-                case 6: printf("gn_solve tail load   %8.2f us\n", us); break;
-                case 7: printf("gn_solve  K: A1 chol (w0)  %8.2f us\n", us); break;
-                case 8: printf("gn_solve  K: A2 rows       %8.2f us\n", us); break;
-                case 9: printf("gn_solve  K: B mfma+extract %8.2f us\n", us); break;
-                case 11: printf("gn_solve  K: barrier B     %8.2f us\n", us); break;
-                case 12: printf("gn_solve  R: factor (w0)  %8.2f us\n", us); break;
-                case 13: printf("gn_solve  R: schur (w0)   %8.2f us\n", us); break;
-                case 14: printf("gn_solve plan to LDS  %8.2f us\n", us); break;
-                default: printf("gn_solve retract     %8.2f us\n", us); break;
+    if (a.debug) {
+        __syncthreads();
+        __builtin_amdgcn_s_waitcnt(0);  // the x / dx / Twc stores acknowledged
+        if (tid == 0 && a.dbg != nullptr) {
+            const uint64_t t_exit = wall_clock64();
+            const uint64_t c_exit = __builtin_amdgcn_s_memtime();
+            a.dbg[kSolveDbgCycles] = c_exit - sEntryCyc;
+            a.dbg[0] = (unsigned long long)nticks;
+            a.dbg[1] = sEntry;
+            a.dbg[2] = t_exit;
+            for (int k = 0; k < nticks; k++) {
+                a.dbg[3 + 2 * k] = (unsigned long long)sTk[k];
+                a.dbg[4 + 2 * k] = sT[k];
             }
         }
     }
+}
+
+void print_solve_debug(const unsigned long long* h) {
+    const int n = (int)h[0];
+    if (n <= 0 || n > kMaxTicks) return;
+    const unsigned long long* T = h + 3;
+    auto us = [](unsigned long long x, unsigned long long y) { return (double)(y - x) * 0.01; };
+    fprintf(stderr, "gn_solve entry->first tick %8.2f us\n", us(h[1], T[1]));
+    for (int k = 1; k < n; k++) {
+        const double d = us(T[2 * k - 1], T[2 * k + 1]);
+        const char* what = "retract";
+        switch ((int)T[2 * k]) {
+            case 1: what = " R: schur+barrier"; break;
+            case 2: what = "tail factor"; break;
+            case 3: what = "tail back"; break;
+            case 4: what = "back rounds"; break;
+            case 6: what = "tail load"; break;
+            case 7: what = " K: A1 chol (w0)"; break;
+            case 8: what = " K: A2 rows"; break;
+            case 9: what = " K: B mfma+extract"; break;
+            case 11: what = " K: barrier B"; break;
+            case 12: what = " R: factor (w0)"; break;
+            case 13: what = " R: schur (w0)"; break;
+            case 14: what = "plan to LDS"; break;
+            case 15: what = " K: pose step"; break;
+            default: break;
+        }
+        fprintf(stderr, "gn_solve %-20s %8.2f us\n", what, d);
+    }
+    fprintf(stderr, "gn_solve last tick->exit %8.2f us\n", us(T[2 * n - 1], h[2]));
+    fprintf(stderr, "gn_solve entry->exit %8.2f us\n", us(h[1], h[2]));
+    fprintf(stderr, "gn_solve shader clock %8.0f MHz over the launch\n",
+                (double)h[kSolveDbgCycles] / us(h[1], h[2]));
 }
 
 int solve_max_poses() { return (kRegionDoubles - kOffX) / 7; }
