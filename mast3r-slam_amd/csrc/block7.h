@@ -38,26 +38,29 @@ __device__ __forceinline__ void chol7(double (&a)[28], double (&inv)[7], bool& b
     }
 }
 
-// out = L^-1 in (forward substitution)
+// out = L^-1 in (forward substitution), column-oriented: each solved entry is applied to all
+// later ones at once, so the dependent chain is 2 ops per entry (14), not up to 7 (28) -- on the
+// pivot chain of every pose step (a dependent f64 op costs tens of cycles on one wave)
 __device__ __forceinline__ void fwd7(const double (&L)[28], const double (&inv)[7],
                                      const double (&in)[7], double (&out)[7]) {
+    double s[7];
+#pragma unroll
+    for (int c = 0; c < 7; c++) s[c] = in[c];
 #pragma unroll
     for (int c = 0; c < 7; c++) {
-        double s = in[c];
+        out[c] = s[c] * inv[c];
 #pragma unroll
-        for (int m = 0; m < c; m++) s = fma(-L[pk(c, m)], out[m], s);
-        out[c] = s * inv[c];
+        for (int r = c + 1; r < 7; r++) s[r] = fma(-L[pk(r, c)], out[c], s[r]);
     }
 }
 
-// z <- L^-T z (backward substitution)
+// z <- L^-T z (backward substitution), column-oriented like fwd7
 __device__ __forceinline__ void bwd7(const double (&L)[28], const double (&inv)[7], double (&z)[7]) {
 #pragma unroll
     for (int c = 6; c >= 0; c--) {
-        double s = z[c];
+        z[c] *= inv[c];
 #pragma unroll
-        for (int m = c + 1; m < 7; m++) s = fma(-L[pk(m, c)], z[m], s);
-        z[c] = s * inv[c];
+        for (int m = 0; m < c; m++) z[m] = fma(-L[pk(c, m)], z[c], z[m]);
     }
 }
 

@@ -55,7 +55,8 @@
 #define M3S_TAIL_FUSED_A 1
 #endif
 // Diagnostic builds only (timing; the results are wrong): bit 1 = no L row stores to global in
-// the tail's phase A, bit 2 = no rank-7 MFMA update, bit 4 = no next-panel extraction
+// the tail's phase A, bit 2 = no rank-7 MFMA update, bit 4 = no next-panel extraction, bit 8 =
+// no 7x7 factor / forward substitutions in phase A
 #ifndef M3S_TAIL_DIAG
 #define M3S_TAIL_DIAG 0
 #endif
@@ -93,30 +94,6 @@ constexpr int kRegionDoubles =
 
 __host__ __device__ constexpr int pk(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower
 
-// Compile-time tile map of a T x T tile lower triangle: tile column J is cut into groups of
-// 4 consecutive tile rows (I0, I0+1, I0+2, I0+3), one per wave; slot s = one group.
-__host__ __device__ constexpr int tail_slots(int T) {
-    int n = 0;
-    for (int J = 0; J < T; J++) n += (T - J + 3) / 4;
-    return n;
-}
-__host__ __device__ constexpr int slot_J(int T, int s) {
-    for (int J = 0; J < T; J++) {
-        const int g = (T - J + 3) / 4;
-        if (s < g) return J;
-        s -= g;
-    }
-    return T;
-}
-__host__ __device__ constexpr int slot_I0(int T, int s) {
-    for (int J = 0; J < T; J++) {
-        const int g = (T - J + 3) / 4;
-        if (s < g) return J + 4 * s;
-        s -= g;
-    }
-    return T;
-}
-
 // Workgroup barrier that orders LDS only: it waits for this wave's LDS operations but not for
 // its global stores (a __syncthreads() release fence waits for every outstanding global store
 // to be acknowledged, ~1 us).  Global data handed between waves of the solve always crosses a
@@ -149,26 +126,29 @@ __device__ __forceinline__ void chol7(double (&a)[28], double (&inv)[7], bool& b
     }
 }
 
-// out = L^-1 in (forward substitution)
+// out = L^-1 in (forward substitution), column-oriented: each solved entry is applied to all
+// later ones at once, so the dependent chain is 2 ops per entry (14), not up to 7 (28) -- on the
+// pivot chain of every pose step (a dependent f64 op costs tens of cycles on one wave)
 __device__ __forceinline__ void fwd7(const double (&L)[28], const double (&inv)[7],
                                      const double (&in)[7], double (&out)[7]) {
+    double s[7];
+#pragma unroll
+    for (int c = 0; c < 7; c++) s[c] = in[c];
 #pragma unroll
     for (int c = 0; c < 7; c++) {
-        double s = in[c];
+        out[c] = s[c] * inv[c];
 #pragma unroll
-        for (int m = 0; m < c; m++) s = fma(-L[pk(c, m)], out[m], s);
-        out[c] = s * inv[c];
+        for (int r = c + 1; r < 7; r++) s[r] = fma(-L[pk(r, c)], out[c], s[r]);
     }
 }
 
-// z <- L^-T z (backward substitution)
+// z <- L^-T z (backward substitution), column-oriented like fwd7
 __device__ __forceinline__ void bwd7(const double (&L)[28], const double (&inv)[7], double (&z)[7]) {
 #pragma unroll
     for (int c = 6; c >= 0; c--) {
-        double s = z[c];
+        z[c] *= inv[c];
 #pragma unroll
-        for (int m = c + 1; m < 7; m++) s = fma(-L[pk(m, c)], z[m], s);
-        z[c] = s * inv[c];
+        for (int m = 0; m < c; m++) z[m] = fma(-L[pk(c, m)], z[c], z[m]);
     }
 }
 
@@ -199,17 +179,35 @@ struct SlotMap {
     int n;
     int I[64], J[64];
 };
+// Tiles are dealt to the 4 waves so that their MFMA issue is balanced: a tile of column J is
+// updated at every pose step until its column is factored, ~(16 J + 9) / 7 steps; tiles are
+// taken longest-lived first and each goes to the wave with the least work so far (fewest
+// slots on a tie).  (The former map -- groups of 4 consecutive rows per column, one row per
+// wave -- gave wave 0 twice the slot-steps of wave 3.)  A wave's slots are sorted by J, so the
+// live slots at a step are a suffix.
+__host__ __device__ constexpr int tile_life(int J) { return (16 * J + 9 + 6) / 7; }
 __host__ __device__ constexpr SlotMap make_slot_map(int T, int W) {
-    SlotMap m{};
-    m.n = 0;
-    for (int s = 0; s < tail_slots(T); s++) {
-        const int I = slot_I0(T, s) + W, J = slot_J(T, s);
-        if (I < T) {
-            m.I[m.n] = I;
-            m.J[m.n] = J;
-            m.n++;
+    int load[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+    int owner[16][16] = {};
+    for (int J = T - 1; J >= 0; J--) {
+        for (int I = T - 1; I >= J; I--) {
+            int best = 0;
+            for (int w = 1; w < 4; w++)
+                if (load[w] < load[best] || (load[w] == load[best] && cnt[w] < cnt[best])) best = w;
+            owner[I][J] = best;
+            load[best] += tile_life(J);
+            cnt[best]++;
         }
     }
+    SlotMap m{};
+    m.n = 0;
+    for (int J = 0; J < T; J++)
+        for (int I = J; I < T; I++)
+            if (owner[I][J] == W) {
+                m.I[m.n] = I;
+                m.J[m.n] = J;
+                m.n++;
+            }
     return m;
 }
 
@@ -303,9 +301,18 @@ __device__ __forceinline__ void tail_solve(const SolveArgs& a, const int* __rest
 #pragma unroll
             for (int c = 0; c < 7; c++) in[c] = prow ? sPn[i * kSS + so + c] : (c == m ? 1.0 : 0.0);
             const double zr0 = prow ? sZ[i] : 0.0;
+#if M3S_TAIL_DIAG & 8
+#pragma unroll
+            for (int c = 0; c < 7; c++) {
+                yK[c] = z[c] + L[pk(c, c)];
+                out[c] = in[c] + L[pk(6, c)];
+                inv[c] = 1.0;
+            }
+#else
             chol7(L, inv, bad);
             fwd7(L, inv, z, yK);
             fwd7(L, inv, in, out);
+#endif
             if (prow) {
                 double* Lg = a.Lg + (int64_t)i * n + c0;
                 double zr = zr0;
