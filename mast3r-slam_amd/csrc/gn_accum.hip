@@ -669,9 +669,23 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
 // idx 8 + valid 1 + Q 4 + Cj 4 + gathered Ci 4 = 21 B, and the point math is unchanged
 // (invalid points are still evaluated with weight 0, so NaN poisoning is kept).
 // ---------------------------------------------------------------------------
+// Per keyframe n: cok[n] stays 1 (as uploaded) iff every confidence c of it passes c > C_thresh
+// (a NaN fails, like the reference's test).  The pack then skips its 8 B per point-edge of Cj
+// reads and Ci gathers for edges whose two keyframes pass: the same validity bits, decided from
+// one pass over the N x HW confidences instead of one per directed edge (cfg3: 4 per keyframe).
+__global__ __launch_bounds__(256) void gn_cpass_kernel(const float* __restrict__ Cs, AccParams P,
+                                                       int* __restrict__ cok, const int* __restrict__ flags) {
+    if (flags[kFlagDone]) return;
+    const int n = blockIdx.y;
+    const float* __restrict__ C = Cs + (int64_t)n * P.HW;
+    bool ok = true;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < P.HW; k += gridDim.x * 256) ok = ok && (C[k] > P.C_thresh);
+    if (!__all(ok) && (threadIdx.x & 63) == 0) cok[n] = 0;  // benign race: every writer stores 0
+}
+
 __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
     const float* __restrict__ Cs, const int* __restrict__ ii_loc, const int* __restrict__ jj_loc,
-    EdgeSrc es, AccParams P, int4* __restrict__ pack, const int* __restrict__ flags) {
+    EdgeSrc es, AccParams P, const int* __restrict__ cok, int4* __restrict__ pack, const int* __restrict__ flags) {
     if (flags[kFlagDone]) return;
     const int e = blockIdx.y;
     const int HW = P.HW;
@@ -691,7 +705,10 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
     const longlong2 id01 = *reinterpret_cast<const longlong2*>(idx + k);
     const longlong2 id23 = *reinterpret_cast<const longlong2*>(idx + k + 2);
     const float4 q4 = *reinterpret_cast<const float4*>(Q + k);
-    const float4 cj4 = *reinterpret_cast<const float4*>(Cj_b + k);
+    // the edge's keyframes whose every confidence passes (gn_cpass_kernel): no reads of them
+    const bool ci_all = cok != nullptr && cok[ii_loc[e]] != 0;
+    const bool cj_all = cok != nullptr && cok[jj_loc[e]] != 0;
+    const float4 cj4 = cj_all ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(Cj_b + k);
     const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
     const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
     const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
@@ -700,7 +717,8 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
 #pragma unroll
     for (int s = 0; s < 4; s++) {
         const int ind = match_index(ids[s], vm[s], HW);
-        const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (cjs[s] > P.C_thresh);
+        const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (ci_all || Ci_b[ind] > P.C_thresh) &&
+                        (cj_all || cjs[s] > P.C_thresh);
         code[s] = pack_code(ind, ok, P);
         sqb[s] = __float_as_int(vsqrt(qs[s]));
     }
@@ -1036,7 +1054,7 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
 }
 
 hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
-                       const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P,
+                       const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P, int* cok,
                        int4* pack, float* px, int* pcnt, float* Zs, const int* flags) {
     if (E_local > 0 && px) {
         const dim3 grid((unsigned)P.nchunks, (unsigned)E_local);
@@ -1051,9 +1069,13 @@ hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, i
             hipLaunchKernelGGL(gn_pack_compact_kernel<GN_POINTS>, grid, dim3(kAccThreads), 0, st, Xs, Cs, ii_loc,
                                jj_loc, es, P, pk, px, pcnt, flags);
     } else if (E_local > 0) {
+        if (cok != nullptr && N > 0) {  // per keyframe: do all its confidences pass C_thresh?
+            const int bx = (int)std::max<int64_t>(1, std::min<int64_t>((P.HW + 1023) / 1024, 8192 / std::max<int64_t>(N, 1)));
+            hipLaunchKernelGGL(gn_cpass_kernel, dim3(bx, (unsigned)N), dim3(256), 0, st, Cs, P, cok, flags);
+        }
         const dim3 grid((unsigned)((P.HW / 4 + kAccThreads - 1) / kAccThreads), (unsigned)E_local);
         hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, es,
-                           P, pack, flags);
+                           P, cok, pack, flags);
     }
     if (Zs) {
         const int64_t total = N * (int64_t)P.HW;

@@ -211,7 +211,7 @@ int chunk_points(int64_t HW, int nchunks) {
 
 struct Layout {
     size_t partials, edgeblk, compact, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent, blk_ref, grad_ptr,
-        grad_ent, ecnt, sched, pack, packx, pcnt, zs, total;
+        grad_ent, ecnt, cok, sched, pack, packx, pcnt, zs, total;
     int nchunks, npad, nblk_max;
 };
 
@@ -252,6 +252,7 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
     L.ecnt = take(sizeof(int) * (size_t)E_local);  // fused edge reduce: finished chunks per edge
+    L.cok = take(sizeof(int) * (size_t)std::max<int64_t>(N, 1));  // per keyframe: every c > C_thresh
     L.sched = take(sizeof(int) * 4 * (size_t)E_local * L.nchunks);  // {edge, chunk, ix, jx} per task
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
@@ -993,6 +994,7 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     put(L.grad_ptr, p.grad_ptr);
     put(L.grad_ent, p.grad_ent);
     std::memset(h + (L.ecnt - lo), 0, sizeof(int) * (size_t)a.E_local);  // (the kernel re-zeroes them)
+    std::memset(h + (L.cok - lo), 1, sizeof(int) * (size_t)std::max<int64_t>(a.N, 1));  // gn_cpass_kernel clears
     M3S_HIP_CHECK(stagings().ws.upload(c.ws + lo, h, L.sched - lo, c.st));
     if (early_pack) {
         rc = prepare_iterations(a, c);
@@ -1025,7 +1027,7 @@ int prepare_iterations(const m3s_gn_args& a, Ctx& c) {
     if (!c.packed) return M3S_OK;
     const Layout& L = c.L;
     M3S_HIP_CHECK(launch_pack(a.mode, c.st, (int)a.E_local, a.Xs, a.N, a.Cs, c.at<int>(L.ii_loc),
-                              c.at<int>(L.jj_loc), c.es, c.P, c.at<int4>(L.pack),
+                              c.at<int>(L.jj_loc), c.es, c.P, c.at<int>(L.cok), c.at<int4>(L.pack),
                               c.compact ? c.at<float>(L.packx) : nullptr, c.at<int>(L.pcnt),
                               a.mode == M3S_GN_CALIB ? c.at<float>(L.zs) : nullptr,
                               c.at<int>(L.flags)));

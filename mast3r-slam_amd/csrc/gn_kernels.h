@@ -102,7 +102,7 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
 // px == nullptr: the positional packed stream (8 B per point-edge); else the compacted one
 // (live points only: records in pack, Xj copies in px, per-(edge, chunk) counts in pcnt)
 hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
-                       const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P,
+                       const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P, int* cok,
                        int4* pack, float* px, int* pcnt, float* Zs, const int* flags);
 hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
                                const float* Xs, const float* Zs, const int* ii_loc,

@@ -253,6 +253,33 @@ def test_packed_stream_gives_identical_system(backend, monkeypatch, mode):
 
 
 @pytest.mark.parametrize("mode", ["rays", "calib", "points"])
+def test_confidence_pass_skips_only_passing_keyframes(backend, monkeypatch, mode):
+    """The pack skips the Cj reads / Ci gathers of an edge whose two keyframes have every
+    confidence above C_thresh (gn_cpass_kernel, one pass over N x HW): with C_thresh = 1.5,
+    keyframes that pass wholly, keyframes with some confidences at or below it, and one with a
+    NaN confidence (which fails c > C_thresh like the reference), the packed system is bitwise
+    the direct path's, which tests every point."""
+    from m3s.debug import build_system_gpu
+
+    g = _graph(mode, N=6, E=8)
+    Lc = dict(LOCAL, C_conf=1.5)
+    Cs = g.Cs.clone()
+    Cs[0] = Cs[0].clamp(min=1.6)          # passes wholly
+    Cs[1] = Cs[1].clamp(min=1.6)
+    Cs[2, 5:40] = 1.5                     # at the threshold: fails (strict >)
+    Cs[3] = Cs[3].clamp(min=1.6)
+    Cs[3, 17] = float("nan")              # fails
+    Cs[4, ::7] = 0.5
+    g.Cs = Cs.contiguous()
+    monkeypatch.setenv("M3S_GN_PACK", "0")
+    H0, b0 = build_system_gpu(g, mode, Lc)
+    monkeypatch.setenv("M3S_GN_PACK", "2")
+    monkeypatch.setenv("M3S_GN_COMPACT", "0")
+    H2, b2 = build_system_gpu(g, mode, Lc)
+    assert np.array_equal(H0, H2, equal_nan=True) and np.array_equal(b0, b2, equal_nan=True)
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib", "points"])
 def test_compacted_stream_keeps_nan_poisoning_and_empty_edges(backend, oracle, monkeypatch, mode):
     """Dead-point compaction (gn_pack_compact_kernel) drops a point only when its validity fails
     AND its own and its matched point are finite (then its contribution is exactly 0): a NaN
