@@ -200,24 +200,42 @@ __device__ __forceinline__ void panel_factor(double* A, double* Li, int c0, int*
     }
 }
 
-// A[I-block rows][J-block cols] -= P_I P_J^T with the panel at columns c0 .. c0+7 (MFMA, two
-// K = 4 steps); only trailing lower entries (row >= col >= c0 + 8) are written back.
-__device__ __forceinline__ void trail_block(double* A, int c0, int I, int J) {
+// A[I-block rows][J-block cols] -= P_I P_J^T with the panel at columns c0 .. c0+7; only trailing
+// lower entries (row >= col >= c0 + 8) are written back.
+// NB trailing blocks (I[k], J[k]) at once, the blocks with on[k] written back: the two K = 4
+// MFMAs of a block go to separate accumulators and every block's MFMAs are issued before any
+// result is read, so a step costs one MFMA latency (~0.2 us for f64), not one per block and
+// pass (trail_block one block after the other: ~0.2 us per block on the panel chain).
+template <int NB>
+__device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[NB], const int (&J)[NB],
+                                             const bool (&on)[NB]) {
     const int lane = threadIdx.x & 63;
     const int r16 = lane & 15, kq = lane >> 4;
     const int lo = c0 + 8;
-    d4 c;
+    d4 c[NB], d[NB];
+    double a0[NB], a1[NB], b0[NB], b1[NB];
 #pragma unroll
-    for (int e = 0; e < 4; e++) c[e] = A[(16 * I + kq + 4 * e) * LD + 16 * J + r16];
-    const double a0 = -A[(16 * I + r16) * LD + c0 + kq], a1 = -A[(16 * I + r16) * LD + c0 + 4 + kq];
-    const double b0 = A[(16 * J + r16) * LD + c0 + kq], b1 = A[(16 * J + r16) * LD + c0 + 4 + kq];
-    c = mfma(a0, b0, c);
-    c = mfma(a1, b1, c);
-    const int col = 16 * J + r16;
+    for (int k = 0; k < NB; k++) {
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
-        const int row = 16 * I + kq + 4 * e;
-        if (col >= lo && col <= row) A[row * LD + col] = c[e];
+        for (int e = 0; e < 4; e++) c[k][e] = A[(16 * I[k] + kq + 4 * e) * LD + 16 * J[k] + r16];
+        a0[k] = -A[(16 * I[k] + r16) * LD + c0 + kq];
+        a1[k] = -A[(16 * I[k] + r16) * LD + c0 + 4 + kq];
+        b0[k] = A[(16 * J[k] + r16) * LD + c0 + kq];
+        b1[k] = A[(16 * J[k] + r16) * LD + c0 + 4 + kq];
+    }
+#pragma unroll
+    for (int k = 0; k < NB; k++) c[k] = mfma(a0[k], b0[k], c[k]);
+#pragma unroll
+    for (int k = 0; k < NB; k++) d[k] = mfma(a1[k], b1[k], d4{0.0, 0.0, 0.0, 0.0});
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        if (!on[k]) continue;
+        const int col = 16 * J[k] + r16;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int row = 16 * I[k] + kq + 4 * e;
+            if (col >= lo && col <= row) A[row * LD + col] = c[k][e] + d[k][e];
+        }
     }
 }
 
@@ -243,13 +261,16 @@ __device__ void potrf_inverse(double* A, double* Li, double* Tm, int* flags, lon
         const int c0 = 8 * s;
         const int J1 = (c0 + 8) >> 4;  // block column holding panel s+1
         if (w == 0) {
-#pragma unroll
-            for (int I = 0; I < 4; I++)
-                if (I >= J1) trail_block(A, c0, I, J1);
+            const int I[4] = {0, 1, 2, 3}, J[4] = {J1, J1, J1, J1};
+            const bool on[4] = {0 >= J1, 1 >= J1, 2 >= J1, 3 >= J1};
+            trail_blocks<4>(A, c0, I, J, on);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS writes before the reads
             panel_factor(A, Li, c0 + 8, flags);
         } else {
-            for (int J = J1 + 1; J <= w; J++) trail_block(A, c0, w, J);
+            const int I[3] = {w, w, w};
+            const int J[3] = {min(J1 + 1, 3), min(J1 + 2, 3), min(J1 + 3, 3)};
+            const bool on[3] = {J1 + 1 <= w, J1 + 2 <= w, J1 + 3 <= w};
+            if (on[0]) trail_blocks<3>(A, c0, I, J, on);
         }
         __syncthreads();
         pstamp(2 + s);
