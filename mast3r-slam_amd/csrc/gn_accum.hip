@@ -678,8 +678,17 @@ __global__ __launch_bounds__(256) void gn_cpass_kernel(const float* __restrict__
     if (flags[kFlagDone]) return;
     const int n = blockIdx.y;
     const float* __restrict__ C = Cs + (int64_t)n * P.HW;
+    const float t = P.C_thresh;
     bool ok = true;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < P.HW; k += gridDim.x * 256) ok = ok && (C[k] > P.C_thresh);
+    if ((P.HW & 3) == 0) {  // 16-B loads (every keyframe row is 16-B aligned)
+        const float4* __restrict__ C4 = reinterpret_cast<const float4*>(C);
+        for (int k = blockIdx.x * 256 + threadIdx.x; k < (P.HW >> 2); k += gridDim.x * 256) {
+            const float4 c = C4[k];
+            ok = ok & (c.x > t) & (c.y > t) & (c.z > t) & (c.w > t);
+        }
+    } else {
+        for (int k = blockIdx.x * 256 + threadIdx.x; k < P.HW; k += gridDim.x * 256) ok = ok & (C[k] > t);
+    }
     if (!__all(ok) && (threadIdx.x & 63) == 0) cok[n] = 0;  // benign race: every writer stores 0
 }
 
