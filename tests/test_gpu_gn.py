@@ -175,7 +175,8 @@ def test_full_size_cfg2_matches_oracle(backend, oracle):
 
 
 @pytest.mark.parametrize("solver", ["1", "2", "3"])
-@pytest.mark.parametrize("topo", ["cfg3", "cfg4", "chain", "star", "clique", "clique27", "clique28"])
+@pytest.mark.parametrize("topo", ["cfg3", "cfg4", "chain", "star", "clique", "clique27", "clique28",
+                                  "clique4", "clique8", "clique17", "clique21"])
 def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, solver):
     """The block-sparse solvers against the dense blocked Cholesky (M3S_SOLVER_DENSE=1) on the
     same system: one GN step, f64 solves of the same matrix in different orders -> updates
@@ -186,7 +187,8 @@ def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, sol
     cover the BASELINE graphs, a chain (everything eliminated in rounds), a star around the
     pinned pose (poses without fronts) and cliques (no independent low-degree set: dense tail
     only; 27 non-pinned poses = the largest in-register tail, 189 unknowns in 12 x 12 tiles of
-    16x16; 28 = beyond it)."""
+    16x16; 28 = beyond it; 3 / 7 / 11 / 16 / 20 poses: tails of 2 / 4 / 6 / 8 / 10 tile rows, so
+    every instantiated tile map -- dealt to the waves by MFMA work -- is exercised)."""
     if topo == "chain":
         N = 24
         und = [(k - 1, k) for k in range(1, N)]
@@ -194,7 +196,8 @@ def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, sol
         N = 6
         und = [(0, k) for k in range(1, N)]
     elif topo.startswith("clique"):
-        N = {"clique": 12, "clique27": 28, "clique28": 29}[topo]
+        N = {"clique": 12, "clique27": 28, "clique28": 29, "clique4": 4, "clique8": 8, "clique17": 17,
+             "clique21": 21}[topo]
         und = [(a, b) for a in range(N) for b in range(a + 1, N)]
     if topo in ("chain", "star") or topo.startswith("clique"):
         g = synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
