@@ -515,6 +515,13 @@ RoundPolicy hybrid_policy() {
 
 void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparsePlan& sp) {
     sp = SparsePlan();
+    {  // capacities from the pose graph's size: no reallocation while the lists grow
+        const size_t e = p.pairs.size() + (size_t)npose, big = 16 * e + 1024;
+        for (std::vector<int>* v : {&sp.tg, &sp.tc, &sp.tc3, &sp.rtg, &sp.rc, &sp.rc4, &sp.inl, &sp.fronts})
+            v->reserve(big);
+        sp.nodes.reserve(npose);
+        sp.fptr.reserve(npose + 1);
+    }
     const int dcap = pol.dcap, rmin = pol.rmin, rmax = pol.rmax, tailcap = pol.tailcap, kmin = pol.kmin;
     // adjacency as bitsets (one row of nw 64-bit words per pose), degrees, dense block ids
     const int nw = (npose + 63) / 64;
@@ -1306,19 +1313,39 @@ int run(const m3s_gn_args& a) {
         // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
         // single-workgroup solve when its plan needs few rounds, else multi-launch
         const int choice = env_int("M3S_SOLVER", 0);
-        build_sparse_plan(c.plan, npose, fused_policy(), c.sp);
+        const int max_fused_rounds = env_int("M3S_FUSED_MAX_ROUNDS", 3);
+        const bool hybrid_on = env_int("M3S_HYBRID", 1) != 0;
+        // Default choice: the hybrid plan first.  The fused policy is the hybrid's plus a cap on
+        // the poses per round (LDS staging), so it never needs fewer rounds; when the hybrid
+        // plan already needs more than max_fused_rounds, the fused solve would be rejected and
+        // building its plan (~0.23 ms of host time on cfg3, exposed once the per-call pack is
+        // short, e.g. edge-sharded over several GPUs) is skipped.
+        bool planned = false;
+        if (choice == 0 && hybrid_on) {
+            build_sparse_plan(c.plan, npose, hybrid_policy(), c.sp);
+            if ((int)c.sp.rounds.size() > max_fused_rounds) {
+                const bool hyb = c.sp.fused_tail && npose <= solve_max_poses() &&
+                                 solve_lds_bytes((int)c.sp.nints_back) <= (size_t)kSolveMaxLds;
+                if (!hyb) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
+                c.sp.hybrid = hyb;
+                planned = true;
+            }
+        }
         t2a = now();
-        const bool meta_fits = solve_lds_bytes((int)c.sp.nints) <= (size_t)kSolveMaxLds;
-        const bool fused_ok = c.sp.fused && meta_fits && npose <= solve_max_poses() &&
-                              (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <=
-                                                                   env_int("M3S_FUSED_MAX_ROUNDS", 3)));
-        if (env_int("M3S_SOLVE_DEBUG", 0) && !fused_ok)
+        bool fused_ok = false, meta_fits = false;
+        if (!planned) {
+            build_sparse_plan(c.plan, npose, fused_policy(), c.sp);
+            meta_fits = solve_lds_bytes((int)c.sp.nints) <= (size_t)kSolveMaxLds;
+            fused_ok = c.sp.fused && meta_fits && npose <= solve_max_poses() &&
+                       (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <= max_fused_rounds));
+        }
+        if (env_int("M3S_SOLVE_DEBUG", 0) && !fused_ok && !planned)
             fprintf(stderr, "fused solve rejected: fused_tail %d (ntail %d) rounds %zu nints %zu meta_fits %d\n",
                     (int)c.sp.fused, c.sp.ntail, c.sp.rounds.size(), c.sp.nints, (int)meta_fits);
-        if (!fused_ok) {
+        if (!fused_ok && !planned) {
             // M3S_SOLVER=3 / default: multi-launch rounds + the in-register core when it fits
             bool hyb = false;
-            if (choice == 3 || (choice == 0 && env_int("M3S_HYBRID", 1) != 0)) {
+            if (choice == 3 || (choice == 0 && hybrid_on)) {
                 build_sparse_plan(c.plan, npose, hybrid_policy(), c.sp);
                 hyb = c.sp.fused_tail && npose <= solve_max_poses() &&
                       solve_lds_bytes((int)c.sp.nints_back) <= (size_t)kSolveMaxLds;
@@ -1335,7 +1362,7 @@ int run(const m3s_gn_args& a) {
         t3 = now();
     }
     if (prof_host)
-        fprintf(stderr, "gn host: setup %.0f us, fused plan %.0f us, other plan %.0f us, upload %.0f us\n",
+        fprintf(stderr, "gn host: setup %.0f us, first plan %.0f us, second plan %.0f us, upload %.0f us\n",
                 us(t0, t1), us(t1, t2a), us(t2a, t2), us(t2, t3));
     for (int itr = 0; itr < a.max_iter; itr++) {
         g_prof.mark(c.st);
