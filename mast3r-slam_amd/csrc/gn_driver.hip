@@ -842,6 +842,7 @@ struct Ctx {
     bool compact = false;  // ... holding only the live points (gn_pack_compact_kernel)
     bool ref_order = false;  // M3S_GN_ORDER_REFERENCE: gn_refacc.hip accumulate + assembly
     bool pack_issued = false;  // prepare_iterations already enqueued (setup's early pack)
+    bool acc_enqueued = false;  // iteration 0's accumulate enqueued before the planning
     RefParams R;
     Layout L;
     Plan plan;
@@ -1041,6 +1042,9 @@ int prepare_iterations(const m3s_gn_args& a, Ctx& c) {
     return M3S_OK;
 }
 
+int enqueue_accumulate(const m3s_gn_args& a, Ctx& c);
+int enqueue_assembly(const m3s_gn_args& a, Ctx& c);
+
 // accumulate + edge reduce + compact (+ all-reduce): the system of one iteration
 int enqueue_system(const m3s_gn_args& a, Ctx& c) {
     const Layout& L = c.L;
@@ -1068,6 +1072,19 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
         }
         return M3S_OK;
     }
+    if (!c.acc_enqueued) {
+        int rc = enqueue_accumulate(a, c);
+        if (rc) return rc;
+    }
+    c.acc_enqueued = false;
+    return enqueue_assembly(a, c);
+}
+
+// the accumulate (+ edge reduce) of one iteration: needs no elimination plan, so iteration 0's
+// is enqueued before the host builds it
+int enqueue_accumulate(const m3s_gn_args& a, Ctx& c) {
+    const Layout& L = c.L;
+    int* flags = c.at<int>(L.flags);
     if (a.E_local > 0) {
         g_prof.mark(c.st, true);
         const dim3 grid((unsigned)(L.nchunks * a.E_local));
@@ -1093,6 +1110,13 @@ int enqueue_system(const m3s_gn_args& a, Ctx& c) {
             M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
                                              a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
     }
+    return M3S_OK;
+}
+
+// edge blocks -> the solver's system (+ the all-reduce)
+int enqueue_assembly(const m3s_gn_args& a, Ctx& c) {
+    const Layout& L = c.L;
+    int* flags = c.at<int>(L.flags);
     const int npose = (int)(a.N - 1);
     if (c.sp.enabled) {
         // block format for the sparse solves, in the solver's buffer
@@ -1309,6 +1333,15 @@ int run(const m3s_gn_args& a) {
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
     std::chrono::steady_clock::time_point t2 = t1, t2a = t1, t3 = t1;
+    // M3S_EARLY_ACC (default 1): iteration 0's accumulate is enqueued before the host builds the
+    // elimination plan (the GPU works while the host plans; the per-call pack alone no longer
+    // covers the planning once the edges are sharded over several GPUs)
+    if (!c.ref_order && a.max_iter > 0 && env_int("M3S_EARLY_ACC", 1) != 0) {
+        g_prof.mark(c.st);
+        rc = enqueue_accumulate(a, c);
+        if (rc) return rc;
+        c.acc_enqueued = true;
+    }
     if (env_int("M3S_SOLVER_DENSE", 0) == 0 || c.ref_order) {
         // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
         // single-workgroup solve when its plan needs few rounds, else multi-launch
@@ -1365,7 +1398,7 @@ int run(const m3s_gn_args& a) {
         fprintf(stderr, "gn host: setup %.0f us, first plan %.0f us, second plan %.0f us, upload %.0f us\n",
                 us(t0, t1), us(t1, t2a), us(t2a, t2), us(t2, t3));
     for (int itr = 0; itr < a.max_iter; itr++) {
-        g_prof.mark(c.st);
+        if (!c.acc_enqueued) g_prof.mark(c.st);  // (iteration 0's mark preceded its early accumulate)
         rc = enqueue_system(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
