@@ -1291,10 +1291,12 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         // retraction: one single-workgroup launch (gn_solve.hip) reading the plan prefix; the
         // core is first laid out densely by a many-workgroup fill (one CU gathering it block by
         // block took ~28 us) -- inside the cooperative launch, or its own launch
-        if (!coop)
+        // M3S_SOLVE_GATHER=1 (A/B): no fill launch, the core gathers its tiles from the blocks
+        static const bool gather = env_int("M3S_SOLVE_GATHER", 0) != 0;
+        if (!coop && !gather)
             M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail),
                                               sp.ntail, sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
-        S.Hd = sp.ntail > 0 ? sp.dptr<double>(sp.o_dense) : nullptr;
+        S.Hd = sp.ntail > 0 && !gather ? sp.dptr<double>(sp.o_dense) : nullptr;
         S.npad_h = sp.npad_tail;
         S.nmeta = (int)sp.nints_back;
         S.meta_lds = 1;
