@@ -23,18 +23,18 @@
 //             deterministic), b_r -= sum_v W_rv y_v.  barrier.
 //   tail      the remaining dense core (<= 27 poses, 189 unknowns) lives in REGISTERS as 16x16
 //             f64 tiles of the lower triangle.  The tile map is a compile-time function of the
-//             tail's tile count T: slot s holds tile (I0_s + wave, J_s), i.e. each tile column
-//             is cut into groups of 4 consecutive tiles, one per wave.  Factored right-looking
-//             one pose (7 columns) at a time, two barriers per pose:
-//               A: every wave with panel rows factors the 7x7 diagonal block in registers (from
-//                  LDS broadcasts) and solves y_K = L^-1 z_K; each thread turns one panel row
-//                  into a row of L (forward substitution) and updates its RHS entry; wave 0
-//                  stores L_KK^-1 for the back-substitution | barrier |
-//               B: rank-7 update of the live tiles, two v_mfma_f64_16x16x4_f64 each (operand
-//                  loads of 4 slots ahead of their MFMAs); the owners of the next 7 columns
-//                  extract them to LDS | barrier.
+//             tail's tile count T: tiles are dealt to the 4 waves by their MFMA work (a tile of
+//             column J is updated ~(16 J + 9) / 7 times), each wave's slots sorted by J.
+//             Factored right-looking one pose (7 columns) at a time, two barriers per pose:
+//               A: every thread factors the 7x7 diagonal block in registers (from LDS
+//                  broadcasts) and solves y_K = L^-1 z_K; each thread turns one panel row into a
+//                  row of L (forward substitution) and updates its RHS entry; 7 threads produce
+//                  the columns of L_KK^-1 for the back-substitution | barrier |
+//               B: rank-7 update of the live tiles, two v_mfma_f64_16x16x4_f64 each; the one or
+//                  two tile columns holding the next pose are written whole (branch-free) into
+//                  an LDS strip | barrier.
 //             Back-substitution right-looking (x_K = L_KK^-T z_K as a matvec), one barrier
-//             per pose, the L entries of the next pose prefetched.
+//             per pose, the L entries prefetched three poses ahead.
 //   back      the rounds in reverse: x_v = L^-T (y_v - sum_r W_rv^T x_r), 7 lanes per pose;
 //             a round of <= 18 poses (the late, dense ones) splits each pose's fronts over
 //             36 / nn groups whose partials meet in LDS (one round trip instead of ~6).
