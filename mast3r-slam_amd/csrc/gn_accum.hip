@@ -891,14 +891,30 @@ __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__
     if (!ray) flags[kFlagNotRay] = 1;  // benign race: every writer stores 1
 }
 
+// The reference's per-point inputs of one directed edge, for the first iteration's accumulate
+// that builds the packed records itself (gn_accum_packed_kernel<..., FIRST>).
+struct RawSrc {
+    const int64_t* idx;
+    const uint8_t* valid;
+    const float* Q;
+    const float* Ci_b;
+    const float* Cj_b;
+    int4* pk_w;          // the edge's packed records, written for the later iterations
+    bool ci_all, cj_all;  // every confidence of keyframe i / j passes (gn_cpass_kernel)
+};
+
 // One lane's steps of the packed accumulate (NP points per step); the records of the next step
 // are loaded one step ahead.  RC: Xj_b is keyframe j's depth row and x, y come from the ray
-// tables that follow Zs (total = N * HW floats of depth).
-template <int MODE, bool RC, int NP = 4>
+// tables that follow Zs (total = N * HW floats of depth).  FIRST (NP = 4): the records are built
+// from the reference's inputs exactly as gn_pack_kernel builds them (and stored for the later
+// iterations) instead of being read: the per-call pack pass is folded into the first iteration.
+template <int MODE, bool RC, int NP = 4, bool FIRST = false>
 __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, const float* __restrict__ Xi_b,
                                             const float* __restrict__ Zi_b, const int4* __restrict__ pk_b,
                                             int k0, int k1, const RelXf& T, const AccParams& P,
-                                            const float* __restrict__ Zs, float* __restrict__ acc) {
+                                            const float* __restrict__ Zs, float* __restrict__ acc,
+                                            const RawSrc& raw = RawSrc{}) {
+    static_assert(!FIRST || NP == 4, "the fused first iteration handles 4 points per step");
     constexpr int S = NP * kAccThreads;
     AccStage<MODE, RC, true, NP> cur;
     cur.width = P.width;
@@ -911,8 +927,34 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
     }
     // the records of NP points: one int4 per two
     auto records = [&](int kk, int4& a, int4& b) {
-        a = pk_b[kk / 2];
-        if constexpr (NP == 4) b = pk_b[kk / 2 + 1];
+        if constexpr (FIRST) {
+            const uchar4 vm4 = *reinterpret_cast<const uchar4*>(raw.valid + kk);
+            const longlong2 id01 = *reinterpret_cast<const longlong2*>(raw.idx + kk);
+            const longlong2 id23 = *reinterpret_cast<const longlong2*>(raw.idx + kk + 2);
+            const float4 q4 = *reinterpret_cast<const float4*>(raw.Q + kk);
+            const float4 cj4 =
+                raw.cj_all ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(raw.Cj_b + kk);
+            const bool vm[4] = {vm4.x != 0, vm4.y != 0, vm4.z != 0, vm4.w != 0};
+            const int64_t ids[4] = {id01.x, id01.y, id23.x, id23.y};
+            const float qs[4] = {q4.x, q4.y, q4.z, q4.w};
+            const float cjs[4] = {cj4.x, cj4.y, cj4.z, cj4.w};
+            int code[4], sqb[4];
+#pragma unroll
+            for (int s = 0; s < 4; s++) {  // gn_pack_kernel's record, operation for operation
+                const int ind = match_index(ids[s], vm[s], P.HW);
+                const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (raw.ci_all || raw.Ci_b[ind] > P.C_thresh) &&
+                                (raw.cj_all || cjs[s] > P.C_thresh);
+                code[s] = pack_code(ind, ok, P);
+                sqb[s] = __float_as_int(vsqrt(qs[s]));
+            }
+            a = int4{code[0], sqb[0], code[1], sqb[1]};
+            b = int4{code[2], sqb[2], code[3], sqb[3]};
+            raw.pk_w[kk / 2] = a;
+            raw.pk_w[kk / 2 + 1] = b;
+        } else {
+            a = pk_b[kk / 2];
+            if constexpr (NP == 4) b = pk_b[kk / 2 + 1];
+        }
     };
     int4 na = int4{0, 0, 0, 0}, nb = int4{0, 0, 0, 0};
     int k = k0 + NP * threadIdx.x;
@@ -959,14 +1001,23 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
 #ifndef M3S_ACC_WAVES
 #define M3S_ACC_WAVES 1
 #endif
-template <int MODE, bool COMPACT, bool RCOK = false>
+// FIRST (calib, the positional stream): the first iteration of a call, building the packed
+// records from the reference's inputs on the way (RawSrc; no separate gn_pack_kernel pass).
+struct FirstSrc {
+    EdgeSrc es;
+    const float* Cs;
+    const int* cok;
+    int4* pack_w;
+};
+
+template <int MODE, bool COMPACT, bool RCOK = false, bool FIRST = false>
 __global__ __launch_bounds__(kAccThreads) __attribute__((amdgpu_waves_per_eu(M3S_ACC_WAVES)))
 void gn_accum_packed_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Zs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int4* __restrict__ pack,
     AccParams P, const int4* __restrict__ sched, float* __restrict__ partials,
     const int* __restrict__ flags, const float* __restrict__ px, const int* __restrict__ pcnt,
-    int* __restrict__ ecnt, double* __restrict__ edgeblk) {
+    int* __restrict__ ecnt, double* __restrict__ edgeblk, FirstSrc fs) {
     const int4 tk = sched[blockIdx.x];  // {edge, chunk, ix, jx}, loaded together with the flag
     if (flags[kFlagDone]) return;
     const int e = tk.x, c = tk.y, ix = tk.z, jx = tk.w;
@@ -1020,6 +1071,18 @@ void gn_accum_packed_kernel(
         const int64_t cb = ((int64_t)e * P.nchunks + c) * P.chunk;
         accum_steps<MODE, false, acc_np<MODE>()>(px + cb * 3, Xi_b, Zi_b, pack + cb / 2, 0, pcnt[(int64_t)e * P.nchunks + c], T, P,
                                  Zs, acc);
+    } else if constexpr (FIRST) {
+        RawSrc raw;
+        fs.es.at(e, HW, raw.idx, raw.valid, raw.Q);
+        raw.Ci_b = fs.Cs + (int64_t)ix * HW;
+        raw.Cj_b = fs.Cs + (int64_t)jx * HW;
+        raw.pk_w = fs.pack_w + ebase / 2;
+        raw.ci_all = fs.cok != nullptr && fs.cok[ix] != 0;
+        raw.cj_all = fs.cok != nullptr && fs.cok[jx] != 0;
+        if (RCOK && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
+            accum_steps<MODE, true, 4, true>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc, raw);
+        else
+            accum_steps<MODE, false, 4, true>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc, raw);
     } else if (RCOK && MODE == GN_CALIB && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
         // calib with ray-constrained keyframe points (gn_depth_kernel's check): Xj from its depth
         accum_steps<MODE, true, acc_np<MODE>()>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
@@ -1064,7 +1127,7 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
 
 hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
                        const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P, int* cok,
-                       int4* pack, float* px, int* pcnt, float* Zs, const int* flags) {
+                       int4* pack, float* px, int* pcnt, float* Zs, const int* flags, bool skip_pack) {
     if (E_local > 0 && px) {
         const dim3 grid((unsigned)P.nchunks, (unsigned)E_local);
         int2* pk = reinterpret_cast<int2*>(pack);
@@ -1083,8 +1146,9 @@ hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, i
             hipLaunchKernelGGL(gn_cpass_kernel, dim3(bx, (unsigned)N), dim3(256), 0, st, Cs, P, cok, flags);
         }
         const dim3 grid((unsigned)((P.HW / 4 + kAccThreads - 1) / kAccThreads), (unsigned)E_local);
-        hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, es,
-                           P, cok, pack, flags);
+        if (!skip_pack)  // (else the first iteration's accumulate builds the records)
+            hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, es,
+                               P, cok, pack, flags);
     }
     if (Zs) {
         const int64_t total = N * (int64_t)P.HW;
@@ -1101,10 +1165,25 @@ hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float*
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,
                                const int4* sched, float* partials, const int* flags, const float* px,
-                               const int* pcnt, int* ecnt, double* edgeblk) {
+                               const int* pcnt, int* ecnt, double* edgeblk, const EdgeSrc* first_es,
+                               const float* Cs, const int* cok) {
+    if (first_es != nullptr) {  // the first iteration builds the records (calib, positional stream)
+        if (mode != GN_CALIB || px != nullptr) return hipErrorInvalidValue;
+        const FirstSrc fs{*first_es, Cs, cok, const_cast<int4*>(pack)};
+        if (P.raycheck)
+            hipLaunchKernelGGL((gn_accum_packed_kernel<GN_CALIB, false, true, true>), grid, dim3(kAccThreads), 0, st,
+                               Twc, Xs, Zs, ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt,
+                               edgeblk, fs);
+        else
+            hipLaunchKernelGGL((gn_accum_packed_kernel<GN_CALIB, false, false, true>), grid, dim3(kAccThreads), 0, st,
+                               Twc, Xs, Zs, ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt,
+                               edgeblk, fs);
+        return hipGetLastError();
+    }
+    const FirstSrc fs0{};
 #define M3S_ACCP(MODE, CP, RC)                                                                       \
     hipLaunchKernelGGL((gn_accum_packed_kernel<MODE, CP, RC>), grid, dim3(kAccThreads), 0, st, Twc, Xs, Zs, \
-                       ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt, edgeblk)
+                       ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt, edgeblk, fs0)
 #define M3S_ACCP2(MODE, CP) M3S_ACCP(MODE, CP, false)
     const bool cp = px != nullptr;
     if (mode == GN_RAYS) {

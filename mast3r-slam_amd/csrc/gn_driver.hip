@@ -843,6 +843,8 @@ struct Ctx {
     bool ref_order = false;  // M3S_GN_ORDER_REFERENCE: gn_refacc.hip accumulate + assembly
     bool pack_issued = false;  // prepare_iterations already enqueued (setup's early pack)
     bool acc_enqueued = false;  // iteration 0's accumulate enqueued before the planning
+    // the first accumulate of the call builds the packed records (no separate pack pass)
+    bool first_pack = false;
     RefParams R;
     Layout L;
     Plan plan;
@@ -1004,6 +1006,12 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     std::memset(h + (L.ecnt - lo), 0, sizeof(int) * (size_t)a.E_local);  // (the kernel re-zeroes them)
     std::memset(h + (L.cok - lo), 1, sizeof(int) * (size_t)std::max<int64_t>(a.N, 1));  // gn_cpass_kernel clears
     M3S_HIP_CHECK(stagings().ws.upload(c.ws + lo, h, L.sched - lo, c.st));
+    // M3S_GN_PACK_FIRST (default 1): a calib call's first accumulate builds the packed records
+    // from the reference's inputs itself (gn_accum_packed_kernel<..., FIRST>): 13 B read + 8 B
+    // written per point-edge inside the first iteration instead of a separate 21-B pack pass
+    // followed by the first iteration's 8-B record reads (run() only: its early pack)
+    c.first_pack = early_pack && c.packed && !c.compact && !c.ref_order && a.mode == M3S_GN_CALIB &&
+                   a.max_iter > 0 && env_int("M3S_GN_PACK_FIRST", 1) != 0;
     if (early_pack) {
         rc = prepare_iterations(a, c);
         if (rc) return rc;
@@ -1038,7 +1046,7 @@ int prepare_iterations(const m3s_gn_args& a, Ctx& c) {
                               c.at<int>(L.jj_loc), c.es, c.P, c.at<int>(L.cok), c.at<int4>(L.pack),
                               c.compact ? c.at<float>(L.packx) : nullptr, c.at<int>(L.pcnt),
                               a.mode == M3S_GN_CALIB ? c.at<float>(L.zs) : nullptr,
-                              c.at<int>(L.flags)));
+                              c.at<int>(L.flags), c.first_pack));
     return M3S_OK;
 }
 
@@ -1092,15 +1100,17 @@ int enqueue_accumulate(const m3s_gn_args& a, Ctx& c) {
         // the edge reduce (no separate launch); 0: gn_edge_reduce_kernel
         const bool fuse_reduce = env_int("M3S_GN_FUSE_REDUCE", 1) != 0;
         const bool fused = c.packed && fuse_reduce;
-        if (c.packed)
+        if (c.packed) {
             M3S_HIP_CHECK(launch_accum_packed(a.mode, grid, c.st, a.Twc, a.Xs, c.at<float>(L.zs),
                                               c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
                                               c.at<int4>(L.pack), c.P, c.at<int4>(L.sched),
                                               c.at<float>(L.partials), flags,
                                               c.compact ? c.at<float>(L.packx) : nullptr,
                                               c.at<int>(L.pcnt), fused ? c.at<int>(L.ecnt) : nullptr,
-                                              c.at<double>(L.edgeblk)));
-        else
+                                              c.at<double>(L.edgeblk), c.first_pack ? &c.es : nullptr,
+                                              a.Cs, c.at<int>(L.cok)));
+            c.first_pack = false;  // the records exist from here on
+        } else
             M3S_HIP_CHECK(launch_accum(a.mode, c.vec, grid, c.st, a.Twc, a.Xs, a.Cs,
                                        c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), c.es, c.P,
                                        c.at<int4>(L.sched), c.at<float>(L.partials),

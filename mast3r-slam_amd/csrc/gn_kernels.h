@@ -103,12 +103,14 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
 // (live points only: records in pack, Xj copies in px, per-(edge, chunk) counts in pcnt)
 hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
                        const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P, int* cok,
-                       int4* pack, float* px, int* pcnt, float* Zs, const int* flags);
+                       int4* pack, float* px, int* pcnt, float* Zs, const int* flags, bool skip_pack = false);
 hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,
                                const int4* sched, float* partials, const int* flags, const float* px,
-                               const int* pcnt, int* ecnt = nullptr, double* edgeblk = nullptr);
+                               const int* pcnt, int* ecnt = nullptr, double* edgeblk = nullptr,
+                               const EdgeSrc* first_es = nullptr, const float* Cs = nullptr,
+                               const int* cok = nullptr);
 hipError_t launch_edge_reduce(int E_local, hipStream_t st, const float* partials, int nchunks,
                               const float* Twc, const int* ii_loc, double* edgeblk,
                               const int* flags);

@@ -282,6 +282,39 @@ def test_confidence_pass_skips_only_passing_keyframes(backend, monkeypatch, mode
     assert np.array_equal(H0, H2, equal_nan=True) and np.array_equal(b0, b2, equal_nan=True)
 
 
+@pytest.mark.parametrize("ray_constrained", [True, False])
+def test_first_iteration_builds_the_packed_records(backend, monkeypatch, ray_constrained):
+    """A calib call's first accumulate builds the packed records from the reference's inputs
+    (M3S_GN_PACK_FIRST=1, default) instead of a separate pack pass: the same records, so the
+    poses and dx after 3 iterations are bitwise those of the separate pass -- with confidences
+    at / below C_thresh, a NaN confidence, Q below Q_thresh and unmatched points; both the
+    ray-constrained (depth-only Xj) and the positional stream."""
+    g = _graph("calib", N=6, E=8)
+    if not ray_constrained:
+        g.Xs = (g.Xs * 1.0001).contiguous()  # off the rays: the positional stream
+    Cs = g.Cs.clone()
+    Cs[0] = Cs[0].clamp(min=1.6)
+    Cs[2, 5:40] = 1.5
+    Cs[3, 17] = float("nan")
+    g.Cs = Cs.contiguous()
+    g.Q[0, :50] = 1.0
+    g.valid[1, 10:90] = False
+    Lc = dict(LOCAL, C_conf=1.5)
+    out = []
+    for first in ("0", "1"):
+        monkeypatch.setenv("M3S_GN_PACK_FIRST", first)
+        Twc = g.Twc.clone().cuda()
+        c = lambda t: t.cuda()
+        (dx,) = backend.gauss_newton_calib(Twc, c(g.Xs), c(g.Cs), c(g.K), c(g.ii), c(g.jj), c(g.idx),
+                                           c(g.valid), c(g.Q), g.H, g.W, Lc["pixel_border"],
+                                           Lc["depth_eps"], Lc["sigma_pixel"], Lc["sigma_depth"],
+                                           Lc["C_conf"], Lc["Q_conf"], 3, 0.0)
+        torch.cuda.synchronize()
+        out.append((Twc.cpu().numpy(), dx.cpu().numpy()))
+    assert np.isfinite(out[1][0]).all()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1], equal_nan=True)
+
+
 @pytest.mark.parametrize("mode", ["rays", "calib", "points"])
 def test_compacted_stream_keeps_nan_poisoning_and_empty_edges(backend, oracle, monkeypatch, mode):
     """Dead-point compaction (gn_pack_compact_kernel) drops a point only when its validity fails
