@@ -194,6 +194,9 @@ def main():
     value = pair_iters / elapsed
     n_it = max(nprof.value, 1)
     acc_ms = prof[0] / n_it if acc_events else ph[0] / n_ph
+    # a calib call's first accumulate builds the packed records itself (M3S_GN_PACK_FIRST):
+    # another kernel, timed apart from the iteration kernel the roofline prices
+    first_ms = prof[1] / prof[2] if acc_events and prof[2] > 0 else None
     packed = iters >= 3 and os.environ.get("M3S_GN_PACK", "1") != "0"
     bpe = (RAY_BYTES_PER_POINT_EDGE if ray_path else PACKED_BYTES_PER_POINT_EDGE[mode]) if packed \
         else REF_BYTES_PER_POINT_EDGE
@@ -258,6 +261,8 @@ def main():
             "avg_launch_ms": acc_ms,
             "ref_formulation_bytes_per_launch": ref_bytes_launch,
             "ref_formulation_equiv_GBps": ref_bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None,
+            "launches_per_step": n_it / args.steps,
+            "first_accumulate_with_pack_ms": first_ms,
         },
         "cpu_baseline": None,
     }

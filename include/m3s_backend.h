@@ -246,7 +246,9 @@ int m3s_gn_edge_hessians(const m3s_gn_args* args, float* Hs_host, float* gs_host
  */
 int m3s_prof_begin(void);
 /* The same, recording only the two events around each accumulate launch (every timed event
- * record idles the GPU ~5 us): m3s_prof_end then fills out[0] and *n_iter, out[1..3] = 0. */
+ * record idles the GPU ~5 us): m3s_prof_end then fills out[0] and *n_iter with the iteration
+ * kernel's launches, out[1] / out[2] with the ms and count of the launches that also built the
+ * packed records (a calib call's first accumulate, M3S_GN_PACK_FIRST), out[3] = 0. */
 int m3s_prof_begin_accum(void);
 int m3s_prof_end(double* out /* [4] */, int* n_iter);
 

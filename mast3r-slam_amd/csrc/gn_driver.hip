@@ -53,10 +53,14 @@ struct Prof {
     bool accum_only = false;  // record only the two events bracketing the accumulate kernel
     // (every timed event record is a queue marker with a release to system scope: ~5 us of idle
     // GPU each, so the timed bench region carries only the accumulate pair)
-    void mark(hipStream_t st, bool accum = false) {
+    std::vector<char> first;  // accum_only: per event pair, the launch built the packed records
+    void mark(hipStream_t st, bool accum = false, bool first_pack = false) {
         if (!on || (accum_only && !accum)) return;
         hipEvent_t e = get();
-        if (e && hipEventRecord(e, st) == hipSuccess) marks.push_back(e);
+        if (e && hipEventRecord(e, st) == hipSuccess) {
+            marks.push_back(e);
+            if (accum_only && marks.size() % 2 == 0) first.push_back(first_pack);
+        }
     }
 };
 Prof g_prof;
@@ -1100,6 +1104,7 @@ int enqueue_accumulate(const m3s_gn_args& a, Ctx& c) {
         // the edge reduce (no separate launch); 0: gn_edge_reduce_kernel
         const bool fuse_reduce = env_int("M3S_GN_FUSE_REDUCE", 1) != 0;
         const bool fused = c.packed && fuse_reduce;
+        const bool was_first = c.packed && c.first_pack;
         if (c.packed) {
             M3S_HIP_CHECK(launch_accum_packed(a.mode, grid, c.st, a.Twc, a.Xs, c.at<float>(L.zs),
                                               c.at<int>(L.ii_loc), c.at<int>(L.jj_loc),
@@ -1115,7 +1120,7 @@ int enqueue_accumulate(const m3s_gn_args& a, Ctx& c) {
                                        c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), c.es, c.P,
                                        c.at<int4>(L.sched), c.at<float>(L.partials),
                                        flags));
-        g_prof.mark(c.st, true);
+        g_prof.mark(c.st, true, was_first);
         if (!fused)
             M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
                                              a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
@@ -1678,6 +1683,7 @@ extern "C" int m3s_gauss_newton_calib(float* Twc, const float* Xs, const float* 
 extern "C" int m3s_prof_begin(void) {
     for (hipEvent_t e : g_prof.marks) g_prof.pool.push_back(e);
     g_prof.marks.clear();
+    g_prof.first.clear();
     g_prof.accum_only = false;
     g_prof.on = true;
     return M3S_OK;
@@ -1696,13 +1702,21 @@ extern "C" int m3s_prof_end(double* out, int* n_iter) {
     double acc[4] = {0, 0, 0, 0};
     int n = 0;
     if (g_prof.accum_only) {  // a0 a1 per iteration
+        // out[0] / *n_iter: the iteration kernel (records already packed); out[1] / out[2]: the
+        // launches that built the records themselves (a call's first, M3S_GN_PACK_FIRST) and
+        // their count
         g_prof.accum_only = false;
         for (size_t k = 0; k + 2 <= g_prof.marks.size(); k += 2) {
             float ms = 0.f;
             M3S_HIP_CHECK(hipEventSynchronize(g_prof.marks[k + 1]));
             M3S_HIP_CHECK(hipEventElapsedTime(&ms, g_prof.marks[k], g_prof.marks[k + 1]));
-            acc[0] += ms;
-            n++;
+            if (k / 2 < g_prof.first.size() && g_prof.first[k / 2]) {
+                acc[1] += ms;
+                acc[2] += 1;
+            } else {
+                acc[0] += ms;
+                n++;
+            }
         }
         for (int q = 0; q < 4; q++) out[q] = acc[q];
         *n_iter = n;
