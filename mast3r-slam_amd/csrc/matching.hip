@@ -160,8 +160,45 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
     converged[g] = conv;
 }
 
+#ifndef M3S_REFINE_WAVES
+#define M3S_REFINE_WAVES 1
+#endif
+#ifndef M3S_REFINE_GROUP
+#define M3S_REFINE_GROUP 64
+#endif
+// Candidates J0 .. J0+NG-1 of one window column (v offsets inner, matching_kernels.cu:55): their
+// rows loaded together, the score chains interleaved, then compared in candidate order; the next
+// group of the column after it (M3S_REFINE_GROUP candidates per group: fewer rows live at once)
+template <int F, int J0, int G, int SC>
+__device__ __forceinline__ void refine_column(const half2_t (&q2)[F / 2], const uint16_t* __restrict__ img,
+                                              int64_t u, int64_t vb, int d, int W, int H,
+                                              half_t& max_score, int64_t& u_new, int64_t& v_new) {
+    constexpr int NG = G < SC - J0 ? G : SC - J0;
+    uint4 rows[NG][F / 8];
+    bool ok[NG];
+#pragma unroll
+    for (int j = 0; j < NG; j++) {
+        const int64_t v = vb + (int64_t)(J0 + j) * d;
+        ok[j] = inside_image(u, v, W, H);
+        const uint4* src = reinterpret_cast<const uint4*>(img + (ok[j] ? (v * W + u) * F : 0));
+#pragma unroll
+        for (int c = 0; c < F / 8; c++) rows[j][c] = src[c];
+    }
+    half_t score[NG];
+    score_f16_multi<F, NG>(q2, rows, score);
+#pragma unroll
+    for (int j = 0; j < NG; j++) {
+        if (ok[j] && score[j] > max_score) {
+            max_score = score[j];
+            u_new = u;
+            v_new = vb + (int64_t)(J0 + j) * d;
+        }
+    }
+    if constexpr (J0 + NG < SC) refine_column<F, J0 + NG, G, SC>(q2, img, u, vb, d, W, H, max_score, u_new, v_new);
+}
+
 template <int F, int R>
-__global__ __launch_bounds__(kBlock) void refine_f16_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M3S_REFINE_WAVES))) void refine_f16_kernel(
     const uint16_t* __restrict__ D11, const uint16_t* __restrict__ D21,
     const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int64_t* __restrict__ lin, int H,
     int W, int64_t N, int64_t B, TileMap tm, int radius_rt, int dilation_max) {
@@ -194,27 +231,8 @@ __global__ __launch_bounds__(kBlock) void refine_f16_kernel(
         for (int i = 0; i < S; i++) {          // u offset outer (matching_kernels.cu:54)
             const int64_t u = u0 - rd + (int64_t)i * d;
             if constexpr (R >= 0) {
-                constexpr int SC = 2 * R + 1;
-                uint4 rows[SC][F / 8];
-                bool ok[SC];
-#pragma unroll
-                for (int j = 0; j < SC; j++) {  // v offset inner (:55)
-                    const int64_t v = v0 - rd + (int64_t)j * d;
-                    ok[j] = inside_image(u, v, W, H);
-                    const uint4* src = reinterpret_cast<const uint4*>(img + (ok[j] ? (v * W + u) * F : 0));
-#pragma unroll
-                    for (int c = 0; c < F / 8; c++) rows[j][c] = src[c];
-                }
-                half_t score[SC];
-                score_f16_multi<F, SC>(q2, rows, score);
-#pragma unroll
-                for (int j = 0; j < SC; j++) {
-                    if (ok[j] && score[j] > max_score) {
-                        max_score = score[j];
-                        u_new = u;
-                        v_new = v0 - rd + (int64_t)j * d;
-                    }
-                }
+                refine_column<F, 0, M3S_REFINE_GROUP, 2 * R + 1>(q2, img, u, v0 - rd, d, W, H, max_score, u_new,
+                                                                 v_new);
             } else {
                 for (int j = 0; j < S; j++) {
                     const int64_t v = v0 - rd + (int64_t)j * d;
