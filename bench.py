@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--iters", type=int, default=None, help="GN iterations per op call")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-matching", action="store_true", help="skip the matching-kernel section")
+    ap.add_argument("--no-cfg4", action="store_true",
+                    help="skip the configs[3] block (1024-edge graph, edge-sharded like the headline config)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "accum_traffic.json"))
     return ap.parse_args()
 
@@ -99,7 +101,12 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU)")
     if os.environ.get("M3S_BENCH_SPAWN_CHECK"):  # tests/test_bench_cli.py: the launch, no GPU work
-        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank}), flush=True)
+        from m3s import synth
+        from m3s.dist import shard_range
+        plan = {c: list(shard_range(2 * synth.CONFIGS[c]["E"], world, rank))
+                for c in ([args.config] + (["cfg4"] if args.config != "cfg4" and not args.no_cfg4 else []))}
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "edge_ranges": plan}),
+              flush=True)
         return
     if os.environ.get("M3S_EXIT_MAPS"):
         _dump_maps_at_exit(os.environ["M3S_EXIT_MAPS"])
@@ -116,80 +123,19 @@ def main():
     torch.cuda.set_device(dev)
 
     import mast3r_slam_backends as mb
+    from m3s.dist import HostComm, RcclComm
+
+    comm = (HostComm() if rehearse else RcclComm(rank, world, device=dev)) if world > 1 else None
+    r = time_config(args.config, args.iters, args.steps, args.warmup, world, rank, rehearse, dev, comm)
+    g, mode, iters, E_und, lo, hi = r["g"], r["mode"], r["iters"], r["E_und"], r["lo"], r["hi"]
+    Twc0, Twc, elapsed = r["Twc0"], r["Twc"], r["elapsed"]
+    prof, nprof, ph, nph, ray_path = r["prof"], r["nprof"], r["ph"], r["nph"], r["ray_path"]
+    acc_events = r["acc_events"]
+    n_ph = max(nph.value, 1)
     from m3s import synth
-    from m3s.dist import HostComm, RcclComm, gauss_newton_sharded, shard_range
-    from m3s.geometry import constrain_points_to_ray
 
     spec = synth.CONFIGS[args.config]
-    mode = spec["mode"]
-    iters = args.iters if args.iters is not None else spec["iters"]
-    E_und = spec["E"]
     E_dir = 2 * E_und
-    lo, hi = shard_range(E_dir, world, rank)
-    g = synth.make_graph(args.config, device=dev, edge_range=(lo, hi))
-    if mode == "calib":  # solve_GN_calib does this before the op (global_opt.py:172)
-        g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
-    comm = (HostComm() if rehearse else RcclComm(rank, world, device=dev)) if world > 1 else None
-    Twc0 = g.Twc.clone()
-    Twc = g.Twc.clone()
-    L = dict(LOCAL, K=g.K, height=g.H, width=g.W)
-
-    def step():
-        Twc.copy_(Twc0)
-        if world == 1:
-            if mode == "calib":
-                mb.gauss_newton_calib(Twc, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
-                                      L["pixel_border"], L["depth_eps"], L["sigma_pixel"],
-                                      L["sigma_depth"], L["C_conf"], L["Q_conf"], iters, 0.0)
-            else:
-                mb.gauss_newton_rays(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, L["sigma_ray"],
-                                     L["sigma_dist"], L["C_conf"], L["Q_conf"], iters, 0.0)
-        else:
-            gauss_newton_sharded(mode, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, lo, comm,
-                                 iters, 0.0, **L)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # the timed region carries HIP events around each accumulate launch only (the roofline
-    # kernel); the other phases are timed in one extra untimed step below
-    acc_events = os.environ.get("M3S_BENCH_ACC_EVENTS", "1") != "0"
-    if acc_events:
-        mb.lib.m3s_prof_begin_accum()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    prof = (ctypes.c_double * 4)()
-    nprof = ctypes.c_int(0)
-    mb.lib.m3s_prof_end(prof, ctypes.byref(nprof))
-    mb.lib.m3s_prof_begin()
-    step()
-    torch.cuda.synchronize()
-    ph = (ctypes.c_double * 4)()
-    nph = ctypes.c_int(0)
-    mb.lib.m3s_prof_end(ph, ctypes.byref(nph))
-    # which accumulate path the op took (its device flags, read back by one more untimed call)
-    os.environ["M3S_GN_DEBUG_FLAGS"] = "2"
-    step()
-    torch.cuda.synchronize()
-    del os.environ["M3S_GN_DEBUG_FLAGS"]
-    dbg = (ctypes.c_int * 4)()
-    mb.lib.m3s_gn_debug_flags(dbg)
-    ray_path = bool(dbg[3])
-    n_ph = max(nph.value, 1)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
     pair_iters = E_und * iters * args.steps
     value = pair_iters / elapsed
     n_it = max(nprof.value, 1)
@@ -272,6 +218,15 @@ def main():
         out["accuracy"] = accuracy(g, mode, Twc0, Twc, cpu_baseline.last_poses,
                                    cpu_baseline.exact_poses, cpu_baseline.full_poses, iters,
                                    cpu_baseline.last_step, cpu_baseline.exact_step)
+        if os.environ.get("M3S_BENCH_REF_ORDER", "1") != "0":
+            out["accuracy"]["reference_order_mode"] = reference_order_block(g, mode, Twc0, args, iters)
+    # BASELINE.json configs[3] (1024 edges, the config SURVEY §8(e) sets the scaling target on):
+    # with --gpus N it is edge-sharded like the headline config, so the driver's SCALE run
+    # measures it at every N.  Its own block; ``value`` stays the headline config's.
+    if args.config != "cfg4" and not args.no_cfg4:
+        del g, Twc0, Twc, r  # the headline graph is not needed any more
+        torch.cuda.empty_cache()
+        out["cfg4"] = config_block("cfg4", args, world, rank, rehearse, dev, comm)
     if rank == 0 and world == 1 and not args.no_matching:
         out["matching"] = matching_bench(dev)
         out["tracking"] = tracking_bench(dev)
@@ -281,6 +236,171 @@ def main():
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def time_config(cfg, iters_arg, steps, warmup, world, rank, rehearse, dev, comm):
+    """Build ``cfg``'s graph (this rank's directed-edge range only), run ``warmup`` untimed op
+    calls, then time ``steps`` calls bracketed by a barrier + synchronize on both sides
+    (max over ranks); one more untimed call gives the phase times, another the accumulate path
+    the op took."""
+    import mast3r_slam_backends as mb
+    from m3s import synth
+    from m3s.dist import gauss_newton_sharded, shard_range
+    from m3s.geometry import constrain_points_to_ray
+
+    spec = synth.CONFIGS[cfg]
+    mode = spec["mode"]
+    iters = iters_arg if iters_arg is not None else spec["iters"]
+    E_und = spec["E"]
+    lo, hi = shard_range(2 * E_und, world, rank)
+    g = synth.make_graph(cfg, device=dev, edge_range=(lo, hi))
+    if mode == "calib":  # solve_GN_calib does this before the op (global_opt.py:172)
+        g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    Twc0 = g.Twc.clone()
+    Twc = g.Twc.clone()
+    L = dict(LOCAL, K=g.K, height=g.H, width=g.W)
+
+    def step():
+        Twc.copy_(Twc0)
+        if world == 1:
+            if mode == "calib":
+                mb.gauss_newton_calib(Twc, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
+                                      L["pixel_border"], L["depth_eps"], L["sigma_pixel"],
+                                      L["sigma_depth"], L["C_conf"], L["Q_conf"], iters, 0.0)
+            else:
+                mb.gauss_newton_rays(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, L["sigma_ray"],
+                                     L["sigma_dist"], L["C_conf"], L["Q_conf"], iters, 0.0)
+        else:
+            gauss_newton_sharded(mode, Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, lo, comm,
+                                 iters, 0.0, **L)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # the timed region carries HIP events around each accumulate launch only (the roofline
+    # kernel); the other phases are timed in one extra untimed step below
+    acc_events = os.environ.get("M3S_BENCH_ACC_EVENTS", "1") != "0"
+    if acc_events:
+        mb.lib.m3s_prof_begin_accum()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    prof = (ctypes.c_double * 4)()
+    nprof = ctypes.c_int(0)
+    mb.lib.m3s_prof_end(prof, ctypes.byref(nprof))
+    mb.lib.m3s_prof_begin()
+    step()
+    torch.cuda.synchronize()
+    ph = (ctypes.c_double * 4)()
+    nph = ctypes.c_int(0)
+    mb.lib.m3s_prof_end(ph, ctypes.byref(nph))
+    # which accumulate path the op took (its device flags, read back by one more untimed call)
+    os.environ["M3S_GN_DEBUG_FLAGS"] = "2"
+    step()
+    torch.cuda.synchronize()
+    del os.environ["M3S_GN_DEBUG_FLAGS"]
+    dbg = (ctypes.c_int * 4)()
+    mb.lib.m3s_gn_debug_flags(dbg)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return dict(g=g, mode=mode, iters=iters, E_und=E_und, lo=lo, hi=hi, Twc0=Twc0, Twc=Twc,
+                elapsed=elapsed, prof=prof, nprof=nprof, ph=ph, nph=nph, ray_path=bool(dbg[3]),
+                acc_events=acc_events, step=step)
+
+
+def config_block(cfg, args, world, rank, rehearse, dev, comm):
+    """One more BASELINE config timed exactly like the headline one (same steps / warmup, same
+    edge sharding over the ranks), as its own JSON block."""
+    from m3s import synth
+    from m3s.dist import comm_size
+
+    r = time_config(cfg, None, args.steps, args.warmup, world, rank, rehearse, dev, comm)
+    spec = synth.CONFIGS[cfg]
+    nph = max(r["nph"].value, 1)
+    n_it = max(r["nprof"].value, 1)
+    acc_ms = r["prof"][0] / n_it if r["acc_events"] else r["ph"][0] / nph
+    packed = r["iters"] >= 3 and os.environ.get("M3S_GN_PACK", "1") != "0"
+    bpe = PACKED_BYTES_PER_POINT_EDGE[r["mode"]] if packed else REF_BYTES_PER_POINT_EDGE
+    local = r["hi"] - r["lo"]
+    bytes_launch = bpe * r["g"].HW * local
+    return {
+        "value": r["E_und"] * r["iters"] * args.steps / r["elapsed"],
+        "unit": "keyframe-pair GN iters/s",
+        "ms_per_step": r["elapsed"] / args.steps * 1e3,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "scaling": "strong",
+        "workload": f"{cfg}: gauss_newton_{r['mode']} op call, {r['E_und']} keyframe-pair edges "
+                    f"({2 * r['E_und']} directed), {spec['N']} keyframes, {r['g'].H}x{r['g'].W}, "
+                    f"{r['iters']} GN iters/step, delta_thresh=0",
+        "directed_edges_this_rank": local,
+        "n_ranks": world,
+        "n_ranks_comm": comm_size(comm) if comm is not None else 1,
+        "comm": (("host all-reduce (rehearsal)" if rehearse else "RCCL") if world > 1 else None),
+        "phase_ms_per_iter": {
+            "accumulate": acc_ms,
+            "reduce_compact_allreduce": r["ph"][1] / nph,
+            "solve": r["ph"][2] / nph,
+            "retract": r["ph"][3] / nph,
+        },
+        "accumulate_GBps": bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None,
+        "accumulate_bytes_per_point_edge": bpe,
+    }
+
+
+def reference_order_block(g, mode, Twc0, args, iters, reps=3):
+    """The price of parity: the same op call in the reference-order mode (gn_refacc.hip: the
+    reference kernels' own float order and formulas) -- its throughput on
+    this graph, and its poses after one iteration against the CPU oracle's."""
+    import numpy as np
+
+    import mast3r_slam_backends as mb
+
+    L = dict(LOCAL, K=g.K, height=g.H, width=g.W)
+    Twc = Twc0.clone()
+
+    def call(n):
+        Twc.copy_(Twc0)
+        if mode == "calib":
+            mb.gauss_newton_calib(Twc, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
+                                  L["pixel_border"], L["depth_eps"], L["sigma_pixel"], L["sigma_depth"],
+                                  L["C_conf"], L["Q_conf"], n, 0.0)
+        else:
+            mb.gauss_newton_rays(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, L["sigma_ray"],
+                                 L["sigma_dist"], L["C_conf"], L["Q_conf"], n, 0.0)
+
+    prev = mb.set_gn_order("reference")
+    try:
+        call(iters)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call(iters)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        call(1)
+        T1 = Twc.cpu().numpy().astype(np.float64)
+    finally:
+        mb.set_gn_order(prev)
+    To = np.asarray(cpu_baseline.last_poses, np.float64)
+    E_und = g.ii.shape[0] // 2
+    return {
+        "value": E_und * iters / dt,
+        "unit": "keyframe-pair GN iters/s",
+        "ms_per_call": dt * 1e3,
+        "calls_timed": reps,
+        "pose_max_rel_err_vs_oracle_1iter": float(np.abs(T1 - To).max() / np.abs(To).max()),
+    }
 
 
 def matching_bench(dev, reps=10):

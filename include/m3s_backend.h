@@ -361,6 +361,9 @@ int m3s_comm_init(const void* id, int nranks, int rank, void** comm_out);
 typedef int (*m3s_host_allreduce_fn)(void* user, double* buf, size_t count);
 int m3s_comm_init_host(m3s_host_allreduce_fn fn, void* user, int nranks, int rank, void** comm_out);
 int m3s_comm_destroy(void* comm);
+/* The number of ranks the communicator spans, as its transport reports it (RCCL:
+ * ncclCommCount; host callback: the count it was created with). */
+int m3s_comm_size(void* comm, int* nranks_out);
 
 #ifdef __cplusplus
 }

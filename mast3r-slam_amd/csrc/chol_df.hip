@@ -139,65 +139,68 @@ __device__ __forceinline__ void put_block(double* S, int r0, int c0, d4 d, doubl
     for (int e = 0; e < 4; e++) S[(r0 + (lane >> 4) + 4 * e) * LD + c0 + (lane & 15)] = sgn * d[e];
 }
 
-// Panel step of the tile LL^T, run by wave 0 (lanes >= c0): columns c0 .. c0+7 of rows >= c0
-// are final after it, and the diagonal lanes have written the 8x8 inverse block into Li.
-__device__ __forceinline__ void panel_factor(double* A, double* Li, int c0, int* flags) {
+// one lane's double, broadcast to the wave (two v_readlane_b32: SGPRs)
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __hiloint2double(hi, lo);
+}
+
+// Panel step of the tile LL^T, run by wave 0: columns c0 .. c0+7 of every row, lane = row, in
+// registers, right-looking over the 8 columns.  A pivot and the panel's diagonal-block entries
+// reach the other lanes by v_readlane (no LDS round trip, no barrier on the pivot chain), and
+// the rows below the diagonal block get their L entries in the same sweep (the panel's trsm).
+// The critical chain per column is readlane -> rsq + Newton -> scale -> the next column's
+// update in the next pivot's lane -> readlane.  Dinv[p] = 1 / l_pp (the pivot's rsqrt) for the
+// 8x8 inverse block (diag_inv8, off the chain).
+__device__ __forceinline__ void panel_factor(double* A, double* Dinv, int c0, int* flags) {
     const int lane = threadIdx.x & 63;
-    if (lane >= c0) {
-        // every lane factors the 8x8 diagonal block in registers (redundantly: no cross-lane
-        // traffic), right-looking, one rsq + one Newton step per pivot (1/l_pp is that
-        // rsqrt), then ONE forward substitution x = L_pp^-1 a per lane with no divergence:
-        // panel lanes solve their row (a = their row of A), diagonal-block lanes solve
-        // a = e_i, i.e. column i of L_pp^-1 (the doubling inverse's 8x8 blocks)
-        const int r = lane;
-        const bool dg = r < c0 + 8;
-        double D[8][8], x[8];
+    double a[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++)
+    for (int p = 0; p < 8; p++) a[p] = A[lane * LD + c0 + p];
+    bool bad = false;
 #pragma unroll
-            for (int p = 0; p <= i; p++) D[i][p] = A[(c0 + i) * LD + c0 + p];
+    for (int p = 0; p < 8; p++) {
+        const double d = rdlane(a[p], c0 + p);
+        bad |= d <= 0.0;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
+        double y = __builtin_amdgcn_rsq(d);
+        y = y * fma(-0.5 * d * y, y, 1.5);
+        const double l = a[p] * y;
+        a[p] = lane >= c0 + p ? l : 0.0;
+        if (lane == 0) Dinv[c0 + p] = y;
 #pragma unroll
-        for (int p = 0; p < 8; p++) x[p] = dg ? (r - c0 == p ? 1.0 : 0.0) : A[r * LD + c0 + p];
-        double l[8][8], inv[8];
-        bool bad = false;
-#pragma unroll
-        for (int p = 0; p < 8; p++) {
-            const double dpp = D[p][p];
-            if (dpp <= 0.0) bad = true;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
-            double y = __builtin_amdgcn_rsq(dpp);
-            y = y * fma(-0.5 * dpp * y, y, 1.5);
-            inv[p] = y;
-            l[p][p] = dpp * y;
-#pragma unroll
-            for (int i = p + 1; i < 8; i++) l[i][p] = D[i][p] * y;
-#pragma unroll
-            for (int i = p + 1; i < 8; i++)
-#pragma unroll
-                for (int j = p + 1; j <= i; j++) D[i][j] = fma(-l[i][p], l[j][p], D[i][j]);
-        }
-        if (bad && r == c0) flags[kFlagFail] = 1;
-#pragma unroll
-        for (int p = 0; p < 8; p++) {
-            const double xp = x[p] * inv[p];
-            x[p] = xp;
-#pragma unroll
-            for (int i = p + 1; i < 8; i++) x[i] = fma(-xp, l[i][p], x[i]);
-        }
-        if (dg) {
-            const int i = r - c0;
-#pragma unroll
-            for (int ii = 0; ii < 8; ii++)
-                if (ii == i) {
-#pragma unroll
-                    for (int p = 0; p <= ii; p++) A[r * LD + c0 + p] = l[ii][p];
-                }
-#pragma unroll
-            for (int m = 0; m < 8; m++) Li[(c0 + m) * LD + r] = x[m];
-        } else {
-#pragma unroll
-            for (int p = 0; p < 8; p++) A[r * LD + c0 + p] = x[p];
-        }
+        for (int q = p + 1; q < 8; q++) a[q] = fma(-a[p], rdlane(a[p], c0 + q), a[q]);
     }
+    if (bad && lane == 0) flags[kFlagFail] = 1;
+    // rows below the block: the whole panel row; diagonal-block rows: their lower part only
+    // (the upper entries of the tile stay as they were: never read)
+#pragma unroll
+    for (int p = 0; p < 8; p++)
+        if (lane >= c0 + p) A[lane * LD + c0 + p] = a[p];
+}
+
+// the panel's 8x8 inverse block L_pp^-1 -> Li (lanes 0..7 of the calling wave: lane i solves
+// L_pp x = e_i, i.e. column i of the inverse), from L_pp in A and 1/l_pp in Dinv
+__device__ __forceinline__ void diag_inv8(const double* A, double* Li, const double* Dinv, int c0) {
+    const int i = threadIdx.x & 63;
+    if (i >= 8) return;
+    double L[8][8], inv[8], x[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+        inv[m] = Dinv[c0 + m];
+#pragma unroll
+        for (int k = 0; k < m; k++) L[m][k] = A[(c0 + m) * LD + c0 + k];
+    }
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+        double s = m == i ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < m; k++) s = fma(-L[m][k], x[k], s);
+        x[m] = m >= i ? s * inv[m] : 0.0;
+    }
+#pragma unroll
+    for (int m = 0; m < 8; m++) Li[(c0 + m) * LD + c0 + i] = x[m];
 }
 
 // A[I-block rows][J-block cols] -= P_I P_J^T with the panel at columns c0 .. c0+7; only trailing
@@ -216,6 +219,7 @@ __device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[N
     double a0[NB], a1[NB], b0[NB], b1[NB];
 #pragma unroll
     for (int k = 0; k < NB; k++) {
+        if (!on[k]) continue;
 #pragma unroll
         for (int e = 0; e < 4; e++) c[k][e] = A[(16 * I[k] + kq + 4 * e) * LD + 16 * J[k] + r16];
         a0[k] = -A[(16 * I[k] + r16) * LD + c0 + kq];
@@ -224,9 +228,11 @@ __device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[N
         b1[k] = A[(16 * J[k] + r16) * LD + c0 + 4 + kq];
     }
 #pragma unroll
-    for (int k = 0; k < NB; k++) c[k] = mfma(a0[k], b0[k], c[k]);
+    for (int k = 0; k < NB; k++)
+        if (on[k]) c[k] = mfma(a0[k], b0[k], c[k]);
 #pragma unroll
-    for (int k = 0; k < NB; k++) d[k] = mfma(a1[k], b1[k], d4{0.0, 0.0, 0.0, 0.0});
+    for (int k = 0; k < NB; k++)
+        if (on[k]) d[k] = mfma(a1[k], b1[k], d4{0.0, 0.0, 0.0, 0.0});
 #pragma unroll
     for (int k = 0; k < NB; k++) {
         if (!on[k]) continue;
@@ -242,21 +248,23 @@ __device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[N
 // LL^T of the lower triangle of A (LDS) in place and Li = L^-1 (Li zeroed by the caller).
 // Look-ahead: in step s wave 0 applies panel s to the block column holding panel s+1 and
 // factors panel s+1 right away, while waves 1-3 apply panel s to the block columns right of it
-// (one barrier per step; the single-wave panel factor overlaps the rest of the update).
+// and wave 1 inverts panel s's 8x8 diagonal block (one barrier per step; the step loop is
+// unrolled, so every step issues only the MFMAs of its live blocks).
 // early: a ready word published once every wave's earlier stores landed (after the first panel
 // step, when they long have), so the caller's stores need no waiting on its critical path
-__device__ void potrf_inverse(double* A, double* Li, double* Tm, int* flags, long long* pt, int* early,
-                              int epoch) {
+__device__ void potrf_inverse(double* A, double* Li, double* Tm, double* Dinv, int* flags, long long* pt,
+                              int* early, int epoch) {
     const int tid = threadIdx.x, w = tid >> 6;
     auto pstamp = [&](int slot) {
         if (pt && tid == 0) pt[slot] = (long long)__builtin_amdgcn_s_memrealtime();
     };
     pstamp(0);
-    if (w == 0) panel_factor(A, Li, 0, flags);
+    if (w == 0) panel_factor(A, Dinv, 0, flags);
     if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (early && tid == 0) __hip_atomic_store(early, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     pstamp(1);
+#pragma unroll
     for (int s = 0; s + 1 < T / 8; s++) {
         const int c0 = 8 * s;
         const int J1 = (c0 + 8) >> 4;  // block column holding panel s+1
@@ -265,16 +273,19 @@ __device__ void potrf_inverse(double* A, double* Li, double* Tm, int* flags, lon
             const bool on[4] = {0 >= J1, 1 >= J1, 2 >= J1, 3 >= J1};
             trail_blocks<4>(A, c0, I, J, on);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS writes before the reads
-            panel_factor(A, Li, c0 + 8, flags);
+            panel_factor(A, Dinv, c0 + 8, flags);
         } else {
             const int I[3] = {w, w, w};
             const int J[3] = {min(J1 + 1, 3), min(J1 + 2, 3), min(J1 + 3, 3)};
             const bool on[3] = {J1 + 1 <= w, J1 + 2 <= w, J1 + 3 <= w};
             if (on[0]) trail_blocks<3>(A, c0, I, J, on);
+            if (w == 1) diag_inv8(A, Li, Dinv, c0);
         }
         __syncthreads();
         pstamp(2 + s);
     }
+    if (w == 1) diag_inv8(A, Li, Dinv, T - 8);
+    __syncthreads();
     // inverse by doubling, [[Ai,0],[B,Ci]]^-1 = [[Ai,0],[-Ci B Ai, Ci]]; the 8x8 diagonal
     // inverses came from the panel steps.  Stage 8 on VALU (one output per thread):
     {
@@ -312,6 +323,46 @@ __device__ void potrf_inverse(double* A, double* Li, double* Tm, int* flags, lon
         __syncthreads();
     }
     pstamp(17);
+}
+
+// Z (lower 16x16 blocks) -= X X^T, X: [64][LD] in LDS.  The 10 lower blocks are dealt 3/3/2/2 to
+// the waves (a wave per block row would give wave 3 four blocks, 64 MFMAs): 48 MFMAs on the
+// busiest wave instead of the full product's 64.
+template <int W>
+__device__ __forceinline__ void syrk_lower_w(double* Z, const double* X) {
+    constexpr int BI[4][3] = {{0, 1, 2}, {1, 2, 3}, {2, 3, 0}, {3, 3, 0}};
+    constexpr int BJ[4][3] = {{0, 0, 0}, {1, 1, 0}, {2, 1, 0}, {2, 3, 0}};
+    constexpr int NB = W < 2 ? 3 : 2;
+    const int lane = threadIdx.x & 63;
+    const int r = lane & 15, kq = lane >> 4;
+    d4 acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) acc[b][e] = Z[(16 * BI[W][b] + kq + 4 * e) * LD + 16 * BJ[W][b] + r];
+#pragma unroll
+    for (int st = 0; st < 16; st++) {
+        double x[NB], y[NB];
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            x[b] = -X[(16 * BI[W][b] + r) * LD + 4 * st + kq];
+            y[b] = X[(16 * BJ[W][b] + r) * LD + 4 * st + kq];
+        }
+#pragma unroll
+        for (int b = 0; b < NB; b++) acc[b] = mfma(x[b], y[b], acc[b]);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) Z[(16 * BI[W][b] + kq + 4 * e) * LD + 16 * BJ[W][b] + r] = acc[b][e];
+}
+__device__ __forceinline__ void syrk_lower(double* Z, const double* X) {
+    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+        case 0: syrk_lower_w<0>(Z, X); break;
+        case 1: syrk_lower_w<1>(Z, X); break;
+        case 2: syrk_lower_w<2>(Z, X); break;
+        default: syrk_lower_w<3>(Z, X); break;
+    }
 }
 
 // Workgroup 0 runs the whole diagonal chain C: for j = 0 .. nt-1
@@ -373,6 +424,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
     __shared__ __attribute__((aligned(16))) double X[T * LD];
     __shared__ __attribute__((aligned(16))) double Y[T * LD];
     __shared__ __attribute__((aligned(16))) double Z[T * LD];
+    __shared__ double Dinv[T];
     const int tid = threadIdx.x;
     const int nt = a.nt;
     const int64_t ld = a.npad;
@@ -392,6 +444,9 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             cstamp(j, 0);
             if (j == 0) {
                 load_acc<false>(accd, tile(0, 0), ld);
+                acc_to_lds(Z, accd);
+                for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;
+                __syncthreads();
             } else {
                 d4 accs[4];
                 if (j == 1) {
@@ -404,6 +459,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 // the loads drained the queue: Linv_{j-1}'s stores have landed
                 publish(a, (j - 1) * nt + (j - 1));
                 acc_to_lds(X, accs);
+                acc_to_lds(Z, accd);
                 __syncthreads();
 #pragma unroll
                 for (int J = 0; J < 4; J++) accs[J] = d4{0.0, 0.0, 0.0, 0.0};
@@ -411,15 +467,13 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 store_acc_coh(tile(j, j - 1), ld, accs);
                 __syncthreads();
                 acc_to_lds(X, accs);
+                for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;  // Linv_{j-1} read: Y -> the new Li
                 __syncthreads();
-                gemm_nt(X, X, accd, -1.0);
+                syrk_lower(Z, X);  // A'_jj = P_d(j) - L_{j,j-1} L_{j,j-1}^T (lower blocks)
                 __syncthreads();
             }
             cstamp(j, 1);
-            acc_to_lds(X, accd);
-            for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;
-            __syncthreads();
-            potrf_inverse(X, Y, Z, a.flags, a.trace && j == 0 ? a.trace + 4 * a.ntiles : nullptr,
+            potrf_inverse(Z, Y, X, Dinv, a.flags, a.trace && j == 0 ? a.trace + 4 * a.ntiles : nullptr,
                           j >= 1 ? a.ready + j * nt + (j - 1) : nullptr, a.epoch);
             cstamp(j, 2);
             double* Lk = a.Linv + (int64_t)j * T * T;

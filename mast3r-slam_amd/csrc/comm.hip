@@ -35,6 +35,7 @@ struct Rccl {
     nccl_result_t (*all_reduce)(const void*, void*, size_t, int, int, nccl_comm_t,
                                 hipStream_t) = nullptr;
     const char* (*err_str)(nccl_result_t) = nullptr;
+    nccl_result_t (*comm_count)(nccl_comm_t, int*) = nullptr;
 };
 
 Rccl* rccl() {
@@ -53,6 +54,7 @@ Rccl* rccl() {
             r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.h, "ncclCommDestroy");
             r.all_reduce = (decltype(r.all_reduce))dlsym(r.h, "ncclAllReduce");
             r.err_str = (decltype(r.err_str))dlsym(r.h, "ncclGetErrorString");
+            r.comm_count = (decltype(r.comm_count))dlsym(r.h, "ncclCommCount");
         }
     }
     if (!r.h || !r.get_unique_id || !r.comm_init_rank || !r.all_reduce) return nullptr;
@@ -176,6 +178,26 @@ extern "C" int m3s_comm_init_host(m3s_host_allreduce_fn fn, void* user, int nran
     c->fn = fn;
     c->user = user;
     *comm_out = c;
+    return M3S_OK;
+}
+
+extern "C" int m3s_comm_size(void* comm, int* nranks_out) {
+    Comm* c = as_comm(comm);
+    if (!c || !nranks_out) {
+        m3s::set_error("comm size: not an m3s communicator handle");
+        return M3S_ERR_COMM;
+    }
+    if (c->kind == kCommRccl) {
+        Rccl* r = rccl();
+        int n = 0;
+        if (!r || !r->comm_count || r->comm_count(c->nccl, &n) != 0) {
+            m3s::set_error("ncclCommCount failed");
+            return M3S_ERR_COMM;
+        }
+        *nranks_out = n;
+        return M3S_OK;
+    }
+    *nranks_out = c->nranks;
     return M3S_OK;
 }
 

@@ -51,6 +51,11 @@ __device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a
 __device__ __forceinline__ float vsplat(float s, float) { return s; }
 __device__ __forceinline__ float vrcp(float a) { return __builtin_amdgcn_rcpf(a); }    // v_rcp_f32
 __device__ __forceinline__ float vsqrt(float a) { return __builtin_amdgcn_sqrtf(a); }  // normal or 0 inputs
+// sqrt(q) of the point records: correctly rounded, as the reference's sqrtf(conf_weight)
+// (gn_kernels.cu:1404-1405; nvcc's sqrtf is IEEE).  Computed once per call (the record builders:
+// the pack, the first accumulate, the unpacked path of 1-2 iteration calls), so the ~10 extra
+// VALU of the exact expansion are off the iteration kernel.
+__device__ __forceinline__ float sqrt_cr(float a) { return __builtin_sqrtf(a); }
 __device__ __forceinline__ float vlog2(float a) { return __builtin_amdgcn_logf(a); }   // inputs > z_eps
 // rays mode's normalisation (M3S_RAYS_CR): 0 (default) = the hardware v_sqrt_f32 / v_rcp_f32
 // (1 ulp); 1 = correctly rounded sqrtf and v_rcp_f32 + one Newton step (the reference's sqrtf /
@@ -625,7 +630,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
                 const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) &&
                                 (cjs[s] > P.C_thresh);
                 code[s] = ok ? ind : (int)((unsigned)ind | 0x80000000u);
-                sqb[s] = __float_as_int(vsqrt(qs[s]));
+                sqb[s] = __float_as_int(sqrt_cr(qs[s]));
             }
             AccStage<MODE, false, false, NP> st;
             st.set(int4{code[0], sqb[0], code[1], sqb[1]}, int4{code[2], sqb[2], code[3], sqb[3]});
@@ -653,7 +658,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_kernel(
             p.xi2 = Xi_b[(int64_t)ind * 3 + 2];
             if constexpr (MODE == GN_CALIB) p.xi2 = p.xi2 > P.z_eps ? vrcp(p.xi2) : __builtin_nanf("");
             p.valid = vm && (q > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (Cj_b[k] > P.C_thresh);
-            p.sq = vsqrt(q);
+            p.sq = sqrt_cr(q);
             if constexpr (MODE == GN_CALIB) pixel_of(ind, P, p.ut, p.vt);
             point_body<MODE, float>(p, T, P, accs);
         }
@@ -729,7 +734,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_kernel(
         const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (ci_all || Ci_b[ind] > P.C_thresh) &&
                         (cj_all || cjs[s] > P.C_thresh);
         code[s] = pack_code(ind, ok, P);
-        sqb[s] = __float_as_int(vsqrt(qs[s]));
+        sqb[s] = __float_as_int(sqrt_cr(qs[s]));
     }
     int4* dst = pack + (ebase + k) / 2;
     dst[0] = int4{code[0], sqb[0], code[1], sqb[1]};
@@ -802,7 +807,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
                 const int ind = match_index(ids[s], vm[s], HW);
                 const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (Ci_b[ind] > P.C_thresh) && (cjs[s] > P.C_thresh);
                 code[s] = pack_code(ind, ok, P);
-                sqb[s] = __float_as_int(vsqrt(qs[s]));
+                sqb[s] = __float_as_int(sqrt_cr(qs[s]));
                 const float* xi = Xi_b + (int64_t)ind * 3;
                 const bool fin = finite3(&xj[3 * s]) &&
                                  (MODE == GN_CALIB ? (bool)isfinite(xi[2]) : finite3(xi));
@@ -847,7 +852,7 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
         const int kd = s_dead;  // pad > 0 implies a dead point exists (chunks are multiples of 4)
         const int64_t id = idx_e[kd];
         const int ind = match_index(id, valid_e[kd] != 0, HW);
-        pk[obase + running + tid] = make_int2(pack_code(ind, false, P), __float_as_int(vsqrt(Q_e[kd])));
+        pk[obase + running + tid] = make_int2(pack_code(ind, false, P), __float_as_int(sqrt_cr(Q_e[kd])));
         float* o = px + (obase + running + tid) * 3;
         o[0] = Xj_b[(int64_t)kd * 3];
         o[1] = Xj_b[(int64_t)kd * 3 + 1];
@@ -945,7 +950,7 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
                 const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (raw.ci_all || raw.Ci_b[ind] > P.C_thresh) &&
                                 (raw.cj_all || cjs[s] > P.C_thresh);
                 code[s] = pack_code(ind, ok, P);
-                sqb[s] = __float_as_int(vsqrt(qs[s]));
+                sqb[s] = __float_as_int(sqrt_cr(qs[s]));
             }
             a = int4{code[0], sqb[0], code[1], sqb[1]};
             b = int4{code[2], sqb[2], code[3], sqb[3]};
@@ -995,9 +1000,6 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
 // Per-iteration accumulate over the packed stream: 8 B {code, sqrt q} + Xj 12 B + the gather
 // of the matched point (calib: its depth from Zs; rays/points: Xi) per point-edge.
 
-#ifndef M3S_ACC_PIPE
-#define M3S_ACC_PIPE 1
-#endif
 #ifndef M3S_ACC_WAVES
 #define M3S_ACC_WAVES 1
 #endif
@@ -1035,37 +1037,10 @@ void gn_accum_packed_kernel(
     float acc[kNacc];
 #pragma unroll
     for (int q = 0; q < kNacc; q++) acc[q] = 0.0f;
-    // Steps of 4 points per lane; the packed records of the next step are loaded one step
+    // Steps of NP points per lane; the packed records of the next step are loaded one step
     // ahead, so a step waits for one memory round trip (its gathers + Xj) instead of two
     // (records, then the gathers they index).  A deeper pipeline (gathers of the next step
-    // in flight too) needs ~180 VGPRs, drops to 2 waves/SIMD and measured 8 % slower.
-#if M3S_ACC_PIPE == 2
-    const int tid = threadIdx.x;
-    constexpr int S = 4 * kAccThreads;
-    // two-deep: the gathers + Xj of step s+1 and the records of step s+2 are in flight while
-    // step s is computed
-    AccStage<MODE> cur, nxt;
-    cur.width = nxt.width = P.width;
-    int4 pa2 = int4{0, 0, 0, 0}, pb2 = int4{0, 0, 0, 0};
-    int k = k0 + 4 * tid;
-    if (k < k1) {
-        cur.set(pk_b[k / 2], pk_b[k / 2 + 1]);
-        cur.template load<MODE>(Xj_b, Xi_b, Zi_b, k);
-    }
-    if (k + S < k1) {
-        nxt.set(pk_b[(k + S) / 2], pk_b[(k + S) / 2 + 1]);
-    }
-    for (; k < k1; k += S) {
-        if (k + S < k1) nxt.template load<MODE>(Xj_b, Xi_b, Zi_b, k + S);
-        if (k + 2 * S < k1) {
-            pa2 = pk_b[(k + 2 * S) / 2];
-            pb2 = pk_b[(k + 2 * S) / 2 + 1];
-        }
-        cur.template compute<MODE>(T, P, acc);
-        cur = nxt;
-        nxt.set(pa2, pb2);
-    }
-#else
+    // in flight too) needs ~180 VGPRs, drops to 2 waves/SIMD and measured 8 % slower (removed).
     if constexpr (COMPACT) {
         // compacted stream: the chunk's live points, Xj copied alongside the records
         const int64_t cb = ((int64_t)e * P.nchunks + c) * P.chunk;
@@ -1088,7 +1063,6 @@ void gn_accum_packed_kernel(
         accum_steps<MODE, true, acc_np<MODE>()>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
     else
         accum_steps<MODE, false, acc_np<MODE>()>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
-#endif
     block_partial(acc, partials + ((int64_t)e * P.nchunks + c) * kNaccPad, ecnt != nullptr);
     if (ecnt != nullptr) {
         // fused edge reduce: the edge's last workgroup to finish sums its chunk partials (in

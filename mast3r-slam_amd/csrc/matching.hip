@@ -163,12 +163,10 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
 #ifndef M3S_REFINE_WAVES
 #define M3S_REFINE_WAVES 1
 #endif
-#ifndef M3S_REFINE_GROUP
-#define M3S_REFINE_GROUP 64
-#endif
 // Candidates J0 .. J0+NG-1 of one window column (v offsets inner, matching_kernels.cu:55): their
-// rows loaded together, the score chains interleaved, then compared in candidate order; the next
-// group of the column after it (M3S_REFINE_GROUP candidates per group: fewer rows live at once)
+// rows loaded together, the score chains interleaved, then compared in candidate order.  (Scoring
+// the column in groups of 1-3 candidates -- 7 instead of 3 waves per SIMD -- and a buffer-load
+// form with 32-bit offsets measured no gain at B=8; both were removed.)
 template <int F, int J0, int G, int SC>
 __device__ __forceinline__ void refine_column(const half2_t (&q2)[F / 2], const uint16_t* __restrict__ img,
                                               int64_t u, int64_t vb, int d, int W, int H,
@@ -196,44 +194,6 @@ __device__ __forceinline__ void refine_column(const half2_t (&q2)[F / 2], const 
     }
     if constexpr (J0 + NG < SC) refine_column<F, J0 + NG, G, SC>(q2, img, u, vb, d, W, H, max_score, u_new, v_new);
 }
-
-// The same column as buffer loads from a wave-uniform image descriptor (SGPRs): each row is a
-// 32-bit VGPR byte offset, no 64-bit address arithmetic per candidate row.  Valid when the wave's
-// pixels share one image and |u|, |v| < 2^20 (the kernel checks both).
-template <int F, int J0, int G, int SC>
-__device__ __forceinline__ void refine_column32(const half2_t (&q2)[F / 2], __amdgpu_buffer_rsrc_t img,
-                                                int u, int vb, int d, int W, int H,
-                                                half_t& max_score, int64_t& u_new, int64_t& v_new) {
-    constexpr int NG = G < SC - J0 ? G : SC - J0;
-    uint4 rows[NG][F / 8];
-    bool ok[NG];
-#pragma unroll
-    for (int j = 0; j < NG; j++) {
-        const int v = vb + (J0 + j) * d;
-        ok[j] = (unsigned)v < (unsigned)H && (unsigned)u < (unsigned)W;  // inside_image
-        const unsigned boff = ok[j] ? (unsigned)(v * W + u) * (unsigned)(F * 2) : 0u;  // < 2^31 bytes
-#pragma unroll
-        for (int c = 0; c < F / 8; c++) {
-            const auto w = __builtin_amdgcn_raw_buffer_load_b128(img, boff + 16u * c, 0, 0);
-            rows[j][c] = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-    }
-    half_t score[NG];
-    score_f16_multi<F, NG>(q2, rows, score);
-#pragma unroll
-    for (int j = 0; j < NG; j++) {
-        if (ok[j] && score[j] > max_score) {
-            max_score = score[j];
-            u_new = u;
-            v_new = vb + (J0 + j) * d;
-        }
-    }
-    if constexpr (J0 + NG < SC) refine_column32<F, J0 + NG, G, SC>(q2, img, u, vb, d, W, H, max_score, u_new, v_new);
-}
-
-#ifndef M3S_REFINE_OFF32
-#define M3S_REFINE_OFF32 0
-#endif
 
 template <int F, int R>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M3S_REFINE_WAVES))) void refine_f16_kernel(
@@ -264,34 +224,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M3S_REFI
     int64_t u_new = u0, v_new = v0;
     const int radius = R >= 0 ? R : radius_rt;
     const int S = 2 * radius + 1;
-    if constexpr (R >= 0 && M3S_REFINE_OFF32) {
-        constexpr int64_t kLim = 1 << 20;
-        const int bf = __builtin_amdgcn_readfirstlane((int)b);
-        const bool small = u0 > -kLim && u0 < kLim && v0 > -kLim && v0 < kLim && dilation_max < 1024 &&
-                           (int64_t)H * W * F * 2 < (int64_t)1 << 31;
-        if (__all(b == bf && small)) {
-            // the wave's image base, uniform (SGPRs); offsets in 32 bits
-            const __amdgpu_buffer_rsrc_t img4 = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(D11 + (int64_t)bf * H * W * F), (short)0, (int)((int64_t)H * W * F * 2), 0x00020000);
-            for (int d = dilation_max; d > 0; d--) {
-                const int rd = radius * d;
-                for (int i = 0; i < S; i++) {  // u offset outer (matching_kernels.cu:54)
-                    refine_column32<F, 0, M3S_REFINE_GROUP, 2 * R + 1>(q2, img4, (int)u0 - rd + i * d, (int)v0 - rd,
-                                                                       d, W, H, max_score, u_new, v_new);
-                }
-                u0 = u_new;
-                v0 = v_new;
-            }
-            store_match(p1_new, lin, g, W, u_new, v_new);
-            return;
-        }
-    }
     for (int d = dilation_max; d > 0; d--) {
         const int rd = radius * d;
         for (int i = 0; i < S; i++) {          // u offset outer (matching_kernels.cu:54)
             const int64_t u = u0 - rd + (int64_t)i * d;
             if constexpr (R >= 0) {
-                refine_column<F, 0, M3S_REFINE_GROUP, 2 * R + 1>(q2, img, u, v0 - rd, d, W, H, max_score, u_new,
+                refine_column<F, 0, 2 * R + 1, 2 * R + 1>(q2, img, u, v0 - rd, d, W, H, max_score, u_new,
                                                                  v_new);
             } else {
                 for (int j = 0; j < S; j++) {

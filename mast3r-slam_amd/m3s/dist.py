@@ -33,6 +33,13 @@ def shard_range(n_edges: int, world: int, rank: int):
     return lo, hi
 
 
+def comm_size(comm) -> int:
+    """Ranks the communicator spans, as its transport reports them (RCCL: ncclCommCount)."""
+    n = ctypes.c_int(0)
+    mb._raise(mb.lib.m3s_comm_size(comm.handle, ctypes.byref(n)), "comm size")
+    return n.value
+
+
 class RcclComm:
     """Backend-owned RCCL communicator for the per-iteration Hessian all-reduce."""
 

@@ -133,6 +133,7 @@ lib.m3s_gn_edge_hessians.argtypes = [ctypes.POINTER(GNArgs), _vp, _vp]
 lib.m3s_comm_get_unique_id.argtypes = [_vp]
 lib.m3s_comm_init.argtypes = [_vp, _i, _i, ctypes.POINTER(_vp)]
 lib.m3s_comm_destroy.argtypes = [_vp]
+lib.m3s_comm_size.argtypes = [_vp, ctypes.POINTER(_i)]
 # int (*)(void* user, double* buf, size_t count)
 HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(_i, _vp, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t)
 lib.m3s_comm_init_host.argtypes = [HOST_ALLREDUCE_FN, _vp, _i, _i, ctypes.POINTER(_vp)]

@@ -25,6 +25,19 @@ def test_gpus_flag_spawns_one_rank_per_gpu():
     assert sorted(d["rank"] for d in lines) == [0, 1]
     assert all(d["world"] == 2 for d in lines)
     assert sorted(d["local_rank"] for d in lines) == [0, 1]
+    # every rank also times BASELINE configs[3] (the 1024-edge cfg4 graph: 2048 directed edges),
+    # edge-sharded like the headline config: the ranks' ranges tile [0, 2048)
+    for cfg, n in (("cfg3", 512), ("cfg4", 2048)):
+        ranges = sorted(tuple(d["edge_ranges"][cfg]) for d in lines)
+        assert ranges[0][0] == 0 and ranges[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+
+
+def test_cfg4_block_can_be_skipped():
+    r = _run(["--gpus", "1", "--no-cfg4"], {"M3S_BENCH_SPAWN_CHECK": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    (d,) = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert list(d["edge_ranges"]) == ["cfg3"]
 
 
 def test_world_size_must_match_gpus_flag():
