@@ -27,6 +27,16 @@
 
 #include "gn_kernels.h"
 
+#ifndef M3S_DF_CC
+#define M3S_DF_CC 1  // 1: the column-cyclic tile factor (potrf_cc); 0: the 8-column panel steps (potrf_inverse)
+#endif
+#ifndef M3S_CC_OWNER_LDS
+#define M3S_CC_OWNER_LDS 1  // potrf_cc owner: later columns' updates from the LDS column (1) or all by v_readlane (0)
+#endif
+#ifndef M3S_DF_STAMPS
+#define M3S_DF_STAMPS 0  // diagnostics (tools/ubench_potrf64.hip): cycle stamps inside the potrf steps
+#endif
+
 namespace m3s {
 
 namespace {
@@ -45,7 +55,14 @@ struct DfArgs {
     int npad, nt, ntiles, epoch;  // ntiles = number of tasks (num_tasks)
     int spin_limit;  // bound of a ready wait (s_sleep(1) steps); < 0: every wait times out (test hook)
     long long* trace;  // diagnostics (tools/ubench_chol_df.hip): 4 timestamps per tile, else null
+    double* x;         // != null: the back-substitution L^T x = y runs in this launch too (x: npad)
 };
+
+// workgroup barrier ordering LDS only (__syncthreads also waits for every outstanding global
+// store to be acknowledged: ~1 us after write-through stores)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 __device__ __forceinline__ void stamp(const DfArgs& a, int t, int slot) {
     if (a.trace && threadIdx.x == 0) a.trace[4 * t + slot] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -120,25 +137,6 @@ __device__ __forceinline__ void gemm_nt(const double* X, const double* Y, d4 acc
     }
 }
 
-// D (16x16) = sum_{k < K} P[pr + i][pc + k] * Q[qr + k][qc + j]  (P, Q: [64][LD] in LDS)
-template <int K>
-__device__ __forceinline__ d4 block_mm(const double* P, int pr, int pc, const double* Q, int qr,
-                                       int qc) {
-    const int lane = threadIdx.x & 63;
-    const int r = lane & 15, kq = lane >> 4;
-    d4 d = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < K / 4; s++)
-        d = mfma(P[(pr + r) * LD + pc + 4 * s + kq], Q[(qr + 4 * s + kq) * LD + qc + r], d);
-    return d;
-}
-
-__device__ __forceinline__ void put_block(double* S, int r0, int c0, d4 d, double sgn) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int e = 0; e < 4; e++) S[(r0 + (lane >> 4) + 4 * e) * LD + c0 + (lane & 15)] = sgn * d[e];
-}
-
 // one lane's double, broadcast to the wave (two v_readlane_b32: SGPRs)
 __device__ __forceinline__ double rdlane(double v, int l) {
     const long long b = __double_as_longlong(v);
@@ -156,28 +154,32 @@ __device__ __forceinline__ double rdlane(double v, int l) {
 // 8x8 inverse block (diag_inv8, off the chain).
 __device__ __forceinline__ void panel_factor(double* A, double* Dinv, int c0, int* flags) {
     const int lane = threadIdx.x & 63;
-    double a[8];
+    double a[8], y[8];
 #pragma unroll
     for (int p = 0; p < 8; p++) a[p] = A[lane * LD + c0 + p];
     bool bad = false;
+    // lanes above a column's pivot hold upper-triangle garbage in it: never broadcast (only the
+    // lanes below a pivot are) and never stored, so no masking on the chain
 #pragma unroll
     for (int p = 0; p < 8; p++) {
         const double d = rdlane(a[p], c0 + p);
         bad |= d <= 0.0;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
-        double y = __builtin_amdgcn_rsq(d);
-        y = y * fma(-0.5 * d * y, y, 1.5);
-        const double l = a[p] * y;
-        a[p] = lane >= c0 + p ? l : 0.0;
-        if (lane == 0) Dinv[c0 + p] = y;
+        double r = __builtin_amdgcn_rsq(d);
+        r = r * fma(-0.5 * d * r, r, 1.5);
+        y[p] = r;
+        a[p] *= r;
 #pragma unroll
         for (int q = p + 1; q < 8; q++) a[q] = fma(-a[p], rdlane(a[p], c0 + q), a[q]);
     }
-    if (bad && lane == 0) flags[kFlagFail] = 1;
-    // rows below the block: the whole panel row; diagonal-block rows: their lower part only
-    // (the upper entries of the tile stay as they were: never read)
+    if (lane == 0) {
+        if (bad) flags[kFlagFail] = 1;
 #pragma unroll
-    for (int p = 0; p < 8; p++)
-        if (lane >= c0 + p) A[lane * LD + c0 + p] = a[p];
+        for (int p = 0; p < 8; p++) Dinv[c0 + p] = y[p];
+    }
+    // every lane stores its panel row: the rows above the pivots write garbage into the tile's
+    // upper triangle, which is never read
+#pragma unroll
+    for (int p = 0; p < 8; p++) A[lane * LD + c0 + p] = a[p];
 }
 
 // the panel's 8x8 inverse block L_pp^-1 -> Li (lanes 0..7 of the calling wave: lane i solves
@@ -203,12 +205,46 @@ __device__ __forceinline__ void diag_inv8(const double* A, double* Li, const dou
     for (int m = 0; m < 8; m++) Li[(c0 + m) * LD + c0 + i] = x[m];
 }
 
-// A[I-block rows][J-block cols] -= P_I P_J^T with the panel at columns c0 .. c0+7; only trailing
-// lower entries (row >= col >= c0 + 8) are written back.
-// NB trailing blocks (I[k], J[k]) at once, the blocks with on[k] written back: the two K = 4
-// MFMAs of a block go to separate accumulators and every block's MFMAs are issued before any
-// result is read, so a step costs one MFMA latency (~0.2 us for f64), not one per block and
-// pass (trail_block one block after the other: ~0.2 us per block on the panel chain).
+// Block row s (rows 8s .. 8s+7) of Li = L^-1, by one wave, for the column blocks k < s with
+// k = part (mod nparts):  X_ss = L_ss^-1 (diag_inv8; every wave that calls this writes the same
+// bytes) and X_sk = -X_ss sum_{m=k}^{s-1} L_sm X_mk, lane = (row r, column c) of the 8x8 block.
+// Needs the panels <= s factored and X's block rows < s complete: in the potrf step loop block
+// row s is built by waves 1-3 during step s, off the pivot chain, so only block row 7 is left
+// after the last panel (it replaces the 8 -> 16 -> 32 doubling stages, ~27 % of potrf + inverse).
+// scr: 64 doubles of LDS for this wave (the T block between its two products).
+__device__ __forceinline__ void inv_row(const double* A, double* Li, const double* Dinv, int s, int part,
+                                        int nparts, double* scr) {
+    const int lane = threadIdx.x & 63;
+    const int r = lane >> 3, c = lane & 7;
+    const int c0 = 8 * s;
+    diag_inv8(A, Li, Dinv, c0);
+    if (s == 0) return;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    double xs[8];  // row r of X_ss
+#pragma unroll
+    for (int m = 0; m < 8; m++) xs[m] = Li[(c0 + r) * LD + c0 + m];
+    for (int k = part; k < s; k += nparts) {
+        double t = 0.0;
+        for (int m = k; m < s; m++) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) t = fma(A[(c0 + r) * LD + 8 * m + q], Li[(8 * m + q) * LD + 8 * k + c], t);
+        }
+        scr[lane] = t;  // T[r][c]
+        double x = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++) x = fma(xs[m], scr[8 * m + c], x);
+        Li[(c0 + r) * LD + 8 * k + c] = -x;
+    }
+}
+
+// A[I-block rows][J-block cols] -= P_I P_J^T with the panel at columns c0 .. c0+7, for the
+// trailing columns (>= c0 + 8).  Block columns that still hold the panel itself (its 8 columns
+// are the block's first half) get a zero B operand there, so those outputs equal their input and
+// every block is stored whole: no per-element masked stores (a diagonal block's upper triangle
+// takes garbage, which is never read).
+// NB trailing blocks (I[k], J[k]) at once, the blocks with on[k] updated: the two K = 4 MFMAs
+// of a block go to separate accumulators and every block's MFMAs are issued before any result
+// is read, so a step costs one MFMA latency, not one per block and pass.
 template <int NB>
 __device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[NB], const int (&J)[NB],
                                              const bool (&on)[NB]) {
@@ -224,8 +260,9 @@ __device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[N
         for (int e = 0; e < 4; e++) c[k][e] = A[(16 * I[k] + kq + 4 * e) * LD + 16 * J[k] + r16];
         a0[k] = -A[(16 * I[k] + r16) * LD + c0 + kq];
         a1[k] = -A[(16 * I[k] + r16) * LD + c0 + 4 + kq];
-        b0[k] = A[(16 * J[k] + r16) * LD + c0 + kq];
-        b1[k] = A[(16 * J[k] + r16) * LD + c0 + 4 + kq];
+        const bool trailing = 16 * J[k] + r16 >= lo;
+        b0[k] = trailing ? A[(16 * J[k] + r16) * LD + c0 + kq] : 0.0;
+        b1[k] = trailing ? A[(16 * J[k] + r16) * LD + c0 + 4 + kq] : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < NB; k++)
@@ -236,23 +273,19 @@ __device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[N
 #pragma unroll
     for (int k = 0; k < NB; k++) {
         if (!on[k]) continue;
-        const int col = 16 * J[k] + r16;
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int row = 16 * I[k] + kq + 4 * e;
-            if (col >= lo && col <= row) A[row * LD + col] = c[k][e] + d[k][e];
-        }
+        for (int e = 0; e < 4; e++) A[(16 * I[k] + kq + 4 * e) * LD + 16 * J[k] + r16] = c[k][e] + d[k][e];
     }
 }
 
 // LL^T of the lower triangle of A (LDS) in place and Li = L^-1 (Li zeroed by the caller).
 // Look-ahead: in step s wave 0 applies panel s to the block column holding panel s+1 and
 // factors panel s+1 right away, while waves 1-3 apply panel s to the block columns right of it
-// and wave 1 inverts panel s's 8x8 diagonal block (one barrier per step; the step loop is
-// unrolled, so every step issues only the MFMAs of its live blocks).
+// and build block row s of the inverse (inv_row); one barrier per step, and the step loop is
+// unrolled, so every step issues only the MFMAs of its live blocks.
 // early: a ready word published once every wave's earlier stores landed (after the first panel
 // step, when they long have), so the caller's stores need no waiting on its critical path
-__device__ void potrf_inverse(double* A, double* Li, double* Tm, double* Dinv, int* flags, long long* pt,
+[[maybe_unused]] __device__ void potrf_inverse(double* A, double* Li, double* Tm, double* Dinv, int* flags, long long* pt,
                               int* early, int epoch) {
     const int tid = threadIdx.x, w = tid >> 6;
     auto pstamp = [&](int slot) {
@@ -273,56 +306,241 @@ __device__ void potrf_inverse(double* A, double* Li, double* Tm, double* Dinv, i
             const bool on[4] = {0 >= J1, 1 >= J1, 2 >= J1, 3 >= J1};
             trail_blocks<4>(A, c0, I, J, on);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS writes before the reads
+#if M3S_DF_STAMPS
+            if (pt && tid == 0) pt[20 + 4 * s] = (long long)__builtin_amdgcn_s_memtime();
+#endif
             panel_factor(A, Dinv, c0 + 8, flags);
+#if M3S_DF_STAMPS
+            if (pt && tid == 0) pt[21 + 4 * s] = (long long)__builtin_amdgcn_s_memtime();
+#endif
         } else {
             const int I[3] = {w, w, w};
             const int J[3] = {min(J1 + 1, 3), min(J1 + 2, 3), min(J1 + 3, 3)};
             const bool on[3] = {J1 + 1 <= w, J1 + 2 <= w, J1 + 3 <= w};
             if (on[0]) trail_blocks<3>(A, c0, I, J, on);
-            if (w == 1) diag_inv8(A, Li, Dinv, c0);
+            inv_row(A, Li, Dinv, s, w - 1, 3, Tm + 64 * w);
+#if M3S_DF_STAMPS
+            if (pt && tid == 192) pt[22 + 4 * s] = (long long)__builtin_amdgcn_s_memtime();
+#endif
         }
         __syncthreads();
+#if M3S_DF_STAMPS
+        if (pt && tid == 0) pt[23 + 4 * s] = (long long)__builtin_amdgcn_s_memtime();
+#endif
         pstamp(2 + s);
     }
-    if (w == 1) diag_inv8(A, Li, Dinv, T - 8);
+    inv_row(A, Li, Dinv, T / 8 - 1, w, 4, Tm + 64 * w);  // the last block row of the inverse
     __syncthreads();
-    // inverse by doubling, [[Ai,0],[B,Ci]]^-1 = [[Ai,0],[-Ci B Ai, Ci]]; the 8x8 diagonal
-    // inverses came from the panel steps.  Stage 8 on VALU (one output per thread):
-    {
-        const int p = 16 * (tid >> 6), a = (tid >> 3) & 7, b = tid & 7;
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < 8; m++)
-            if (m >= b) acc = fma(A[(p + 8 + a) * LD + p + m], Li[(p + m) * LD + p + b], acc);
-        Tm[(p + 8 + a) * LD + p + b] = acc;
-        __syncthreads();
-        acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < 8; m++)
-            if (m <= a) acc = fma(Li[(p + 8 + a) * LD + p + 8 + m], Tm[(p + 8 + m) * LD + p + b], acc);
-        Li[(p + 8 + a) * LD + p + b] = -acc;
-        __syncthreads();
-    }
-    // stage 16: pairs p = 0, 32 on waves 0, 1 (one 16x16 MFMA block each)
-    if (w < 2) {
-        const int p = 32 * w;
-        put_block(Tm, p + 16, p, block_mm<16>(A, p + 16, p, Li, p, p), 1.0);
-    }
-    __syncthreads();
-    if (w < 2) {
-        const int p = 32 * w;
-        put_block(Li, p + 16, p, block_mm<16>(Li, p + 16, p + 16, Tm, p + 16, p), -1.0);
-    }
-    __syncthreads();
-    // stage 32: the 32x32 off-diagonal block, one 16x16 block per wave
-    {
-        const int bi = w >> 1, bj = w & 1;
-        put_block(Tm, 32 + 16 * bi, 16 * bj, block_mm<32>(A, 32 + 16 * bi, 0, Li, 0, 16 * bj), 1.0);
-        __syncthreads();
-        put_block(Li, 32 + 16 * bi, 16 * bj, block_mm<32>(Li, 32 + 16 * bi, 32, Tm, 32, 16 * bj), -1.0);
-        __syncthreads();
-    }
     pstamp(17);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Column-cyclic LL^T + inverse of the 64x64 tile (M3S_DF_CC=1, default).  Wave w owns columns
+// 16w .. 16w+15, lane = row, in registers.  Column c is factored by its owner (pivot by
+// v_readlane, rsq + one Newton step, scale, then rank-1 updates of the owner's remaining
+// columns by v_readlane broadcasts: no LDS round trip and no barrier on the pivot chain) and
+// published to the LDS column buffer Lc[c][row] with a counter; the later waves apply each
+// published column to their own columns as it arrives (they trail the chain by one LDS hop and
+// catch up while the owner works, since an apply is cheaper than a factor step).  Measured
+// constants (tools/ubench_lat64.hip, gfx950): a dependent f64 VALU op ~5.5 cycles for one wave,
+// an LDS write -> read round trip ~131, a dependent f64 MFMA ~74, a balanced s_barrier ~13 --
+// the pivot chain of the 8-column panel steps (MFMA trailing update + LDS round trips + a barrier
+// per panel) cost ~3x this.
+// Each wave then inverts its 16x16 diagonal block, X_ww = [[X_a, 0], [X_ba, X_b]] (two 8x8
+// inverses, diag_inv8, and X_ba = -X_b L_ba X_a by VALU), and builds block column w of
+// Li = L^-1 (see step 3 below) while the later waves still factor.
+// sync (LDS ints): [0] columns published, [1 + w] X_ww written.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lds_wait_geq(int* p, int v, int* flags) {
+    int x, spins = 0;
+    while ((x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < v) {
+        __builtin_amdgcn_s_sleep(0);
+        if (++spins > (1 << 24)) {  // cannot happen (the producers are this workgroup's waves): fail, never hang
+            flags[kFlagFail] = 1;
+            return v;
+        }
+    }
+    asm volatile("" ::: "memory");
+    return x;
+}
+__device__ __forceinline__ void lds_publish(int* p, int v) {
+    asm volatile("" ::: "memory");  // the data stores first: a wave's LDS operations execute in order
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// X_ww (16x16 diagonal block of Li) by one wave: lanes 0-7 / 8-15 the two 8x8 inverses, then
+// X_ba = -X_b (L_ba X_a), lane = (r, c); scr: 64 doubles of this wave's LDS scratch
+__device__ __forceinline__ void diag_inv16(const double* A, double* Li, const double* Dinv, int c0, double* scr) {
+    const int lane = threadIdx.x & 63;
+    {
+        const int i = lane & 7, pb = c0 + (lane & 8);
+        if (lane < 16) {
+            double L[8][8], inv[8], x[8];
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                inv[m] = Dinv[pb + m];
+#pragma unroll
+                for (int k = 0; k < m; k++) L[m][k] = A[(pb + m) * LD + pb + k];
+            }
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                double s = m == i ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = 0; k < m; k++) s = fma(-L[m][k], x[k], s);
+                x[m] = m >= i ? s * inv[m] : 0.0;
+            }
+#pragma unroll
+            for (int m = 0; m < 8; m++) Li[(pb + m) * LD + pb + i] = x[m];
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int r = lane >> 3, c = lane & 7;
+    double t = 0.0;  // (L_ba X_a)[r][c]
+#pragma unroll
+    for (int m = 0; m < 8; m++) t = fma(A[(c0 + 8 + r) * LD + c0 + m], Li[(c0 + m) * LD + c0 + c], t);
+    scr[lane] = t;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    double x = 0.0;
+#pragma unroll
+    for (int m = 0; m < 8; m++) x = fma(Li[(c0 + 8 + r) * LD + c0 + 8 + m], scr[8 * m + c], x);
+    Li[(c0 + 8 + r) * LD + c0 + c] = -x;
+}
+
+constexpr int kCcScr = 4 * 64 + 4 * 16 * 17;  // LDS scratch of potrf_cc (doubles): per wave 64 + a 16x17 block
+template <int W>
+__device__ __forceinline__ void potrf_cc_w(double* A, double* Li, double* Lc, double* scratch, int* sync, double* Dinv,
+                                           int* flags, long long* pt) {
+    const int lane = threadIdx.x & 63;
+    constexpr int C0 = 16 * W;
+    auto wstamp = [&](int k) {
+#if M3S_DF_STAMPS
+        if (pt && lane == 0) pt[8 * W + k] = (long long)__builtin_amdgcn_s_memtime();
+#endif
+    };
+    wstamp(0);
+    double a[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) a[jj] = A[lane * LD + C0 + jj];
+    // 1. the earlier waves' columns, as they are published: two columns per half-iteration from
+    //    two register buffers, the next pair's LDS loads issued (after polling the counter, when
+    //    the backlog does not already cover them) before the current pair's FMAs.  A runtime
+    //    loop: unrolled, the scheduler hoists every load and spills.
+    if constexpr (W > 0) {
+        int avail = lds_wait_geq(sync, 2, flags);
+        double pa0, pa1, qa0[16], qa1[16], pb0, pb1, qb0[16], qb1[16];
+        auto load = [&](int c, double& p0, double& p1, double (&q0)[16], double (&q1)[16]) {
+            p0 = Lc[c * 64 + lane];
+            p1 = Lc[(c + 1) * 64 + lane];
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) {
+                q0[jj] = Lc[c * 64 + C0 + jj];
+                q1[jj] = Lc[(c + 1) * 64 + C0 + jj];
+            }
+        };
+        auto apply = [&](double p0, double p1, const double (&q0)[16], const double (&q1)[16]) {
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) a[jj] = fma(-p1, q1[jj], fma(-p0, q0[jj], a[jj]));
+        };
+        load(0, pa0, pa1, qa0, qa1);
+#pragma unroll 1
+        for (int c = 0; c < C0; c += 4) {
+            if (c + 4 > avail) avail = lds_wait_geq(sync, c + 4, flags);
+            load(c + 2, pb0, pb1, qb0, qb1);
+            apply(pa0, pa1, qa0, qa1);
+            if (c + 4 < C0) {
+                if (c + 6 > avail) avail = lds_wait_geq(sync, c + 6, flags);
+                load(c + 4, pa0, pa1, qa0, qa1);
+            }
+            apply(pb0, pb1, qb0, qb1);
+        }
+    }
+    wstamp(1);
+    // 2. the own columns: the pivot chain.  The next column's update by v_readlane (on the
+    //    chain); the later ones from the column just written to Lc (uniform LDS reads, off the chain)
+    double y[16];
+    bool bad = false;
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) {
+        const int c = C0 + jj;
+        const double d = rdlane(a[jj], c);
+        bad |= d <= 0.0;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
+        double r = __builtin_amdgcn_rsq(d);
+        r = r * fma(-0.5 * d * r, r, 1.5);
+        y[jj] = r;
+        a[jj] *= r;
+        Lc[c * 64 + lane] = a[jj];
+        if (W < 3) lds_publish(sync, c + 1);
+#if M3S_CC_OWNER_LDS
+        if (jj + 1 < 16) a[jj + 1] = fma(-a[jj], rdlane(a[jj], c + 1), a[jj + 1]);
+#pragma unroll
+        for (int q = jj + 2; q < 16; q++) a[q] = fma(-a[jj], Lc[c * 64 + C0 + q], a[q]);
+#else
+#pragma unroll
+        for (int q = jj + 1; q < 16; q++) a[q] = fma(-a[jj], rdlane(a[jj], C0 + q), a[q]);
+#endif
+    }
+    // L back into the tile (every lane: rows above the pivots write upper-triangle garbage,
+    // never read), 1 / l_pp for the inverse
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) A[lane * LD + C0 + jj] = a[jj];
+    if (lane == 0) {
+        if (bad) flags[kFlagFail] = 1;
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) Dinv[C0 + jj] = y[jj];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // 3. the inverse: X_WW (diagonal block), flagged; then block column W of X, column-oriented:
+    //    X_VW = -X_VV sum_{m=W}^{V-1} L_Vm X_mW for V > W -- the sums need only L (Lc) and this
+    //    wave's own earlier blocks, so each is ready before X_VV is flagged and the tail after the
+    //    last column is wave 3's X_33 plus one 16x16 product per column block
+    double* scr = scratch + 64 * W;               // this wave's scratch
+    double* sT = scratch + 4 * 64 + 16 * 17 * W;  // ... and its 16 x 17 block
+    wstamp(2);
+    diag_inv16(A, Li, Dinv, C0, scr);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_publish(sync + 1 + W, 1);
+    wstamp(3);
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int V = W + 1; V < 4; V++) {
+        lds_wait_geq(sync, 16 * V, flags);  // L_Vm, m < V: the columns of blocks < V published
+        d4 acc[4];
+#pragma unroll
+        for (int m = W; m < V; m++) {
+            acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int st = 0; st < 4; st++)
+                acc[m] = mfma(Lc[(16 * m + 4 * st + kq) * 64 + 16 * V + r16],
+                              Li[(16 * m + 4 * st + kq) * LD + C0 + r16], acc[m]);
+        }
+        d4 t = acc[W];
+#pragma unroll
+        for (int m = W + 1; m < V; m++) t += acc[m];
+#pragma unroll
+        for (int e = 0; e < 4; e++) sT[(kq + 4 * e) * 17 + r16] = t[e];
+        lds_wait_geq(sync + 1 + V, 1, flags);  // X_VV
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        d4 x = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 4; st++)
+            x = mfma(-Li[(16 * V + r16) * LD + 16 * V + 4 * st + kq], sT[(4 * st + kq) * 17 + r16], x);
+#pragma unroll
+        for (int e = 0; e < 4; e++) Li[(16 * V + kq + 4 * e) * LD + C0 + r16] = x[e];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // X_VW before the next V's sum reads it
+        wstamp(4 + V - W - 1);
+    }
+}
+
+// the column-cyclic factor + inverse of the tile (Li zeroed, sync[0..4] zeroed, both visible)
+__device__ __forceinline__ void potrf_cc(double* A, double* Li, double* Lc, double* scratch, int* sync, double* Dinv,
+                                         int* flags, long long* pt = nullptr) {
+    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+        case 0: potrf_cc_w<0>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        case 1: potrf_cc_w<1>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        case 2: potrf_cc_w<2>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        default: potrf_cc_w<3>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+    }
+    __syncthreads();
 }
 
 // Z (lower 16x16 blocks) -= X X^T, X: [64][LD] in LDS.  The 10 lower blocks are dealt 3/3/2/2 to
@@ -419,12 +637,71 @@ __device__ __forceinline__ void publish(const DfArgs& a, int idx) {
     if (threadIdx.x == 0) __hip_atomic_store(a.ready + idx, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Back-substitution task of tile column j (after the factor tasks in the helpers' lists, in
+// descending j): z_j = y_j - sum_{k>j} L_kj^T x_k, x_j = Linv_j^T z_j, published with a ready word
+// (xflag).  Each x_k is applied as soon as it is published, so when x_{j+1} arrives only its own
+// term, the sum and the Linv_j product are left: one hand-off + two 64x64 GEMVs per tile column on
+// the chain instead of the single-workgroup back-substitution's whole row panel per step (which
+// streamed all of L through one CU: 85 us on cfg4).  Thread (c, g): column c, rows 16g .. 16g+15 of
+// each tile; the 4 row-group partials are summed in fixed order (deterministic).  Every wait
+// targets a task earlier in some co-resident workgroup's list: no deadlock.
+__host__ __device__ inline int xflag(int nt, int j) { return (nt + 1) * nt + nt + j; }
+__device__ void back_task(const DfArgs& a, int j, double* S) {
+    const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
+    const int nt = a.nt;
+    const int64_t ld = a.npad;
+    double* sx = S;             // x_k (64)
+    double* sp = S + 64;        // partials [4][64]
+    double* sz = S + 64 + 256;  // z_j (64)
+    double acc = 0.0;
+    for (int k = nt - 1; k > j; k--) {
+        if (tid == 0) {
+            wait_ready(a.ready + k * nt + j, a.epoch, a.flags, a.spin_limit);  // L_kj final
+            wait_ready(a.ready + xflag(nt, k), a.epoch, a.flags, a.spin_limit);
+        }
+        __syncthreads();
+        const double* Lkj = a.Hd + (int64_t)k * T * ld + (int64_t)j * T;
+        double lv[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) lv[q] = ld_coh(Lkj + (int64_t)(16 * g + q) * ld + c);
+        if (tid < 64) sx[tid] = ld_coh(a.x + (int64_t)k * T + tid);
+        lds_barrier();
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc = fma(lv[q], sx[16 * g + q], acc);
+        lds_barrier();  // sx is rewritten by the next k
+    }
+    if (tid == 0) {
+        wait_ready(a.ready + nt * nt + j, a.epoch, a.flags, a.spin_limit);  // y_j (the border tile)
+        wait_ready(a.ready + j * nt + j, a.epoch, a.flags, a.spin_limit);   // Linv_j
+    }
+    sp[g * 64 + c] = acc;
+    __syncthreads();
+    if (tid < 64) {
+        const double y = ld_coh(a.Hd + (int64_t)ld * ld + (int64_t)j * T + c);
+        sz[c] = y - (((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c]);
+    }
+    const double* Lk = a.Linv + (int64_t)j * T * T;
+    double lv[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) lv[q] = ld_coh(Lk + (16 * g + q) * T + c);
+    lds_barrier();
+    double xp = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) xp = fma(lv[q], sz[16 * g + q], xp);
+    sp[g * 64 + c] = xp;
+    lds_barrier();
+    if (tid < 64) st_coh(a.x + (int64_t)j * T + c, ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c]);
+    publish(a, xflag(nt, j));
+}
+
 __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
     if (a.flags[kFlagDone]) return;  // written by earlier launches: all workgroups agree
     __shared__ __attribute__((aligned(16))) double X[T * LD];
     __shared__ __attribute__((aligned(16))) double Y[T * LD];
     __shared__ __attribute__((aligned(16))) double Z[T * LD];
     __shared__ double Dinv[T];
+    __shared__ double Scr[kCcScr];
+    __shared__ int Sync[8];
     const int tid = threadIdx.x;
     const int nt = a.nt;
     const int64_t ld = a.npad;
@@ -432,6 +709,12 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
     long long* ct = a.trace ? a.trace + 4 * a.ntiles + 32 : nullptr;  // C's per-step stamps
     auto cstamp = [&](int j, int slot) {
         if (ct && tid == 0) ct[4 * j + slot] = (long long)__builtin_amdgcn_s_memrealtime();
+    };
+    // M3S_DF_STAMPS (diagnostics): finer chain stamps after the P loads, L_{j,j-1}, the syrk
+    auto fstamp = [&](int j, int slot) {
+#if M3S_DF_STAMPS
+        if (ct && tid == 0) ct[4 * nt + 4 * j + slot] = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
     };
     if (blockIdx.x == 0) {
         // ---- the diagonal chain
@@ -446,6 +729,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 load_acc<false>(accd, tile(0, 0), ld);
                 acc_to_lds(Z, accd);
                 for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;
+                if (tid < 8) Sync[tid] = 0;
                 __syncthreads();
             } else {
                 d4 accs[4];
@@ -460,21 +744,33 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 publish(a, (j - 1) * nt + (j - 1));
                 acc_to_lds(X, accs);
                 acc_to_lds(Z, accd);
-                __syncthreads();
+                lds_barrier();
+                fstamp(j, 0);
 #pragma unroll
                 for (int J = 0; J < 4; J++) accs[J] = d4{0.0, 0.0, 0.0, 0.0};
                 gemm_nt<true>(X, Y, accs, 1.0);  // L_{j,j-1}
+                fstamp(j, 1);
                 store_acc_coh(tile(j, j - 1), ld, accs);
-                __syncthreads();
+                lds_barrier();  // the GEMM's reads of X and Y are done (the stores stay in flight)
                 acc_to_lds(X, accs);
                 for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;  // Linv_{j-1} read: Y -> the new Li
-                __syncthreads();
+                if (tid < 8) Sync[tid] = 0;
+                lds_barrier();
+                fstamp(j, 2);
                 syrk_lower(Z, X);  // A'_jj = P_d(j) - L_{j,j-1} L_{j,j-1}^T (lower blocks)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // L_{j,j-1}'s stores landed (long ago)
                 __syncthreads();
+                fstamp(j, 3);
             }
             cstamp(j, 1);
+#if M3S_DF_CC
+            if (j >= 1 && tid == 0)  // L_{j,j-1}: every wave waited for its stores before the barrier
+                __hip_atomic_store(a.ready + j * nt + (j - 1), a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            potrf_cc(Z, Y, X, Scr, Sync, Dinv, a.flags);  // X (L_{j,j-1}) is free: the column buffer
+#else
             potrf_inverse(Z, Y, X, Dinv, a.flags, a.trace && j == 0 ? a.trace + 4 * a.ntiles : nullptr,
                           j >= 1 ? a.ready + j * nt + (j - 1) : nullptr, a.epoch);
+#endif
             cstamp(j, 2);
             double* Lk = a.Linv + (int64_t)j * T * T;
 #pragma unroll
@@ -487,7 +783,12 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
         cstamp(nt - 1, 3);
         return;
     }
-    for (int t = blockIdx.x - 1; t < a.ntiles; t += gridDim.x - 1) {
+    const int ntasks = a.ntiles + (a.x != nullptr ? nt : 0);
+    for (int t = blockIdx.x - 1; t < ntasks; t += gridDim.x - 1) {
+        if (t >= a.ntiles) {
+            back_task(a, nt - 1 - (t - a.ntiles), X);
+            continue;
+        }
         int j = 0, rem = t;
         while (rem >= col_tasks(j, nt)) {
             rem -= col_tasks(j, nt);
@@ -557,11 +858,11 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
 
 size_t chol_ready_bytes(int npad) {
     const int nt = npad / T;
-    return sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + (size_t)nt);
+    return sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + 2 * (size_t)nt);  // tiles, H_j, x_j
 }
 
 hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
-                                int epoch, int* flags) {
+                                int epoch, int* flags, double* x) {
     static int maxg = 0;
     if (maxg == 0) {
         int dev = 0, ncu = 0, per = 0;
@@ -581,6 +882,7 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
     a.nt = npad / T;
     a.ntiles = num_tasks(a.nt);
     a.epoch = epoch;
+    a.x = x;
     // M3S_TEST_FORCE_TIMEOUT=1 (tests only): every ready wait gives up at once, to exercise the
     // timeout -> M3S_ERR_TIMEOUT path without a real hang
     const char* ft = getenv("M3S_TEST_FORCE_TIMEOUT");

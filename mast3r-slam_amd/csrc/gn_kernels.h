@@ -133,8 +133,10 @@ inline size_t chol_linv_bytes(int npad) {
 inline int* chol_ready_ptr(double* Linv, int npad) {
     return reinterpret_cast<int*>(Linv + (size_t)npad * kCholTile);
 }
+// x != nullptr: the back-substitution L^T x = y (y: the forward-substituted border row) runs as
+// dataflow tasks in the same launch
 hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
-                                int epoch, int* flags);
+                                int epoch, int* flags, double* x = nullptr);
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
                                      double* x, int* flags, int epoch);
 // multi-launch block-sparse elimination (gn_sparse.hip): one launch per round

@@ -610,8 +610,14 @@ hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, doubl
     if (df) {
         // a cooperative launch the device cannot hold (or refuses) falls back to the per-panel
         // launches below instead of failing the call
-        done = launch_chol_dataflow(st, npad, Hd, Linv, chol_ready_ptr(Linv, npad), epoch, flags) == hipSuccess;
+        // M3S_CHOL_DF_BACK=1 (default): the back-substitution runs in the same launch as dataflow
+        // tasks (chol_df.hip back_task); 0: chol_backsolve_kernel after it
+        const char* bk_env = getenv("M3S_CHOL_DF_BACK");
+        const bool in_launch = bk_env ? atoi(bk_env) != 0 : true;
+        done = launch_chol_dataflow(st, npad, Hd, Linv, chol_ready_ptr(Linv, npad), epoch, flags,
+                                    in_launch ? x : nullptr) == hipSuccess;
         if (!done) (void)hipGetLastError();
+        if (done && in_launch) return hipGetLastError();
     }
     if (!done) {
         for (int k = 0; k < nt; k++) {

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 4 step g: potrf_cc + in-launch back-substitution in the product path -- GN tests, cfg4/cfg3 bench
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_gn.py tests/test_gpu_gn_stress.py -s > gpurun_out/r04g_pytest_gn.log 2>&1 || { echo "pytest rc=$?"; tail -30 gpurun_out/r04g_pytest_gn.log; exit 1; }
+tail -3 gpurun_out/r04g_pytest_gn.log; grep "stress iters" gpurun_out/r04g_pytest_gn.log
+timeout -k 10 300 python bench.py --config cfg4 --steps 5 --warmup 2 --no-cpu-baseline --no-matching > gpurun_out/r04g_bench_cfg4.json 2> gpurun_out/r04g_bench_cfg4.err || { echo "bench rc=$?"; tail -5 gpurun_out/r04g_bench_cfg4.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/r04g_bench_cfg4.json')); print('cfg4', round(d['value']), d['ms_per_step'], d['phase_ms_per_iter'])"
+timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-matching --no-cfg4 > gpurun_out/r04g_bench_cfg3.json 2> gpurun_out/r04g_bench_cfg3.err || { echo "bench3 rc=$?"; tail -5 gpurun_out/r04g_bench_cfg3.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/r04g_bench_cfg3.json')); print('cfg3', round(d['value']), d['ms_per_step'], d['phase_ms_per_iter'])"

@@ -3,6 +3,7 @@
 // finished its updates, finished potrf + inverse and published, and the same for tile (j+1, j)
 // (the critical path is diag(j) -> trsm(j+1, j) -> last update of diag(j+1)).  Also checks
 // L L^T = A and the forward substitution against a host f64 Cholesky.
+#define M3S_DF_STAMPS 1
 #include "../mast3r-slam_amd/csrc/chol_df.hip"
 
 #include <cmath>
@@ -39,20 +40,21 @@ int main(int argc, char** argv) {
             H[(size_t)r * npad + c] = H[(size_t)c * npad + r] = s;
         }
     for (int c = 0; c < npad; c++) H[(size_t)npad * npad + c] = nd(rng);
-    double *dH, *dH0, *dLinv;
+    double *dH, *dH0, *dLinv, *dX;
     int *dflags;
     long long* dtr;
     const int ntiles = num_tasks(nt);
     CK(hipMalloc(&dH, H.size() * 8));
     CK(hipMalloc(&dH0, H.size() * 8));
     CK(hipMalloc(&dLinv, chol_linv_bytes(npad)));
+    CK(hipMalloc(&dX, npad * 8));
     CK(hipMalloc(&dflags, 64 * 4));
-    CK(hipMalloc(&dtr, (ntiles * 4 + 32 + 4 * nt) * 8));
-    CK(hipMemset(dtr, 0, (ntiles * 4 + 32 + 4 * nt) * 8));
+    CK(hipMalloc(&dtr, (ntiles * 4 + 32 + 8 * nt) * 8));
+    CK(hipMemset(dtr, 0, (ntiles * 4 + 32 + 8 * nt) * 8));
     CK(hipMemcpy(dH0, H.data(), H.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemset(dflags, 0, 64 * 4));
     CK(hipMemset(chol_ready_ptr(dLinv, npad), 0, chol_ready_bytes(npad)));
-    std::vector<long long> tr(ntiles * 4 + 32 + 4 * nt);
+    std::vector<long long> tr(ntiles * 4 + 32 + 8 * nt);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -69,6 +71,7 @@ int main(int argc, char** argv) {
         a.epoch = rep;
         a.spin_limit = 1 << 22;
         a.trace = dtr;
+        a.x = dX;
         int per = 0, ncu = 0;
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)chol_df_kernel, NT, 0));
         CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -92,6 +95,13 @@ int main(int argc, char** argv) {
         printf("col %2d  C %7.2f %7.2f %7.2f\n", j, (ct[4 * j] - t0) * 0.01, (ct[4 * j + 1] - t0) * 0.01,
                (ct[4 * j + 2] - t0) * 0.01);
     printf("C end %.2f\n", (ct[4 * (nt - 1) + 3] - t0) * 0.01);
+    printf("per column (us): P loads+staging / L_{j,j-1} GEMM / store+stage / syrk / potrf+inverse / to next\n");
+    for (int j = 1; j < nt; j++) {
+        const long long* f = ct + 4 * nt + 4 * j;
+        const long long nx = j + 1 < nt ? ct[4 * (j + 1)] : ct[4 * (nt - 1) + 3];
+        printf("col %2d  %6.2f %6.2f %6.2f %6.2f %6.2f %6.2f\n", j, (f[0] - ct[4 * j]) * 0.01, (f[1] - f[0]) * 0.01,
+               (f[2] - f[1]) * 0.01, (f[3] - f[2]) * 0.01, (ct[4 * j + 2] - f[3]) * 0.01, (nx - ct[4 * j + 2]) * 0.01);
+    }
     printf("potrf of D_0 (us since its start): ");
     for (int q = 1; q < 18; q++) printf("%.2f ", (tr[4 * ntiles + q] - tr[4 * ntiles]) * 0.01);
     printf("\n");
@@ -123,6 +133,21 @@ int main(int argc, char** argv) {
     for (int i = 64; i < npad; i++)
         for (int j = 0; j < (i / 64) * 64; j++)
             lerr = std::max(lerr, std::fabs(Hg[(size_t)i * npad + j] - L[(size_t)i * npad + j]));
+    {   // back-substitution L^T x = y
+        std::vector<double> x(npad), xg(npad);
+        for (int i = npad - 1; i >= 0; i--) {
+            double s = y[i];
+            for (int k = i + 1; k < npad; k++) s -= L[(size_t)k * npad + i] * x[k];
+            x[i] = s / L[(size_t)i * npad + i];
+        }
+        CK(hipMemcpy(xg.data(), dX, npad * 8, hipMemcpyDeviceToHost));
+        double ex = 0, mxx = 0;
+        for (int i = 0; i < npad; i++) {
+            ex = std::max(ex, std::fabs(xg[i] - x[i]));
+            mxx = std::max(mxx, std::fabs(x[i]));
+        }
+        printf("x max err %.3e (max |x| %.3e)\n", ex, mxx);
+    }
     int fl[64];
     CK(hipMemcpy(fl, dflags, sizeof(fl), hipMemcpyDeviceToHost));
     printf("y max err %.3e (max |y| %.3e), off-diagonal L max err %.3e, fail flag %d\n", err, mx, lerr, fl[kFlagFail]);
