@@ -30,9 +30,6 @@
 #ifndef M3S_DF_CC
 #define M3S_DF_CC 1  // 1: the column-cyclic tile factor (potrf_cc); 0: the 8-column panel steps (potrf_inverse)
 #endif
-#ifndef M3S_CC_OWNER_LDS
-#define M3S_CC_OWNER_LDS 1  // potrf_cc owner: later columns' updates from the LDS column (1) or all by v_readlane (0)
-#endif
 #ifndef M3S_DF_STAMPS
 #define M3S_DF_STAMPS 0  // diagnostics (tools/ubench_potrf64.hip): cycle stamps inside the potrf steps
 #endif
@@ -295,7 +292,7 @@ __device__ __forceinline__ void trail_blocks(double* A, int c0, const int (&I)[N
     if (w == 0) panel_factor(A, Dinv, 0, flags);
     if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (early && tid == 0) __hip_atomic_store(early, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (early && tid == 0) __hip_atomic_store(early, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pstamp(1);
 #pragma unroll
     for (int s = 0; s + 1 < T / 8; s++) {
@@ -406,7 +403,9 @@ __device__ __forceinline__ void diag_inv16(const double* A, double* Li, const do
     Li[(c0 + 8 + r) * LD + c0 + c] = -x;
 }
 
-constexpr int kCcScr = 4 * 64 + 4 * 16 * 17;  // LDS scratch of potrf_cc (doubles): per wave 64 + a 16x17 block
+// LDS scratch of potrf_cc (doubles): per wave 64 + a 16x17 block, then per wave a [64][4] batch
+constexpr int kCcScrBase = 4 * 64 + 4 * 16 * 17;
+constexpr int kCcScr = kCcScrBase + 4 * 256;
 template <int W>
 __device__ __forceinline__ void potrf_cc_w(double* A, double* Li, double* Lc, double* scratch, int* sync, double* Dinv,
                                            int* flags, long long* pt) {
@@ -455,29 +454,49 @@ __device__ __forceinline__ void potrf_cc_w(double* A, double* Li, double* Lc, do
         }
     }
     wstamp(1);
-    // 2. the own columns: the pivot chain.  The next column's update by v_readlane (on the
-    //    chain); the later ones from the column just written to Lc (uniform LDS reads, off the chain)
+    // 2. the own columns: the pivot chain, in batches of 4 columns.  Inside a batch each pivot
+    //    updates the batch's later columns by v_readlane (on the chain); after a batch, its
+    //    rank-4 update of the wave's remaining columns reads the 4 values of each target row from
+    //    a row-major copy of the batch (two uniform ds_read_b128 + 4 FMAs per column instead of
+    //    4 x (2 v_readlane + FMA): the owner's issue is what bounds its per-column time)
     double y[16];
     bool bad = false;
+    double* Lr = scratch + kCcScrBase + 256 * W;  // this wave's batch, row-major [64][4]
 #pragma unroll
-    for (int jj = 0; jj < 16; jj++) {
-        const int c = C0 + jj;
-        const double d = rdlane(a[jj], c);
-        bad |= d <= 0.0;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
-        double r = __builtin_amdgcn_rsq(d);
-        r = r * fma(-0.5 * d * r, r, 1.5);
-        y[jj] = r;
-        a[jj] *= r;
-        Lc[c * 64 + lane] = a[jj];
-        if (W < 3) lds_publish(sync, c + 1);
-#if M3S_CC_OWNER_LDS
-        if (jj + 1 < 16) a[jj + 1] = fma(-a[jj], rdlane(a[jj], c + 1), a[jj + 1]);
+    for (int ib = 0; ib < 4; ib++) {
 #pragma unroll
-        for (int q = jj + 2; q < 16; q++) a[q] = fma(-a[jj], Lc[c * 64 + C0 + q], a[q]);
-#else
+        for (int p = 0; p < 4; p++) {
+            const int jj = 4 * ib + p, c = C0 + jj;
+            const double d = rdlane(a[jj], c);
+            bad |= d <= 0.0;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
+            double r = __builtin_amdgcn_rsq(d);
+            r = r * fma(-0.5 * d * r, r, 1.5);
+            y[jj] = r;
+            a[jj] *= r;
+            if (W < 3) {
+                Lc[c * 64 + lane] = a[jj];
+                lds_publish(sync, c + 1);
+            }
 #pragma unroll
-        for (int q = jj + 1; q < 16; q++) a[q] = fma(-a[jj], rdlane(a[jj], C0 + q), a[q]);
-#endif
+            for (int q = p + 1; q < 4; q++) a[4 * ib + q] = fma(-a[jj], rdlane(a[jj], C0 + 4 * ib + q), a[4 * ib + q]);
+        }
+        if (ib < 3) {
+            const int NQ = 12 - 4 * ib;  // this batch's target columns: all loaded, then used
+#pragma unroll
+            for (int p = 0; p < 4; p++) Lr[lane * 4 + p] = a[4 * ib + p];
+            double v[12][4];
+#pragma unroll
+            for (int q = 0; q < 12; q++)
+                if (q < NQ) {
+#pragma unroll
+                    for (int p = 0; p < 4; p++) v[q][p] = Lr[(C0 + 4 * ib + 4 + q) * 4 + p];
+                }
+#pragma unroll
+            for (int q = 0; q < 12; q++)
+                if (q < NQ)
+#pragma unroll
+                for (int p = 0; p < 4; p++) a[4 * ib + 4 + q] = fma(-a[4 * ib + p], v[q][p], a[4 * ib + 4 + q]);
+        }
     }
     // L back into the tile (every lane: rows above the pivots write upper-triangle garbage,
     // never read), 1 / l_pp for the inverse
@@ -630,11 +649,14 @@ __device__ __forceinline__ void store_acc_coh(double* dst, int64_t ld, const d4 
 #pragma unroll
         for (int e = 0; e < 4; e++) st_coh(dst + (int64_t)(16 * w + (lane >> 4) + 4 * e) * ld + 16 * J + (lane & 15), acc[J][e]);
 }
-// after this workgroup's write-through stores landed, set a ready word
+// after this workgroup's write-through stores landed, set a ready word.  Every handed-off byte
+// is stored write-through (sc1) and loaded sc1, and every storing wave waits for its stores
+// before the barrier, so the flag is a relaxed sc1 store: no release fence (an L2 write-back,
+// ~1.7 us per hand-off; MI355X_MICROARCH.md, "Valid forms", first row of the hand-off table)
 __device__ __forceinline__ void publish(const DfArgs& a, int idx) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(a.ready + idx, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(a.ready + idx, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Back-substitution task of tile column j (after the factor tasks in the helpers' lists, in
@@ -653,41 +675,52 @@ __device__ void back_task(const DfArgs& a, int j, double* S) {
     double* sx = S;             // x_k (64)
     double* sp = S + 64;        // partials [4][64]
     double* sz = S + 64 + 256;  // z_j (64)
-    double acc = 0.0;
+    auto Ltile = [&](int k) { return a.Hd + (int64_t)k * T * ld + (int64_t)j * T; };
+    // the tiles this task reads are final long before the x chain reaches it: their words are
+    // checked one step ahead and each tile is loaded while the previous x_k is awaited
+    double acc = 0.0, lv[16], li[16];
+    if (tid == 0) {
+        wait_ready(a.ready + j * nt + j, a.epoch, a.flags, a.spin_limit);  // Linv_j
+        if (j + 1 < nt) wait_ready(a.ready + (nt - 1) * nt + j, a.epoch, a.flags, a.spin_limit);
+    }
+    __syncthreads();
+    const double* Lk = a.Linv + (int64_t)j * T * T;
+#pragma unroll
+    for (int q = 0; q < 16; q++) li[q] = ld_coh(Lk + (16 * g + q) * T + c);
+    if (j + 1 < nt) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) lv[q] = ld_coh(Ltile(nt - 1) + (int64_t)(16 * g + q) * ld + c);
+    }
     for (int k = nt - 1; k > j; k--) {
         if (tid == 0) {
-            wait_ready(a.ready + k * nt + j, a.epoch, a.flags, a.spin_limit);  // L_kj final
             wait_ready(a.ready + xflag(nt, k), a.epoch, a.flags, a.spin_limit);
+            if (k - 1 > j) wait_ready(a.ready + (k - 1) * nt + j, a.epoch, a.flags, a.spin_limit);
         }
         __syncthreads();
-        const double* Lkj = a.Hd + (int64_t)k * T * ld + (int64_t)j * T;
-        double lv[16];
-#pragma unroll
-        for (int q = 0; q < 16; q++) lv[q] = ld_coh(Lkj + (int64_t)(16 * g + q) * ld + c);
         if (tid < 64) sx[tid] = ld_coh(a.x + (int64_t)k * T + tid);
+        double cur[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) cur[q] = lv[q];
+        if (k - 1 > j) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) lv[q] = ld_coh(Ltile(k - 1) + (int64_t)(16 * g + q) * ld + c);
+        }
         lds_barrier();
 #pragma unroll
-        for (int q = 0; q < 16; q++) acc = fma(lv[q], sx[16 * g + q], acc);
+        for (int q = 0; q < 16; q++) acc = fma(cur[q], sx[16 * g + q], acc);
         lds_barrier();  // sx is rewritten by the next k
     }
-    if (tid == 0) {
-        wait_ready(a.ready + nt * nt + j, a.epoch, a.flags, a.spin_limit);  // y_j (the border tile)
-        wait_ready(a.ready + j * nt + j, a.epoch, a.flags, a.spin_limit);   // Linv_j
-    }
+    if (tid == 0) wait_ready(a.ready + nt * nt + j, a.epoch, a.flags, a.spin_limit);  // y_j (the border tile)
     sp[g * 64 + c] = acc;
     __syncthreads();
     if (tid < 64) {
         const double y = ld_coh(a.Hd + (int64_t)ld * ld + (int64_t)j * T + c);
         sz[c] = y - (((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c]);
     }
-    const double* Lk = a.Linv + (int64_t)j * T * T;
-    double lv[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) lv[q] = ld_coh(Lk + (16 * g + q) * T + c);
     lds_barrier();
     double xp = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; q++) xp = fma(lv[q], sz[16 * g + q], xp);
+    for (int q = 0; q < 16; q++) xp = fma(li[q], sz[16 * g + q], xp);
     sp[g * 64 + c] = xp;
     lds_barrier();
     if (tid < 64) st_coh(a.x + (int64_t)j * T + c, ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c]);
@@ -765,7 +798,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             cstamp(j, 1);
 #if M3S_DF_CC
             if (j >= 1 && tid == 0)  // L_{j,j-1}: every wave waited for its stores before the barrier
-                __hip_atomic_store(a.ready + j * nt + (j - 1), a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.ready + j * nt + (j - 1), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             potrf_cc(Z, Y, X, Scr, Sync, Dinv, a.flags);  // X (L_{j,j-1}) is free: the column buffer
 #else
             potrf_inverse(Z, Y, X, Dinv, a.flags, a.trace && j == 0 ? a.trace + 4 * a.ntiles : nullptr,
