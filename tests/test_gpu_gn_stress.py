@@ -11,10 +11,14 @@ more than the 1e-5 tolerance).
 
 Asserted after 1, 3 and 10 iterations, against the CPU oracle (the reference backend restated,
 its fp32 chains in the reference kernels' order, the reference build's FMA contraction):
-  * the default (fast) path within max(1e-5, 4 sigma) of the oracle, sigma = the oracle's own
-    distance from the same float terms summed in double (the reference order's rounding noise;
-    the fast path sums in another order, so it cannot land closer than that to the oracle), and
-    within 1e-5 of the exactly summed system;
+  * the default (fast) path within its MEASURED distance from the oracle plus a 1.5x margin
+    (MEASURED_D_ORACLE; measured on MI355X in round 4, profiles/r04_stress_measured.json -- the op
+    is deterministic, so the distance only moves when its summation order or formulas change),
+    and within 1e-5 of the exactly summed system.  sigma = the oracle's own distance from the
+    same float terms summed in double (the reference order's rounding noise) is printed beside
+    it: the fast path sums in another order, so it cannot land closer than ~sigma to the oracle
+    (measured: 1 iteration 2.1e-5 from the oracle with sigma 2.05e-5, but 6.2e-6 from the exact
+    sums -- closer to the exactly summed system than the reference order is);
   * the reference-order mode (gn_refacc.hip) within max(1e-6, sigma / 10) of the oracle: the
     same formulas in the same order, so what remains -- the f64 solve's summation order and an
     ulp of sin / cos / exp / log -- is orders of magnitude below the fp32 summation noise sigma
@@ -31,6 +35,8 @@ pytestmark = pytest.mark.gpu
 
 LOCAL = dict(sigma_pixel=1.0, sigma_depth=10.0, C_conf=0.0, Q_conf=1.5, pixel_border=-10, depth_eps=1e-6)
 STRESS = dict(init_perturb=(10.0, 0.25, 0.1), outlier_frac=0.10)
+# measured fast-path distance from the oracle (max relative pose error), MI355X, round 4
+MEASURED_D_ORACLE = {1: 2.09e-5, 3: 2.41e-5, 10: 1.59e-6}
 
 
 def _rel(a, b):
@@ -111,7 +117,7 @@ def test_stress_graph_default_path_within_tolerance_of_oracle(backend, oracle, s
     d_o, d_x = _rel(T_g, T_o), _rel(T_g, T_x)
     print(f"stress iters={iters}: fast vs oracle {d_o:.2e}, fast vs exact {d_x:.2e}, sigma {sigma:.2e}")
     assert np.isfinite(T_g).all()
-    assert d_o <= max(1e-5, 4 * sigma), (d_o, sigma)
+    assert d_o <= 1.5 * MEASURED_D_ORACLE[iters], (d_o, sigma)
     assert d_x <= 1e-5, d_x
 
 
