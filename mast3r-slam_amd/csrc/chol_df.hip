@@ -921,8 +921,20 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
     const char* ft = getenv("M3S_TEST_FORCE_TIMEOUT");
     a.spin_limit = (ft && atoi(ft) != 0) ? -1 : (1 << 22);
     const int grid = 1 + a.ntiles < maxg ? 1 + a.ntiles : maxg;  // workgroup 0 = the diagonal chain
+    // A plain launch of a grid the occupancy query admits (one workgroup per CU here: 131 KB of
+    // LDS) gives the same residency as a cooperative one (MI355X_MICROARCH.md, "Residency and
+    // cooperative launch") without its per-launch host cost and without the ROCm 7.2 exit-time
+    // fault of a process that made a cooperative launch (profiles/r03_exit_fault).  Should the
+    // device ever not hold the whole grid (another kernel occupying CUs), the bounded ready waits
+    // fail the solve with M3S_ERR_TIMEOUT instead of hanging.  M3S_CHOL_COOP=1: cooperative.
+    static const bool coop = [] {
+        const char* e = getenv("M3S_CHOL_COOP");
+        return e && atoi(e) != 0;
+    }();
     void* kargs[] = {&a};
-    return hipLaunchCooperativeKernel((const void*)chol_df_kernel, dim3(grid), dim3(NT), kargs, 0, st);
+    if (coop) return hipLaunchCooperativeKernel((const void*)chol_df_kernel, dim3(grid), dim3(NT), kargs, 0, st);
+    hipLaunchKernelGGL(chol_df_kernel, dim3(grid), dim3(NT), 0, st, a);
+    return hipGetLastError();
 }
 
 }  // namespace m3s

@@ -9,6 +9,13 @@
 // canonicalisation may commute the operands.  M3S_CONTRACT_OFF is plain IEEE multiply then add
 // (the round-1/2 convention, `-ffp-contract=off`).  DESIGN.md §2 records the residual ambiguity.
 //
+// UNVERIFIED ASSUMPTION (parity unpinned): which products nvcc fuses is inferred from LLVM's and
+// NVPTX's public combines; NVVM itself is closed, nvcc is not in this image and the reference
+// ships no kernel-output fixtures, so nothing pins the default convention to the reference
+// build's real bits.  The oracle restates the same guess, so "bit-exact vs the oracle in the
+// NVCC convention" proves the kernels implement the convention, not that the convention is
+// nvcc's.  All three conventions stay selectable and tested; the default is the best guess.
+//
 // Each helper turns contraction off in its own body, so the OFF variant stays unfused in any
 // translation unit; code around the helpers follows its file's own -ffp-contract (the parity
 // files are compiled with contraction OFF, so these helpers are their only fused operations).

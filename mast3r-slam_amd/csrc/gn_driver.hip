@@ -1435,6 +1435,20 @@ int run(const m3s_gn_args& a) {
         M3S_REQUIRE(hf != nullptr, "gauss_newton: pinned host allocation failed");
         M3S_HIP_CHECK(hipMemcpyAsync(hf, flags + kFlagTimeout, sizeof(int), hipMemcpyDeviceToHost, c.st));
         M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+        if (a.comm) {
+            // edge-sharded: every rank ran the same replicated solve, but the flag is rank-local --
+            // OR it over the ranks (a sum of 0 / 1) so that all fail together instead of one rank
+            // returning the error while the others go on to their next collective
+            double* hv = reinterpret_cast<double*>(hf) + 1;
+            double* dv = c.at<double>(L.x);  // the solution buffer is free once the call retracted
+            hv[0] = hf[0] != 0 ? 1.0 : 0.0;
+            M3S_HIP_CHECK(hipMemcpyAsync(dv, hv, sizeof(double), hipMemcpyHostToDevice, c.st));
+            rc = comm_allreduce_sum_f64(a.comm, dv, 1, c.st);
+            if (rc) return rc;
+            M3S_HIP_CHECK(hipMemcpyAsync(hv, dv, sizeof(double), hipMemcpyDeviceToHost, c.st));
+            M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+            hf[0] = hv[0] > 0.0 ? 1 : 0;
+        }
         if (hf[0] != 0) {
             set_error("gauss_newton: a device-side wait of the factorisation timed out (the solve "
                       "was discarded; not a singular system)");

@@ -91,12 +91,15 @@ __device__ __forceinline__ void cross_inplace(const float* a, float* b) {
     b[0] = x0; b[1] = x1; b[2] = x2;
 }
 
-// The Sim(3) exponential's float transcendentals, correctly rounded (evaluated in double and
-// rounded once; oracle/m3s_oracle.c does the same).  The reference's CUDA expf / sinf / cosf are
-// <= 2 ulp and platform-specific, and its float formulas amplify one ulp of them enormously --
-// C = (expf(sigma) - 1) / sigma moves by ulp(1) / sigma (~1 % at sigma = 1e-5, i.e. ~1e-5 of a
-// pose after a first GN step) -- so no other platform can reproduce its bits there; with
-// correctly rounded values the op and the oracle retract the same step to the same bits.
+// The Sim(3) exponential's float transcendentals, evaluated in double and rounded once to float
+// (oracle/m3s_oracle.c does the same).  That is correctly rounded except in rare double-rounding
+// cases: ocml's and glibc's double exp / sin / cos are ~1 ulp in double, not correctly rounded,
+// so when the double result lies within ~1 double ulp of a float rounding boundary the GPU and
+// the oracle may round to adjacent floats (a 1-ulp difference of the retraction, not observed on
+// any test graph).  The reference's CUDA expf / sinf / cosf are <= 2 ulp and platform-specific,
+// and its float formulas amplify one ulp of them enormously -- C = (expf(sigma) - 1) / sigma
+// moves by ulp(1) / sigma (~1 % at sigma = 1e-5, i.e. ~1e-5 of a pose after a first GN step) --
+// so no other platform can reproduce its bits there.
 __device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float sinf_cr(float x) { return (float)sin((double)x); }
 __device__ __forceinline__ float cosf_cr(float x) { return (float)cos((double)x); }
