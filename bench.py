@@ -307,6 +307,7 @@ def time_config(cfg, iters_arg, steps, warmup, world, rank, rehearse, dev, comm)
     step()
     torch.cuda.synchronize()
     del os.environ["M3S_GN_DEBUG_FLAGS"]
+    mb.gn_check()  # a timed-out factorisation is reported by the next call or here (deferred)
     dbg = (ctypes.c_int * 4)()
     mb.lib.m3s_gn_debug_flags(dbg)
     if world > 1:

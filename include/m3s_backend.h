@@ -126,6 +126,13 @@ int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D1
  * ray-constrained calib accumulate (Xj read as its depth)} of the last such call. */
 void m3s_gn_debug_flags(int* out4);
 
+/* Deferred error report.  A GN call whose solver has bounded device-side waits (the dataflow
+ * factorisation) exports its timeout flag without a host wait; M3S_ERR_TIMEOUT for it is
+ * returned by the next GN call on the same host thread (before it does any work) or by this
+ * function, which synchronises `stream` (hipStream_t) first.  Env M3S_GN_TIMEOUT_SYNC=1 reports it
+ * from the call itself.  Returns M3S_OK, M3S_ERR_TIMEOUT (then cleared) or M3S_ERR_HIP. */
+int m3s_gn_check(void* stream);
+
 enum { M3S_GN_POINTS = 0, M3S_GN_RAYS = 1, M3S_GN_CALIB = 2 };
 
 /*

@@ -167,11 +167,15 @@ struct Stagings {
     Staging in;   // D2H
     Staging out;  // H2D: the sparse solver's plan
     Staging ws;   // H2D: the workspace's plan (CSR lists, schedule)
+    Staging tmo;  // D2H: the last call's timeout flag (deferred report, see take_deferred_timeout)
+    int tmo_armed = 0;  // 0: nothing to report; 1: tmo holds an int flag; 2: a double (rank sum)
     static void release(void* p) {
         Stagings* s = static_cast<Stagings*>(p);
         Staging::release(&s->in);
         Staging::release(&s->out);
         Staging::release(&s->ws);
+        Staging::release(&s->tmo);
+        s->tmo_armed = 0;
     }
 };
 thread_local Stagings* t_stagings = nullptr;
@@ -1301,6 +1305,27 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
             M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_inl), R.tbeg + R.rbeg, R.nbt, R.nrt,
                                           sp.iptr(sp.i_tc3), sp.iptr(sp.i_rc4), A, b, Ls, W, y, flags));
     }
+    // M3S_HYB_CORE=1 (default): the hybrid's dense core (<= 27 poses) is factored and solved by
+    // the dataflow launch (chol_df.hip: column-cyclic tile factor, ~150 ns per column on the
+    // pivot chain, back-substitution in the same launch) instead of gn_solve's in-register pose
+    // steps (~330-430 ns per column); gn_solve then only back-substitutes through the rounds
+    // and retracts.  0: the in-register core.
+    static const bool core_df = env_int("M3S_HYB_CORE", 1) != 0;
+    if (sp.hybrid && core_df && !coop && sp.ntail > 0) {
+        c.may_timeout = true;  // chol_df's bounded waits
+        M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
+                                     sp.npad_tail, sp.dptr<double>(sp.o_dense), sp.dptr<double>(sp.o_linv),
+                                     sp.dptr<double>(sp.o_xd), x, flags, ++c.chol_epoch));
+        S.Hd = nullptr;
+        S.nmeta = (int)sp.nints_back;
+        S.meta_lds = 1;
+        S.do_fwd = 0;
+        S.do_tail = 0;
+        S.do_back = 1;
+        S.x_tail_global = 1;
+        M3S_HIP_CHECK(launch_gn_solve_dbg(c.st, S));
+        return M3S_OK;
+    }
     if (sp.hybrid) {
         // the <= 27-pose core in registers, the back-substitution through the rounds and the
         // retraction: one single-workgroup launch (gn_solve.hip) reading the plan prefix; the
@@ -1330,6 +1355,23 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     return M3S_OK;
 }
 
+// The deferred timeout report of this thread's last gauss_newton call (waits for its flag copy):
+// M3S_ERR_TIMEOUT once, then cleared.
+int take_deferred_timeout(const char* which) {
+    Stagings& sg = stagings();
+    if (!sg.tmo_armed) return M3S_OK;
+    const int kind = sg.tmo_armed;
+    sg.tmo_armed = 0;
+    const char* h = sg.tmo.get(64);  // waits for the copy (its event)
+    const bool hit = kind == 2 ? *reinterpret_cast<const double*>(h) > 0.0 : *reinterpret_cast<const int*>(h) != 0;
+    if (hit) {
+        set_error("gauss_newton: %sa device-side wait of the factorisation timed out (the solve was "
+                  "discarded; not a singular system)", which);
+        return M3S_ERR_TIMEOUT;
+    }
+    return M3S_OK;
+}
+
 int run(const m3s_gn_args& a) {
     // M3S_PROF_HOST: host-side phase times of the call (stderr)
     static const bool prof_host = env_int("M3S_PROF_HOST", 0) != 0;
@@ -1343,6 +1385,9 @@ int run(const m3s_gn_args& a) {
     // the packed stream is launched inside setup as soon as its inputs are on the device: the
     // GPU builds it while the host plans the accumulate schedule and the elimination
     int rc = setup(a, c, a.N > 1);
+    if (rc) return rc;
+    // an earlier call's timeout (its copy has landed: setup synchronised the stream)
+    rc = take_deferred_timeout("an earlier call: ");
     if (rc) return rc;
     const auto t1 = now();
     const int npose = (int)(a.N - 1);
@@ -1429,30 +1474,38 @@ int run(const m3s_gn_args& a) {
     }
     // (the per-call solver buffers are released by ~Ctx on this and every error path)
     if (c.may_timeout && a.max_iter > 0) {
-        // a bounded device-side wait that gave up discarded that iteration's solve (dx = 0): an
-        // error, not a singular system (the reference's host Eigen solve cannot time out)
-        int* hf = reinterpret_cast<int*>(stagings().in.get(64));
-        M3S_REQUIRE(hf != nullptr, "gauss_newton: pinned host allocation failed");
-        M3S_HIP_CHECK(hipMemcpyAsync(hf, flags + kFlagTimeout, sizeof(int), hipMemcpyDeviceToHost, c.st));
-        M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+        // A bounded device-side wait that gave up discarded that iteration's solve (dx = 0): an
+        // error, not a singular system (the reference's host Eigen solve cannot time out).  The
+        // flag leaves the device without a host wait (a kernel writes it to pinned memory): the
+        // error is reported by the next call on this thread or by m3s_gn_check, like an
+        // asynchronous kernel fault.  Waiting here instead left the GPU idle between calls for
+        // the host's per-call work (cfg3: 694 vs 318 us call-to-call gap, rocprofv3 trace).
+        // M3S_GN_TIMEOUT_SYNC=1: report it from this call (one stream synchronisation).
+        Stagings& sg = stagings();
+        char* h = sg.tmo.get(64);
+        M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
         if (a.comm) {
             // edge-sharded: every rank ran the same replicated solve, but the flag is rank-local --
             // OR it over the ranks (a sum of 0 / 1) so that all fail together instead of one rank
             // returning the error while the others go on to their next collective
-            double* hv = reinterpret_cast<double*>(hf) + 1;
             double* dv = c.at<double>(L.x);  // the solution buffer is free once the call retracted
-            hv[0] = hf[0] != 0 ? 1.0 : 0.0;
-            M3S_HIP_CHECK(hipMemcpyAsync(dv, hv, sizeof(double), hipMemcpyHostToDevice, c.st));
+            M3S_HIP_CHECK(launch_flag_export(c.st, flags + kFlagTimeout, dv, 1));
             rc = comm_allreduce_sum_f64(a.comm, dv, 1, c.st);
             if (rc) return rc;
-            M3S_HIP_CHECK(hipMemcpyAsync(hv, dv, sizeof(double), hipMemcpyDeviceToHost, c.st));
-            M3S_HIP_CHECK(hipStreamSynchronize(c.st));
-            hf[0] = hv[0] > 0.0 ? 1 : 0;
+            M3S_HIP_CHECK(sg.tmo.dev ? launch_stage_copy(c.st, sg.tmo.dev, dv, sizeof(double))
+                                     : hipMemcpyAsync(h, dv, sizeof(double), hipMemcpyDeviceToHost, c.st));
+            sg.tmo_armed = 2;
+        } else {
+            M3S_HIP_CHECK(sg.tmo.dev ? launch_flag_export(c.st, flags + kFlagTimeout, sg.tmo.dev, 0)
+                                     : hipMemcpyAsync(h, flags + kFlagTimeout, sizeof(int),
+                                                      hipMemcpyDeviceToHost, c.st));
+            sg.tmo_armed = 1;
         }
-        if (hf[0] != 0) {
-            set_error("gauss_newton: a device-side wait of the factorisation timed out (the solve "
-                      "was discarded; not a singular system)");
-            return M3S_ERR_TIMEOUT;
+        M3S_HIP_CHECK(sg.tmo.mark(c.st));
+        static const bool sync_report = env_int("M3S_GN_TIMEOUT_SYNC", 0) != 0;
+        if (sync_report) {
+            rc = take_deferred_timeout("");
+            if (rc) return rc;
         }
     }
     if (const int dbg = env_int("M3S_GN_DEBUG_FLAGS", 0)) {  // diagnostics: the device flags after the call
@@ -1477,6 +1530,15 @@ int run(const m3s_gn_args& a) {
 using namespace m3s;
 
 extern "C" const char* m3s_last_error(void) { return m3s::get_error(); }
+
+extern "C" int m3s_gn_check(void* stream) {
+    const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) {
+        set_error("gn_check: %s", hipGetErrorString(e));
+        return M3S_ERR_HIP;
+    }
+    return m3s::take_deferred_timeout("");
+}
 
 extern "C" void m3s_gn_debug_flags(int* out4) {
     for (int k = 0; k < 4; k++) out4[k] = m3s::g_dbg_flags[k];

@@ -204,6 +204,8 @@ struct SolveArgs {
                                    // driver prints them (no printf call in the kernel: a call
                                    // gives it a stack frame)
     int contract;                  // the retraction's M3S_CONTRACT_* (m3s_gn_args.contract)
+    int x_tail_global;             // the dense core was solved by its own launch (chol_df): its x
+                                   // is read from x (pose-indexed) before the back rounds
 };
 size_t solve_lds_bytes(int nmeta_lds);
 int solve_max_poses();  // x stays in LDS: the single-workgroup solve takes at most this many poses
@@ -213,6 +215,8 @@ hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
 // copy `bytes` (a multiple of 4; both addresses 16-B aligned) from pinned host memory (its
 // device address) to device memory, stream-ordered, by a kernel
 hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes);
+// flag[0] != 0 as an int (as_f64 = 0) or a double (as_f64 = 1) at dst (device-accessible)
+hipError_t launch_flag_export(hipStream_t st, const int* flag, void* dst, int as_f64);
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
                           float delta_thresh, int* flags, int contract);
 

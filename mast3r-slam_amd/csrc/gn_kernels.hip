@@ -560,9 +560,24 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(const uint32_t* __restr
     for (int64_t i = 4 * n16 + t0; i < n4; i += stride) dst[i] = src[i];
 }
 
+// The call's timeout flag, exported without a host wait: as an int (to pinned host memory, by
+// its device address) or as 0.0 / 1.0 (a device word the ranks then sum).
+__global__ void flag_export_kernel(const int* __restrict__ flag, void* dst, int as_f64) {
+    if (threadIdx.x == 0) {
+        const int v = flag[0] != 0 ? 1 : 0;
+        if (as_f64) *static_cast<double*>(dst) = (double)v;
+        else *static_cast<int*>(dst) = v;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // launchers (host)
 // ---------------------------------------------------------------------------
+
+hipError_t launch_flag_export(hipStream_t st, const int* flag, void* dst, int as_f64) {
+    hipLaunchKernelGGL(flag_export_kernel, dim3(1), dim3(64), 0, st, flag, dst, as_f64);
+    return hipGetLastError();
+}
 
 hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes) {
     if (bytes == 0) return hipSuccess;

@@ -759,6 +759,15 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
     if (a.do_back) {
         constexpr int NG = NW * kGroups;
         const int gid = wave * kGroups + g;
+        if (a.x_tail_global && a.ntail > 0) {
+            // the core's x from the dense dataflow launch (sp_tail_scatter wrote it pose-indexed)
+            const int* __restrict__ Mtail = M + a.o_tail;
+            for (int i = tid; i < 7 * a.ntail; i += NT) {
+                const int o = Mtail[i / 7] * 7 + i % 7;
+                sX[o] = a.x[o];
+            }
+            lds_barrier();
+        }
         double* __restrict__ sPart = smem + kOffPn;  // tail scratch, free once the tail is done
         static_assert(NG * 7 <= kOffZ - kOffPn, "back-round partials exceed the tail scratch");
         for (int rd = a.nrounds - 1; rd >= 0; rd--) {

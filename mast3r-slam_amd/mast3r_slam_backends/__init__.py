@@ -128,6 +128,7 @@ class GNArgs(ctypes.Structure):
 
 
 lib.m3s_gauss_newton.argtypes = [ctypes.POINTER(GNArgs)]
+lib.m3s_gn_check.argtypes = [_vp]
 lib.m3s_gn_build_system.argtypes = [ctypes.POINTER(GNArgs), _vp, _vp]
 lib.m3s_gn_edge_hessians.argtypes = [ctypes.POINTER(GNArgs), _vp, _vp]
 lib.m3s_comm_get_unique_id.argtypes = [_vp]
@@ -624,6 +625,14 @@ def pointmap_update(mode, X, C, X_new, C_new, T=None):
                                      _ptr(C), HW, _stream(dev))
     _raise(rc, "pointmap_update")
     return X, C
+
+
+def gn_check(device=None):
+    """Raise the deferred error of this thread's last Gauss-Newton call, if any: a bounded
+    device-side wait of its factorisation that timed out (include/m3s_backend.h m3s_gn_check).
+    Synchronises the current stream of `device` (default: the current device)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    _raise(lib.m3s_gn_check(_stream(dev)), "gauss_newton")
 
 
 def version() -> str:

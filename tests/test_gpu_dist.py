@@ -177,6 +177,7 @@ def _timeout_worker(rank, world, port, out_q):
     sys.path[:0] = [root, os.path.join(root, "mast3r-slam_amd")]
     import torch.distributed as dist
 
+    import mast3r_slam_backends as mb
     from m3s.dist import HostComm, gauss_newton_sharded, shard_range
 
     if rank == 1:
@@ -192,7 +193,7 @@ def _timeout_worker(rank, world, port, out_q):
         try:
             gauss_newton_sharded("rays", c(g.Twc), c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx[lo:hi]),
                                  c(g.valid[lo:hi]), c(g.Q[lo:hi]), lo, comm, 2, 0.0, **_params(g, "rays"))
-            torch.cuda.synchronize()
+            mb.gn_check()  # the deferred report (include/m3s_backend.h m3s_gn_check)
         except RuntimeError as e:
             err = str(e)
         out_q.put((rank, err, comm.calls, None))

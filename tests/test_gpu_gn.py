@@ -6,11 +6,15 @@ path sum ~10^5 fp32 terms per entry in different orders (the HIP path accumulate
 pre-adjoint Jacobian and applies the adjoint in f64), so entries agree to ~1e-6 of the
 largest entry; the solved pose updates then agree far below the 1e-5 pose tolerance.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
 from m3s import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -583,9 +587,44 @@ def test_factorisation_timeout_is_an_error_not_a_singular_system(backend, monkey
         monkeypatch.setenv("M3S_SOLVER", "2")
     monkeypatch.setenv("M3S_CHOL_DF", "1")
     T_ok, dx_ok = _run_gpu(backend, g, "rays", 2)
+    backend.gn_check()  # nothing pending
     monkeypatch.setenv("M3S_TEST_FORCE_TIMEOUT", "1")
+    # the report is deferred (no host wait at the end of the call): gn_check raises it ...
+    _run_gpu(backend, g, "rays", 2)
     with pytest.raises(RuntimeError, match="timed out"):
-        _run_gpu(backend, g, "rays", 2)
+        backend.gn_check()
+    backend.gn_check()  # ... once
+    # ... and so does the next call, before it does any work
+    _run_gpu(backend, g, "rays", 2)
     monkeypatch.delenv("M3S_TEST_FORCE_TIMEOUT")
+    with pytest.raises(RuntimeError, match="an earlier call: .*timed out"):
+        _run_gpu(backend, g, "rays", 2)
     T_again, dx_again = _run_gpu(backend, g, "rays", 2)
+    backend.gn_check()
     assert np.array_equal(T_again, T_ok) and np.array_equal(dx_again, dx_ok)
+
+
+def test_factorisation_timeout_sync_report(backend, monkeypatch):
+    """M3S_GN_TIMEOUT_SYNC=1 (read once per process, hence a child process): the timed-out call
+    itself raises."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import numpy as np, torch\n"
+        "import mast3r_slam_backends as mb\n"
+        "from tests import test_gpu_gn as t\n"
+        "from m3s import synth\n"
+        "g = synth.make_graph('cfg4', H=24, W=32, seed=6)\n"
+        "try:\n"
+        "    t._run_gpu(mb, g, 'rays', 2)\n"
+        "    print('NO ERROR')\n"
+        "except RuntimeError as e:\n"
+        "    print('RAISED', e)\n"
+    ) % (ROOT, os.path.join(ROOT, "mast3r-slam_amd"))
+    env = dict(os.environ, M3S_GN_TIMEOUT_SYNC="1", M3S_TEST_FORCE_TIMEOUT="1", M3S_CHOL_DF="1",
+               M3S_SOLVER="2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert "RAISED" in r.stdout and "timed out" in r.stdout, (r.stdout, r.stderr[-2000:])
