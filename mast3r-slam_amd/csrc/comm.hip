@@ -1,5 +1,6 @@
-// comm.hip -- the per-iteration collective of edge-sharded Gauss-Newton: one in-place f64 sum
-// all-reduce of the compact block-sparse system per iteration.
+// comm.hip -- the per-iteration collective of edge-sharded Gauss-Newton: an in-place all-gather
+// of the ranks' per-edge records (default: every rank then assembles ALL edges in edge order, as
+// one GPU does) or an in-place f64 sum all-reduce of the assembled block system.
 //
 // A communicator handle is one of
 //   * RCCL (production): librccl.so.1 resolved with dlopen so the single-GPU path has no RCCL
@@ -34,6 +35,7 @@ struct Rccl {
     nccl_result_t (*comm_destroy)(nccl_comm_t) = nullptr;
     nccl_result_t (*all_reduce)(const void*, void*, size_t, int, int, nccl_comm_t,
                                 hipStream_t) = nullptr;
+    nccl_result_t (*all_gather)(const void*, void*, size_t, int, nccl_comm_t, hipStream_t) = nullptr;
     const char* (*err_str)(nccl_result_t) = nullptr;
     nccl_result_t (*comm_count)(nccl_comm_t, int*) = nullptr;
 };
@@ -53,6 +55,7 @@ Rccl* rccl() {
             r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(r.h, "ncclCommInitRank");
             r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.h, "ncclCommDestroy");
             r.all_reduce = (decltype(r.all_reduce))dlsym(r.h, "ncclAllReduce");
+            r.all_gather = (decltype(r.all_gather))dlsym(r.h, "ncclAllGather");
             r.err_str = (decltype(r.err_str))dlsym(r.h, "ncclGetErrorString");
             r.comm_count = (decltype(r.comm_count))dlsym(r.h, "ncclCommCount");
         }
@@ -120,6 +123,45 @@ int comm_allreduce_sum_f64(void* comm, double* buf, size_t count, hipStream_t st
     nccl_result_t e = r->all_reduce(buf, buf, count, kNcclFloat64, kNcclSum, c->nccl, stream);
     if (e != 0) {
         set_error("ncclAllReduce failed: %s", estr(r, e));
+        return M3S_ERR_COMM;
+    }
+    return M3S_OK;
+}
+
+int comm_rank_size(void* comm, int* rank, int* nranks) {
+    Comm* c = as_comm(comm);
+    if (!c) {
+        set_error("comm: not an m3s communicator handle");
+        return M3S_ERR_COMM;
+    }
+    *rank = c->rank;
+    *nranks = c->nranks;
+    return M3S_OK;
+}
+
+int comm_allgather_f64(void* comm, double* buf, size_t count, hipStream_t stream) {
+    Comm* c = as_comm(comm);
+    if (!c) {
+        set_error("all-gather: not an m3s communicator handle");
+        return M3S_ERR_COMM;
+    }
+    if (count == 0 || c->nranks == 1) return M3S_OK;
+    if (c->kind == kCommHost) {
+        // test hook: the other ranks' blocks zeroed, then the sum all-reduce (x + 0 = x exactly)
+        double* own = buf + (size_t)c->rank * count;
+        if (c->rank > 0) M3S_HIP_CHECK(hipMemsetAsync(buf, 0, sizeof(double) * (size_t)c->rank * count, stream));
+        const size_t after = (size_t)(c->nranks - 1 - c->rank) * count;
+        if (after) M3S_HIP_CHECK(hipMemsetAsync(own + count, 0, sizeof(double) * after, stream));
+        return comm_allreduce_sum_f64(comm, buf, count * (size_t)c->nranks, stream);
+    }
+    Rccl* r = rccl();
+    if (!r || !r->all_gather) {
+        set_error("RCCL all-gather not available (dlopen librccl.so.1 / ncclAllGather)");
+        return M3S_ERR_COMM;
+    }
+    nccl_result_t e = r->all_gather(buf + (size_t)c->rank * count, buf, count, kNcclFloat64, c->nccl, stream);
+    if (e != 0) {
+        set_error("ncclAllGather failed: %s", estr(r, e));
         return M3S_ERR_COMM;
     }
     return M3S_OK;

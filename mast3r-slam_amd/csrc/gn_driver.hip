@@ -255,10 +255,11 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.ii_loc = take(sizeof(int) * (size_t)E_local);
     L.jj_loc = take(sizeof(int) * (size_t)E_local);
     L.blk_ptr = take(sizeof(int) * ((size_t)L.nblk_max + 1));
-    L.blk_ent = take(sizeof(int) * (size_t)E_local * 4);
+    // (the CSR lists span ALL edges when the ranks' records are gathered: Plan::gather)
+    L.blk_ent = take(sizeof(int) * (size_t)std::max(E_local, E_total) * 4);
     L.blk_ref = take(sizeof(int) * (size_t)E_local * 4);  // reference-order assembly codes
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
-    L.grad_ent = take(sizeof(int) * (size_t)E_local * 2);
+    L.grad_ent = take(sizeof(int) * (size_t)std::max(E_local, E_total) * 2);
     L.ecnt = take(sizeof(int) * (size_t)E_local);  // fused edge reduce: finished chunks per edge
     L.cok = take(sizeof(int) * (size_t)std::max<int64_t>(N, 1));  // per keyframe: every c > C_thresh
     L.sched = take(sizeof(int) * 4 * (size_t)E_local * L.nchunks);  // {edge, chunk, ix, jx} per task
@@ -291,6 +292,12 @@ struct Plan {
     std::vector<int> slotmap;                     // (npose x npose) -> slot or -1
     std::vector<std::pair<int, int>> pairs;      // slot nblk0.. -> unordered pose pair (a<b)
     float K[4] = {0, 0, 0, 0};
+    // Edge-ordered exchange of a sharded call: the ranks' per-edge records are all-gathered into
+    // nranks blocks of gchunk records (rank r's edges at r * gchunk), and the CSR lists cover ALL
+    // edges in edge order by their gathered position -- every rank assembles exactly the sum one
+    // GPU does, so the poses do not depend on the rank count
+    bool gather = false;
+    int grank = 0, granks = 1, gchunk = 0;
 };
 
 // XCD-aware order of the accumulate tasks (a performance heuristic only: results do not
@@ -338,13 +345,38 @@ void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_l
             if (k < (int64_t)n[g] * nchunks) put(order[lo[g] + (int)(k % n[g])], (int)(k / n[g]));
 }
 
+int gn_order(const m3s_gn_args& a);
+
 int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     const int64_t E = a.E_total;
-    char* hb = stagings().in.get(sizeof(int64_t) * 2 * (size_t)E + 64);
+    // sharded call: gather the edge records (M3S_GN_GATHER=0: all-reduce the assembled system)
+    int grank = 0, granks = 1;
+    if (a.comm && gn_order(a) != M3S_GN_ORDER_REFERENCE && env_int("M3S_GN_GATHER", 1) != 0) {
+        int rc = comm_rank_size(a.comm, &grank, &granks);
+        if (rc) return rc;
+    }
+    const size_t hb_ranges = align_up(sizeof(int64_t) * 2 * (size_t)E + 64, 64);
+    char* hb = stagings().in.get(hb_ranges + sizeof(double) * 2 * (size_t)granks);
     M3S_REQUIRE(hb != nullptr, "gauss_newton: pinned host allocation failed");
     int64_t* hii = reinterpret_cast<int64_t*>(hb);
     int64_t* hjj = hii + E;
     float* Kh = reinterpret_cast<float*>(hjj + E);
+    double* hr = reinterpret_cast<double*>(hb + hb_ranges);  // every rank's (edge_offset, E_local)
+    double* dr = nullptr;
+    if (granks > 1) {
+        // the ranks' edge ranges (once per call; exact in f64 below 2^53)
+        hr[2 * grank] = (double)a.edge_offset;
+        hr[2 * grank + 1] = (double)a.E_local;
+        M3S_HIP_CHECK(hipMallocAsync((void**)&dr, sizeof(double) * 2 * (size_t)granks, st));
+        M3S_HIP_CHECK(hipMemcpyAsync(dr + 2 * grank, hr + 2 * grank, sizeof(double) * 2, hipMemcpyHostToDevice, st));
+        int rc = comm_allgather_f64(a.comm, dr, 2, st);
+        if (rc) {
+            (void)hipFreeAsync(dr, st);
+            return rc;
+        }
+        M3S_HIP_CHECK(hipMemcpyAsync(hr, dr, sizeof(double) * 2 * (size_t)granks, hipMemcpyDeviceToHost, st));
+        M3S_HIP_CHECK(hipFreeAsync(dr, st));
+    }
     if (E > 0) {
         M3S_HIP_CHECK(hipMemcpyAsync(hii, a.ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
         M3S_HIP_CHECK(hipMemcpyAsync(hjj, a.jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
@@ -352,6 +384,37 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     if (a.mode == M3S_GN_CALIB)
         M3S_HIP_CHECK(hipMemcpyAsync(Kh, a.K, sizeof(float) * 9, hipMemcpyDeviceToHost, st));
     M3S_HIP_CHECK(hipStreamSynchronize(st));
+    // gathered position of every edge, when the ranks' ranges partition [0, E) (else: the
+    // all-reduce of the assembled system, which sums whatever the ranks hold)
+    std::vector<int> gpos;
+    plan.gather = false;
+    plan.grank = grank;
+    plan.granks = granks;
+    plan.gchunk = 0;
+    if (granks > 1) {
+        int64_t chunk = 0;
+        std::vector<int> cover(E, 0);
+        bool ok = true;
+        gpos.assign(E, -1);
+        for (int r = 0; r < granks && ok; r++) {
+            const int64_t off = (int64_t)hr[2 * r], cnt = (int64_t)hr[2 * r + 1];
+            ok = off >= 0 && cnt >= 0 && off + cnt <= E;
+            chunk = std::max(chunk, cnt);
+        }
+        for (int r = 0; r < granks && ok; r++) {
+            const int64_t off = (int64_t)hr[2 * r], cnt = (int64_t)hr[2 * r + 1];
+            for (int64_t k = 0; k < cnt && ok; k++) {
+                ok = cover[off + k]++ == 0;
+                gpos[off + k] = (int)(r * chunk + k);
+            }
+        }
+        for (int64_t e = 0; e < E && ok; e++) ok = cover[e] == 1;
+        ok = ok && (int64_t)granks * chunk < (int64_t)(INT32_MAX >> 3);
+        if (ok && chunk > 0) {
+            plan.gather = true;
+            plan.gchunk = (int)chunk;
+        }
+    }
     if (a.mode == M3S_GN_CALIB) {
         plan.K[0] = Kh[0];  // fx = K[0][0]
         plan.K[1] = Kh[4];  // fy = K[1][1]
@@ -405,15 +468,18 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
             for (int k = 0; k < plan.nblk; k++) plan.blk_ptr[k + 1] += plan.blk_ptr[k];
             for (int k = 0; k < npose; k++) plan.grad_ptr[k + 1] += plan.grad_ptr[k];
             plan.blk_ent.assign(plan.blk_ptr[plan.nblk], 0);
-            plan.blk_ref.assign(plan.blk_ptr[plan.nblk], 0);
+            plan.blk_ref.assign(plan.gather ? 0 : plan.blk_ptr[plan.nblk], 0);
             plan.grad_ent.assign(plan.grad_ptr[npose], 0);
             bfill.assign(plan.blk_ptr.begin(), plan.blk_ptr.end() - 1);
             gfill.assign(plan.grad_ptr.begin(), plan.grad_ptr.end() - 1);
         }
-        for (int64_t el = 0; el < a.E_local; el++) {
-            const int64_t e = a.edge_offset + el;
+        // the lists' edges: the local ones, or ALL (by gathered position) when gathering
+        const int64_t nlist = plan.gather ? E : a.E_local;
+        for (int64_t el = 0; el < nlist; el++) {
+            const int64_t e = plan.gather ? el : a.edge_offset + el;
+            const int64_t code = plan.gather ? gpos[e] : el;
             const int i = iopt[e], j = jopt[e];
-            if (pass == 0) {
+            if (pass == 0 && !plan.gather) {
                 plan.ii_loc[el] = i + 1;
                 plan.jj_loc[el] = j + 1;
             }
@@ -428,20 +494,27 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
                         // the diagonal, Hs[1] at (ii, jj) when ii < jj, Hs[2] at (jj, ii) when
                         // jj < ii, a self-edge's Hs[1]/Hs[2] on its diagonal block
                         const int type = (b == 0 || b == 3) ? 0 : (i == j ? (b == 1 ? 3 : 4) : (b == 1 ? 2 : 1));
-                        plan.blk_ref[bfill[sl]] = (int)(el << 3) | type;
-                        plan.blk_ent[bfill[sl]++] = (int)(el << 1) | neg[b];
+                        if (!plan.gather) plan.blk_ref[bfill[sl]] = (int)(el << 3) | type;
+                        plan.blk_ent[bfill[sl]++] = (int)(code << 1) | neg[b];
                     }
                 }
             }
             if (i >= 0) {  // vi = -vj
                 if (pass == 0) plan.grad_ptr[i + 1]++;
-                else plan.grad_ent[gfill[i]++] = (int)(el << 1) | 1;
+                else plan.grad_ent[gfill[i]++] = (int)(code << 1) | 1;
             }
             if (j >= 0) {
                 if (pass == 0) plan.grad_ptr[j + 1]++;
-                else plan.grad_ent[gfill[j]++] = (int)(el << 1);
+                else plan.grad_ent[gfill[j]++] = (int)(code << 1);
             }
         }
+    }
+    if (plan.gather) {
+        for (int64_t el = 0; el < a.E_local; el++) {
+            plan.ii_loc[el] = iopt[a.edge_offset + el] + 1;
+            plan.jj_loc[el] = jopt[a.edge_offset + el] + 1;
+        }
+        plan.blk_ref.clear();  // (the reference order never gathers)
     }
     return M3S_OK;
 }
@@ -866,6 +939,12 @@ struct Ctx {
     // tile inverses and the (npose x npose) slot table, one stream-ordered allocation
     char* dyn = nullptr;
     size_t o_dense = 0, o_linv = 0, o_slot = 0;
+    double* eall = nullptr;  // Plan::gather: every rank's edge records (granks x gchunk)
+    // where this rank's accumulate writes its f64 edge records, and what the assembly reads
+    double* eblk() const {
+        return eall ? eall + (size_t)plan.grank * plan.gchunk * kEdgeBlk : at<double>(L.edgeblk);
+    }
+    const double* eblk_all() const { return eall ? eall : at<double>(L.edgeblk); }
     int chol_epoch = 0;  // dataflow factorisations enqueued in this call (chol_df.hip ready words)
     bool may_timeout = false;  // a solver with bounded device-side waits ran (kFlagTimeout)
     template <typename T>
@@ -893,6 +972,7 @@ struct Ctx {
     ~Ctx() {
         if (sp.dbuf) (void)hipFreeAsync(sp.dbuf, st);
         if (dyn) (void)hipFreeAsync(dyn, st);
+        if (eall) (void)hipFreeAsync(eall, st);
     }
 };
 
@@ -910,6 +990,9 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     const auto s0 = std::chrono::steady_clock::now();
     rc = build_plan(a, c.st, c.plan);
     if (rc) return rc;
+    if (c.plan.gather)
+        M3S_HIP_CHECK(hipMallocAsync((void**)&c.eall,
+                                     sizeof(double) * kEdgeBlk * (size_t)c.plan.granks * c.plan.gchunk, c.st));
     const auto s1 = std::chrono::steady_clock::now();
     const Layout& L = c.L;
     const Plan& p = c.plan;
@@ -1116,7 +1199,7 @@ int enqueue_accumulate(const m3s_gn_args& a, Ctx& c) {
                                               c.at<float>(L.partials), flags,
                                               c.compact ? c.at<float>(L.packx) : nullptr,
                                               c.at<int>(L.pcnt), fused ? c.at<int>(L.ecnt) : nullptr,
-                                              c.at<double>(L.edgeblk), c.first_pack ? &c.es : nullptr,
+                                              c.eblk(), c.first_pack ? &c.es : nullptr,
                                               a.Cs, c.at<int>(L.cok)));
             c.first_pack = false;  // the records exist from here on
         } else
@@ -1127,7 +1210,7 @@ int enqueue_accumulate(const m3s_gn_args& a, Ctx& c) {
         g_prof.mark(c.st, true, was_first);
         if (!fused)
             M3S_HIP_CHECK(launch_edge_reduce((int)a.E_local, c.st, c.at<float>(L.partials), L.nchunks,
-                                             a.Twc, c.at<int>(L.ii_loc), c.at<double>(L.edgeblk), flags));
+                                             a.Twc, c.at<int>(L.ii_loc), c.eblk(), flags));
     }
     return M3S_OK;
 }
@@ -1137,26 +1220,32 @@ int enqueue_assembly(const m3s_gn_args& a, Ctx& c) {
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
     const int npose = (int)(a.N - 1);
+    if (c.plan.gather) {
+        // every rank's edge records, then the assembly of ALL edges in edge order (no all-reduce)
+        int rc = comm_allgather_f64(a.comm, c.eall, (size_t)c.plan.gchunk * kEdgeBlk, c.st);
+        if (rc) return rc;
+    }
+    const bool reduce = a.comm && !c.plan.gather;
     if (c.sp.enabled) {
         // block format for the sparse solves, in the solver's buffer
         SparsePlan& sp = c.sp;
         double* sys = sp.dptr<double>(sp.o_sys);
-        M3S_HIP_CHECK(launch_assemble(c.st, c.at<double>(L.edgeblk), c.at<int>(L.blk_ptr),
+        M3S_HIP_CHECK(launch_assemble(c.st, c.eblk_all(), c.at<int>(L.blk_ptr),
                                       c.at<int>(L.blk_ent), c.at<int>(L.grad_ptr),
                                       c.at<int>(L.grad_ent), c.plan.nblk, sp.nblocks, npose, sp.bpad,
                                       sys, flags));
-        if (a.comm) {
+        if (reduce) {
             const size_t count = (size_t)sp.bpad + (size_t)c.plan.nblk * 49;
             int rc = comm_allreduce_sum_f64(a.comm, sys, count, c.st);
             if (rc) return rc;
         }
         return M3S_OK;
     }
-    M3S_HIP_CHECK(launch_compact(c.st, c.at<double>(L.edgeblk), c.at<int>(L.blk_ptr),
+    M3S_HIP_CHECK(launch_compact(c.st, c.eblk_all(), c.at<int>(L.blk_ptr),
                                  c.at<int>(L.blk_ent), c.at<int>(L.grad_ptr),
                                  c.at<int>(L.grad_ent), c.plan.nblk, npose,
                                  c.at<double>(L.compact), flags));
-    if (a.comm) {
+    if (reduce) {
         const size_t count = (size_t)c.plan.nblk * 28 + (size_t)npose * 7;
         int rc = comm_allreduce_sum_f64(a.comm, c.at<double>(L.compact), count, c.st);
         if (rc) return rc;

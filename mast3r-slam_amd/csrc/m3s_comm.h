@@ -8,4 +8,9 @@
 namespace m3s {
 // Sum-all-reduce of `count` doubles in place on `stream` (RCCL ring over xGMI).
 int comm_allreduce_sum_f64(void* comm, double* buf, size_t count, hipStream_t stream);
+// This rank and the rank count of the handle (as created).
+int comm_rank_size(void* comm, int* rank, int* nranks);
+// All-gather of `count` doubles per rank on `stream`: rank r's block lands at buf + r * count, and
+// the rank's own block is read from buf + rank * count (in place, ncclAllGather's convention).
+int comm_allgather_f64(void* comm, double* buf, size_t count, hipStream_t stream);
 }  // namespace m3s

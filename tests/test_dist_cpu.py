@@ -87,3 +87,68 @@ def test_two_rank_sharded_system_equals_full(oracle):
         np.testing.assert_allclose(x, x_full, rtol=1e-9, atol=1e-12)
     # both ranks hold bitwise-identical systems and solutions (no broadcast needed)
     assert np.array_equal(res[0][1], res[1][1]) and np.array_equal(res[0][3], res[1][3])
+
+
+def _gather_worker(rank, world, port, ranges, out_q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mast3r-slam_amd")]
+    from m3s import synth
+    from oracle import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = synth.make_graph(dict(N=6, E=9), H=24, W=32, seed=4)
+    P = O.make_params("rays", 0.003, 10.0, 0.0, 1.5, max_iter=1)
+    ie, je, _ = O.remap(g.ii.numpy(), g.jj.numpy())
+    lo, hi = ranges[rank]
+    Hs, gs = O.gn_align(P, g.Twc.numpy(), g.Xs.numpy(), g.Cs.numpy(), ie[lo:hi], je[lo:hi],
+                        g.idx.numpy()[lo:hi], g.valid.numpy()[lo:hi], g.Q.numpy()[lo:hi])
+    # the op's default exchange: every rank's per-edge records (Hs [4, E, 7, 7], gs [2, E, 7]),
+    # gathered in blocks of the largest range (gn_driver.hip Plan::gather), then ALL edges
+    # assembled in edge order on every rank
+    n = hi - lo
+    chunk = max(h - l for l, h in ranges)
+    rec = np.zeros((chunk, 4 * 49 + 2 * 7))
+    rec[:n] = np.concatenate([Hs.transpose(1, 0, 2, 3).reshape(n, -1), gs.transpose(1, 0, 2).reshape(n, -1)], 1)
+    out = [torch.zeros_like(torch.from_numpy(rec)) for _ in range(world)]
+    dist.all_gather(out, torch.from_numpy(rec))
+    E2 = g.ii.shape[0]
+    allrec = np.zeros((E2, rec.shape[1]))
+    for r, (l, h) in enumerate(ranges):
+        allrec[l:h] = out[r].numpy()[: h - l]
+    Hall = np.ascontiguousarray(allrec[:, :196].reshape(E2, 4, 7, 7).transpose(1, 0, 2, 3)).astype(Hs.dtype)
+    gall = np.ascontiguousarray(allrec[:, 196:].reshape(E2, 2, 7).transpose(1, 0, 2)).astype(gs.dtype)
+    H, b = O.gn_assemble(Hall, gall, ie - 1, je - 1, g.N)
+    out_q.put((rank, H, b))
+    dist.destroy_process_group()
+
+
+def test_gathered_edge_records_make_the_system_rank_count_independent(oracle):
+    """Three ranks with ragged ranges: gathering the per-edge records and assembling every edge in
+    edge order gives BITWISE the one-process system (the all-reduce of partial systems above
+    agrees only to summation-reorder level)."""
+    from m3s import synth
+
+    g = synth.make_graph(dict(N=6, E=9), H=24, W=32, seed=4)
+    E2 = g.ii.shape[0]
+    ranges = [(0, 5), (5, 7), (7, E2)]
+    world = len(ranges)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, ranges, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    P = oracle.make_params("rays", 0.003, 10.0, 0.0, 1.5, max_iter=1)
+    ie, je, _ = oracle.remap(g.ii.numpy(), g.jj.numpy())
+    Hs, gs = oracle.gn_align(P, g.Twc.numpy(), g.Xs.numpy(), g.Cs.numpy(), ie, je, g.idx.numpy(),
+                             g.valid.numpy(), g.Q.numpy())
+    H, b = oracle.gn_assemble(Hs, gs, ie - 1, je - 1, g.N)
+    for _, Hr, br in res:
+        assert np.array_equal(Hr, H) and np.array_equal(br, b)

@@ -8,11 +8,14 @@ host-callback communicator (``m3s_comm_init_host``: stream drained, system stage
 all_reduce, copied back) instead of RCCL, which needs one GPU per rank.
 
 Checked: Twc is bitwise identical on both ranks after 3 iterations (no broadcast in the op),
-the callback ran once per iteration, and the result equals the unsharded op to f64
-summation-reorder level (1e-6 relative; the shards' f64 partial systems are added in a
-different order than one process's chunk sums -- the f32 per-edge sums are the same, the chunking
-follows the total edge count), the exactly summed system at the north-star 1e-5 and the oracle
-within max(1e-5, 4 sigma) (sigma: the reference fp32 order's own distance from the exact sums).
+the callback ran once per iteration (plus once per call for the ranks' edge ranges), and the
+result is BITWISE the unsharded op's: the default exchange all-gathers the ranks' f64 per-edge
+records and every rank assembles all edges in edge order, as one GPU does (the per-edge records
+themselves do not depend on the rank count: the chunking follows the total edge count).  The
+former exchange -- an all-reduce of the ranks' assembled partial systems, M3S_GN_GATHER=0 -- is
+checked to f64 summation-reorder level (1e-6 relative).  Also: the exactly summed system at the
+north-star 1e-5 and the oracle within max(1e-5, 4 sigma) (sigma: the reference fp32 order's own
+distance from the exact sums).
 Reference seam: global_opt.py:104-110 (two-way edges), gn_kernels.cu:1201-1209 (the solve).
 """
 import os
@@ -62,8 +65,11 @@ def _params(g, mode):
     return p
 
 
-def _worker(rank, world, port, mode, layout, cfg, out_q):
+def _worker(rank, world, port, mode, layout, cfg, exchange, out_q):
     import sys
+
+    if exchange == "reduce":
+        os.environ["M3S_GN_GATHER"] = "0"
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "mast3r-slam_amd")]
@@ -103,9 +109,11 @@ def _worker(rank, world, port, mode, layout, cfg, out_q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("mode,layout,cfg", [("rays", "contiguous", "cfg2"), ("calib", "contiguous", "cfg2"),
-                                             ("rays", "two_way", "cfg2"), ("rays", "contiguous", "cfg4")])
-def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cfg):
+@pytest.mark.parametrize("mode,layout,cfg,exchange", [
+    ("rays", "contiguous", "cfg2", "gather"), ("calib", "contiguous", "cfg2", "gather"),
+    ("rays", "two_way", "cfg2", "gather"), ("rays", "contiguous", "cfg4", "gather"),
+    ("calib", "contiguous", "cfg2", "reduce"), ("rays", "contiguous", "cfg4", "reduce")])
+def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cfg, exchange):
     """layout "two_way": each rank passes its directed-edge range of a two-way edge store as
     the op's two halves (m3s.dist.two_way_range) -- the owner-sharded store layout.  cfg4: the
     scaling graph's topology (BASELINE configs[3]) at reduced resolution."""
@@ -113,7 +121,8 @@ def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cf
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, layout, cfg, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, layout, cfg, exchange, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -128,9 +137,9 @@ def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cf
     assert all(p.exitcode == 0 for p in procs)
     (_, T0, calls0, rng0, _), (_, T1, calls1, rng1, _) = res
     assert rng0[0] == 0 and rng0[1] == rng1[0] and rng0[1] > 0 and rng1[1] > rng1[0]
-    # one exchange per iteration; cfg4's dataflow factorisation (bounded device waits) adds one
-    # for the ranks' OR of the timeout flag at the end of the call
-    assert calls0 == calls1 == ITERS + (1 if cfg == "cfg4" else 0)
+    # one exchange per iteration (+ the ranks' edge ranges once per call when gathering); cfg4's
+    # dataflow factorisation (bounded device waits) adds one for the ranks' OR of the timeout flag
+    assert calls0 == calls1 == ITERS + (exchange == "gather") + (1 if cfg == "cfg4" else 0)
     # bitwise identical poses on every rank: same all-reduced system, same deterministic solve
     assert np.array_equal(T0, T1)
 
@@ -155,7 +164,10 @@ def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cf
     torch.cuda.synchronize()
     T_full = Twc.cpu().numpy()
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
-    assert rel(T0, T_full) < 1e-6, rel(T0, T_full)
+    if exchange == "gather":
+        assert np.array_equal(T0, T_full), rel(T0, T_full)  # rank-count independent
+    else:
+        assert rel(T0, T_full) < 1e-6, rel(T0, T_full)
     arrs = (g.Twc.numpy(), g.Xs.numpy(), g.Cs.numpy(), g.ii.numpy(), g.jj.numpy(), g.idx.numpy(),
             g.valid.numpy(), g.Q.numpy())
     T_o, _, _ = oracle.gauss_newton(P, *arrs)
@@ -226,7 +238,7 @@ def test_a_timeout_on_one_rank_fails_every_rank(backend):
     for r in res:
         assert r[3] is None, r[3]
         assert r[1] is not None and "timed out" in r[1], r[1]
-    assert res[0][2] == res[1][2] == 2 + 1  # two iterations' exchanges + the flag's
+    assert res[0][2] == res[1][2] == 1 + 2 + 1  # the edge ranges, two iterations' exchanges, the flag
 
 
 def _rccl_worker(port, mode, out_q):
