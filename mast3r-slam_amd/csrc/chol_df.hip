@@ -53,6 +53,7 @@ struct DfArgs {
     int spin_limit;  // bound of a ready wait (s_sleep(1) steps); < 0: every wait times out (test hook)
     long long* trace;  // diagnostics (tools/ubench_chol_df.hip): 4 timestamps per tile, else null
     double* x;         // != null: the back-substitution L^T x = y runs in this launch too (x: npad)
+    DfScatter g;       // g.xpose != null: the back-substitution also writes x pose-indexed
 };
 
 // workgroup barrier ordering LDS only (__syncthreads also waits for every outstanding global
@@ -642,6 +643,10 @@ __device__ __forceinline__ void load_acc(d4 acc[4], const double* src, int64_t l
             acc[J][e] = COH ? ld_coh(p) : *p;
         }
 }
+// the original tile (i, j) of the filled dense matrix
+__device__ __forceinline__ void load_src(d4 acc[4], const DfArgs& a, int i, int j) {
+    load_acc<false>(acc, a.Hd + (int64_t)i * T * a.npad + (int64_t)j * T, a.npad);
+}
 __device__ __forceinline__ void store_acc_coh(double* dst, int64_t ld, const d4 acc[4]) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -723,7 +728,12 @@ __device__ void back_task(const DfArgs& a, int j, double* S) {
     for (int q = 0; q < 16; q++) xp = fma(li[q], sz[16 * g + q], xp);
     sp[g * 64 + c] = xp;
     lds_barrier();
-    if (tid < 64) st_coh(a.x + (int64_t)j * T + c, ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c]);
+    if (tid < 64) {
+        const double xv = ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c];
+        st_coh(a.x + (int64_t)j * T + c, xv);
+        const int q = j * T + c;  // the pose-indexed copy the back rounds read (no scatter launch)
+        if (a.g.xpose && q < 7 * a.g.ntail) a.g.xpose[(int64_t)a.g.tail[q / 7] * 7 + q % 7] = xv;
+    }
     publish(a, xflag(nt, j));
 }
 
@@ -759,7 +769,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             }
             cstamp(j, 0);
             if (j == 0) {
-                load_acc<false>(accd, tile(0, 0), ld);
+                load_src(accd, a, 0, 0);
                 acc_to_lds(Z, accd);
                 for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;
                 if (tid < 8) Sync[tid] = 0;
@@ -767,8 +777,8 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             } else {
                 d4 accs[4];
                 if (j == 1) {
-                    load_acc<false>(accs, tile(1, 0), ld);
-                    load_acc<false>(accd, tile(1, 1), ld);
+                    load_src(accs, a, 1, 0);
+                    load_src(accd, a, 1, 1);
                 } else {
                     load_acc<true>(accs, tile(j, j - 1), ld);
                     load_acc<true>(accd, tile(j, j), ld);
@@ -833,8 +843,8 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             // ---- H_{j+2}: partial sums of tiles (h, h-1), (h, h) over k <= j = h-2
             const int h = j + 2;
             d4 accs[4], accd[4];
-            load_acc<false>(accs, tile(h, h - 1), ld);
-            load_acc<false>(accd, tile(h, h), ld);
+            load_src(accs, a, h, h - 1);
+            load_src(accd, a, h, h);
             for (int k = 0; k <= j; k++) {
                 if (tid == 0) {
                     wait_ready(a.ready + h * nt + k, a.epoch, a.flags, a.spin_limit);
@@ -857,7 +867,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             // ---- regular tile (i, j), left-looking
             const int i = j < nt - 1 ? j + 2 + rem : nt;
             d4 acc[4];
-            load_acc<false>(acc, tile(i, j), ld);
+            load_src(acc, a, i, j);
             for (int k = 0; k < j; k++) {
                 if (tid == 0) {
                     wait_ready(a.ready + i * nt + k, a.epoch, a.flags, a.spin_limit);
@@ -895,7 +905,7 @@ size_t chol_ready_bytes(int npad) {
 }
 
 hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
-                                int epoch, int* flags, double* x) {
+                                int epoch, int* flags, double* x, const DfScatter* g) {
     static int maxg = 0;
     if (maxg == 0) {
         int dev = 0, ncu = 0, per = 0;
@@ -916,6 +926,7 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
     a.ntiles = num_tasks(a.nt);
     a.epoch = epoch;
     a.x = x;
+    if (g) a.g = *g;
     // M3S_TEST_FORCE_TIMEOUT=1 (tests only): every ready wait gives up at once, to exercise the
     // timeout -> M3S_ERR_TIMEOUT path without a real hang
     const char* ft = getenv("M3S_TEST_FORCE_TIMEOUT");

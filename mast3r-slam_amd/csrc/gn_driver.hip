@@ -36,14 +36,23 @@ namespace {
 thread_local std::string g_err;
 
 // Optional phase timing with HIP events on the GN stream (bench.py roofline).
+int env_int(const char* name, int dflt);
+
 struct Prof {
     bool on = false;
     std::vector<hipEvent_t> pool;
     std::vector<hipEvent_t> marks;  // per iteration: t0 accum t1 system t2 solve t3 retract t4
     hipEvent_t get() {
         if (pool.empty()) {
+            // timing-only events: no system-scope release / acquire when recorded (a default
+            // event record writes back and invalidates the caches -- idle GPU between the
+            // kernels it separates); M3S_PROF_SYSFENCE=1: default events
+            static const bool sysfence = env_int("M3S_PROF_SYSFENCE", 0) != 0;
             hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            if (sysfence || hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
+                (void)hipGetLastError();
+                if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            }
             return e;
         }
         hipEvent_t e = pool.back();
@@ -51,8 +60,8 @@ struct Prof {
         return e;
     }
     bool accum_only = false;  // record only the two events bracketing the accumulate kernel
-    // (every timed event record is a queue marker with a release to system scope: ~5 us of idle
-    // GPU each, so the timed bench region carries only the accumulate pair)
+    // (every timed event record is a queue marker; with a release to system scope it left ~5 us
+    // of idle GPU each, so the timed bench region carries only the accumulate pair)
     std::vector<char> first;  // accum_only: per event pair, the launch built the packed records
     void mark(hipStream_t st, bool accum = false, bool first_pack = false) {
         if (!on || (accum_only && !accum)) return;
@@ -1402,9 +1411,12 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     static const bool core_df = env_int("M3S_HYB_CORE", 1) != 0;
     if (sp.hybrid && core_df && !coop && sp.ntail > 0) {
         c.may_timeout = true;  // chol_df's bounded waits
-        M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
-                                     sp.npad_tail, sp.dptr<double>(sp.o_dense), sp.dptr<double>(sp.o_linv),
-                                     sp.dptr<double>(sp.o_xd), x, flags, ++c.chol_epoch));
+        M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
+                                          sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
+        M3S_HIP_CHECK(launch_dense_factor_solve(c.st, sp.npad_tail, sp.dptr<double>(sp.o_dense),
+                                                sp.dptr<double>(sp.o_linv), sp.dptr<double>(sp.o_xd), flags,
+                                                ++c.chol_epoch));
+        S.xd = sp.dptr<double>(sp.o_xd);  // gn_solve reads the core's x in its dense order
         S.Hd = nullptr;
         S.nmeta = (int)sp.nints_back;
         S.meta_lds = 1;

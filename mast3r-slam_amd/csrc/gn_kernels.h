@@ -133,12 +133,21 @@ inline size_t chol_linv_bytes(int npad) {
 inline int* chol_ready_ptr(double* Linv, int npad) {
     return reinterpret_cast<int*>(Linv + (size_t)npad * kCholTile);
 }
+// The elimination's dense core: the in-launch back-substitution also writes x pose-indexed
+// (x_pose[7 tail[i / 7] + i % 7] = x[i], i < 7 ntail) for the back rounds -- no scatter launch
+struct DfScatter {
+    const int* tail;
+    int ntail;
+    double* xpose;
+};
 // x != nullptr: the back-substitution L^T x = y (y: the forward-substituted border row) runs as
 // dataflow tasks in the same launch
 hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
-                                int epoch, int* flags, double* x = nullptr);
+                                int epoch, int* flags, double* x = nullptr, const DfScatter* g = nullptr);
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
-                                     double* x, int* flags, int epoch);
+                                     double* x, int* flags, int epoch, const DfScatter* g = nullptr);
+hipError_t launch_sp_tail_scatter(hipStream_t st, const double* xd, const int* tail, int ntail, double* x,
+                                  const int* flags);
 // multi-launch block-sparse elimination (gn_sparse.hip): one launch per round
 // every elimination round (+ optionally the hybrid core's dense fill) in one cooperative launch
 // Per round target, one record of kSpRec ints: {target, c0, c1, 0} then the first kSpInline
@@ -205,7 +214,8 @@ struct SolveArgs {
                                    // gives it a stack frame)
     int contract;                  // the retraction's M3S_CONTRACT_* (m3s_gn_args.contract)
     int x_tail_global;             // the dense core was solved by its own launch (chol_df): its x
-                                   // is read from x (pose-indexed) before the back rounds
+                                   // is read from xd (the core's dense order) before the back rounds
+    const double* xd;
 };
 size_t solve_lds_bytes(int nmeta_lds);
 int solve_max_poses();  // x stays in LDS: the single-workgroup solve takes at most this many poses

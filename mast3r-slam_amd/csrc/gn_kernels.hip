@@ -615,7 +615,7 @@ hipError_t launch_assemble(hipStream_t st, const double* edgeblk, const int* blk
 }
 
 hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, double* Linv,
-                                     double* x, int* flags, int epoch) {
+                                     double* x, int* flags, int epoch, const DfScatter* g) {
     const int nt = npad / T;
     // M3S_CHOL_DF=1 (default): the whole LL^T as one dataflow launch (chol_df.hip); 0: one
     // potrf / trsm / update launch triple per panel
@@ -629,10 +629,11 @@ hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, doubl
         // tasks (chol_df.hip back_task); 0: chol_backsolve_kernel after it
         const char* bk_env = getenv("M3S_CHOL_DF_BACK");
         const bool in_launch = bk_env ? atoi(bk_env) != 0 : true;
+        // (the pose-indexed copy needs the in-launch back-substitution)
         done = launch_chol_dataflow(st, npad, Hd, Linv, chol_ready_ptr(Linv, npad), epoch, flags,
-                                    in_launch ? x : nullptr) == hipSuccess;
+                                    (in_launch || g) ? x : nullptr, g) == hipSuccess;
         if (!done) (void)hipGetLastError();
-        if (done && in_launch) return hipGetLastError();
+        if (done && (in_launch || g)) return hipGetLastError();
     }
     if (!done) {
         for (int k = 0; k < nt; k++) {
@@ -649,6 +650,7 @@ hipError_t launch_dense_factor_solve(hipStream_t st, int npad, double* Hd, doubl
     }
     hipLaunchKernelGGL(chol_backsolve_kernel, dim3(1), dim3(kBackThreads), 0, st, Hd, npad, Linv,
                        x, flags);
+    if (g && g->xpose) return launch_sp_tail_scatter(st, x, g->tail, g->ntail, g->xpose, flags);
     return hipGetLastError();
 }
 

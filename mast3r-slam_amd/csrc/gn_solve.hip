@@ -760,12 +760,9 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
         constexpr int NG = NW * kGroups;
         const int gid = wave * kGroups + g;
         if (a.x_tail_global && a.ntail > 0) {
-            // the core's x from the dense dataflow launch (sp_tail_scatter wrote it pose-indexed)
+            // the core's x from the dense dataflow launch, in the core's order (no scatter launch)
             const int* __restrict__ Mtail = M + a.o_tail;
-            for (int i = tid; i < 7 * a.ntail; i += NT) {
-                const int o = Mtail[i / 7] * 7 + i % 7;
-                sX[o] = a.x[o];
-            }
+            for (int i = tid; i < 7 * a.ntail; i += NT) sX[Mtail[i / 7] * 7 + i % 7] = a.xd[i];
             lds_barrier();
         }
         double* __restrict__ sPart = smem + kOffPn;  // tail scratch, free once the tail is done
