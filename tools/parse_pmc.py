@@ -33,8 +33,12 @@ fill_kb = [v for k, v in cal_w.items() if "FillFunc" in k][0][0]
 k_write = (1 << 30) / (fill_kb * 1024.0)
 bf = load("bench", "FETCH_SIZE")
 bw = load("bench", "WRITE_SIZE")
+# the steady-state packed accumulate of this config's mode (calib 2, rays 1, points 0): not the
+# call's first launch (FIRST = true, which also builds the records), the most-launched name
+mode = {"cfg3": "2", "cfg4": "1"}.get(cfg, "2")
 names = [k for k in bf if "gn_accum" in k]
-name = ([k for k in names if "packed" in k] or names)[0]
+steady = [k for k in names if f"gn_accum_packed_kernel<{mode}," in k and not k.split(">")[0].endswith("true")]
+name = max(steady or [k for k in names if "packed" in k] or names, key=lambda k: len(bf[k]))
 fetch_kb = sum(bf[name]) / len(bf[name])
 write_kb = sum(bw[name]) / len(bw[name])
 read_b = fetch_kb * 1024 * k_fetch

@@ -11,7 +11,7 @@ mkdir -p $OUT
 CFG="${CFG:-cfg3}"
 for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/bench_$c -o run -- \
-        python bench.py --config $CFG --steps 1 --warmup 0 --iters 3 --no-cpu-baseline \
+        python bench.py --config $CFG --steps 1 --warmup 0 --iters 3 --no-cpu-baseline --no-cfg4 --no-matching \
         > $OUT/bench_$c.log 2>&1
     rc=$?; echo "pmc $c bench rc=$rc"; [ $rc -ne 0 ] && exit $rc
     timeout -k 10 120 rocprofv3 --pmc $c --output-format csv -d $OUT/calib_$c -o run -- \
