@@ -664,77 +664,143 @@ __device__ __forceinline__ void publish(const DfArgs& a, int idx) {
     if (threadIdx.x == 0) __hip_atomic_store(a.ready + idx, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Back-substitution task of tile column j (after the factor tasks in the helpers' lists, in
-// descending j): z_j = y_j - sum_{k>j} L_kj^T x_k, x_j = Linv_j^T z_j, published with a ready word
-// (xflag).  Each x_k is applied as soon as it is published, so when x_{j+1} arrives only its own
-// term, the sum and the Linv_j product are left: one hand-off + two 64x64 GEMVs per tile column on
-// the chain instead of the single-workgroup back-substitution's whole row panel per step (which
-// streamed all of L through one CU: 85 us on cfg4).  Thread (c, g): column c, rows 16g .. 16g+15 of
-// each tile; the 4 row-group partials are summed in fixed order (deterministic).  Every wait
-// targets a task earlier in some co-resident workgroup's list: no deadlock.
+// Back-substitution task of the tile columns jh and jl = jh - 1 (jl < 0: jh alone), after the
+// factor tasks in the helpers' lists, in descending order: z_j = y_j - sum_{k>j} L_kj^T x_k,
+// x_j = Linv_j^T z_j, published with ready words (xflag).  Each x_k is applied as soon as it is
+// published, so when the previous pair's x arrive only their terms, the sums and the Linv
+// products are left -- and x_jh feeds x_jl inside the workgroup (L_{jh,jl}^T x_jh): one hand-off
+// per two tile columns on the back-substitution chain (a hand-off -- write-through store, flag,
+// spin, coherent load -- is ~3 us: 16 of them were 54 us of cfg4's factorisation, r04_r).
+// Thread (c, g): column c, rows 16g .. 16g+15 of each tile; the 4 row-group partials are summed
+// in fixed order (deterministic).  Every wait targets a task earlier in some co-resident
+// workgroup's list: no deadlock.
 __host__ __device__ inline int xflag(int nt, int j) { return (nt + 1) * nt + nt + j; }
-__device__ void back_task(const DfArgs& a, int j, double* S) {
+__device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
     const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
     const int nt = a.nt;
     const int64_t ld = a.npad;
-    double* sx = S;             // x_k (64)
-    double* sp = S + 64;        // partials [4][64]
-    double* sz = S + 64 + 256;  // z_j (64)
-    auto Ltile = [&](int k) { return a.Hd + (int64_t)k * T * ld + (int64_t)j * T; };
+    const bool two = jl >= 0;
+    double* sx = S;                    // x_k (64)
+    double* sp = S + 64;               // partials [4][64]
+    double* sz = S + 64 + 256;         // z (64)
+    double* sxh = S + 64 + 256 + 64;   // x_jh (64)
+    auto Lt = [&](int k, int j) { return a.Hd + (int64_t)k * T * ld + (int64_t)j * T; };
     // the tiles this task reads are final long before the x chain reaches it: their words are
     // checked one step ahead and each tile is loaded while the previous x_k is awaited
-    double acc = 0.0, lv[16], li[16];
+    double acc_h = 0.0, acc_l = 0.0, lvh[16], lvl[16], lih[16], lil[16], lhl[16];
+    // diagnostics (tools/ubench_chol_df.hip, M3S_DF_STAMPS): 4 stamps per pair after the chain's
+    auto bstamp = [&](int slot) {
+#if M3S_DF_STAMPS
+        if (a.trace && tid == 0)
+            a.trace[4 * a.ntiles + 32 + 8 * nt + 4 * ((nt - 1 - jh) / 2) + slot] = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
+    };
     if (tid == 0) {
-        wait_ready(a.ready + j * nt + j, a.epoch, a.flags, a.spin_limit);  // Linv_j
-        if (j + 1 < nt) wait_ready(a.ready + (nt - 1) * nt + j, a.epoch, a.flags, a.spin_limit);
+        wait_ready(a.ready + jh * nt + jh, a.epoch, a.flags, a.spin_limit);  // Linv_jh
+        if (jh + 1 < nt) wait_ready(a.ready + (nt - 1) * nt + jh, a.epoch, a.flags, a.spin_limit);
+        if (two) {
+            wait_ready(a.ready + jl * nt + jl, a.epoch, a.flags, a.spin_limit);  // Linv_jl
+            wait_ready(a.ready + jh * nt + jl, a.epoch, a.flags, a.spin_limit);  // L_{jh,jl}
+            if (jh + 1 < nt) wait_ready(a.ready + (nt - 1) * nt + jl, a.epoch, a.flags, a.spin_limit);
+        }
     }
     __syncthreads();
-    const double* Lk = a.Linv + (int64_t)j * T * T;
 #pragma unroll
-    for (int q = 0; q < 16; q++) li[q] = ld_coh(Lk + (16 * g + q) * T + c);
-    if (j + 1 < nt) {
+    for (int q = 0; q < 16; q++) lih[q] = ld_coh(a.Linv + (int64_t)jh * T * T + (16 * g + q) * T + c);
+    if (two) {
 #pragma unroll
-        for (int q = 0; q < 16; q++) lv[q] = ld_coh(Ltile(nt - 1) + (int64_t)(16 * g + q) * ld + c);
+        for (int q = 0; q < 16; q++) {
+            lil[q] = ld_coh(a.Linv + (int64_t)jl * T * T + (16 * g + q) * T + c);
+            lhl[q] = ld_coh(Lt(jh, jl) + (int64_t)(16 * g + q) * ld + c);
+        }
     }
-    for (int k = nt - 1; k > j; k--) {
+    if (jh + 1 < nt) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) lvh[q] = ld_coh(Lt(nt - 1, jh) + (int64_t)(16 * g + q) * ld + c);
+        if (two) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) lvl[q] = ld_coh(Lt(nt - 1, jl) + (int64_t)(16 * g + q) * ld + c);
+        }
+    }
+    // y_jh, y_jl (the border row: forward-substituted during the factorisation) prefetched, off
+    // the x chain
+    if (tid == 0) {
+        wait_ready(a.ready + nt * nt + jh, a.epoch, a.flags, a.spin_limit);
+        if (two) wait_ready(a.ready + nt * nt + jl, a.epoch, a.flags, a.spin_limit);
+    }
+    __syncthreads();
+    const double yh = tid < 64 ? ld_coh(a.Hd + (int64_t)ld * ld + (int64_t)jh * T + c) : 0.0;
+    const double yl = (two && tid < 64) ? ld_coh(a.Hd + (int64_t)ld * ld + (int64_t)jl * T + c) : 0.0;
+    bstamp(0);
+    for (int k = nt - 1; k > jh; k--) {
         if (tid == 0) {
             wait_ready(a.ready + xflag(nt, k), a.epoch, a.flags, a.spin_limit);
-            if (k - 1 > j) wait_ready(a.ready + (k - 1) * nt + j, a.epoch, a.flags, a.spin_limit);
+            if (k - 1 > jh) {
+                wait_ready(a.ready + (k - 1) * nt + jh, a.epoch, a.flags, a.spin_limit);
+                if (two) wait_ready(a.ready + (k - 1) * nt + jl, a.epoch, a.flags, a.spin_limit);
+            }
         }
         __syncthreads();
         if (tid < 64) sx[tid] = ld_coh(a.x + (int64_t)k * T + tid);
-        double cur[16];
+        double ch[16], cl[16];
 #pragma unroll
-        for (int q = 0; q < 16; q++) cur[q] = lv[q];
-        if (k - 1 > j) {
+        for (int q = 0; q < 16; q++) {
+            ch[q] = lvh[q];
+            cl[q] = lvl[q];
+        }
+        if (k - 1 > jh) {
 #pragma unroll
-            for (int q = 0; q < 16; q++) lv[q] = ld_coh(Ltile(k - 1) + (int64_t)(16 * g + q) * ld + c);
+            for (int q = 0; q < 16; q++) lvh[q] = ld_coh(Lt(k - 1, jh) + (int64_t)(16 * g + q) * ld + c);
+            if (two) {
+#pragma unroll
+                for (int q = 0; q < 16; q++) lvl[q] = ld_coh(Lt(k - 1, jl) + (int64_t)(16 * g + q) * ld + c);
+            }
         }
         lds_barrier();
 #pragma unroll
-        for (int q = 0; q < 16; q++) acc = fma(cur[q], sx[16 * g + q], acc);
+        for (int q = 0; q < 16; q++) acc_h = fma(ch[q], sx[16 * g + q], acc_h);
+        if (two) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc_l = fma(cl[q], sx[16 * g + q], acc_l);
+        }
         lds_barrier();  // sx is rewritten by the next k
     }
-    if (tid == 0) wait_ready(a.ready + nt * nt + j, a.epoch, a.flags, a.spin_limit);  // y_j (the border tile)
-    sp[g * 64 + c] = acc;
-    __syncthreads();
-    if (tid < 64) {
-        const double y = ld_coh(a.Hd + (int64_t)ld * ld + (int64_t)j * T + c);
-        sz[c] = y - (((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c]);
-    }
-    lds_barrier();
-    double xp = 0.0;
+    // x_j = Linv_j^T (y_j - acc) for the column (j, y, acc, Linv rows): into xs (LDS), x and
+    // xpose (LDS-only barriers: the x stores stay in flight until the publish)
+    auto finish = [&](int j, double y, double acc, const double (&li)[16], double* xs) {
+        sp[g * 64 + c] = acc;
+        lds_barrier();
+        if (tid < 64) sz[c] = y - (((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c]);
+        lds_barrier();
+        double xp = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; q++) xp = fma(li[q], sz[16 * g + q], xp);
-    sp[g * 64 + c] = xp;
-    lds_barrier();
-    if (tid < 64) {
-        const double xv = ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c];
-        st_coh(a.x + (int64_t)j * T + c, xv);
-        const int q = j * T + c;  // the pose-indexed copy the back rounds read (no scatter launch)
-        if (a.g.xpose && q < 7 * a.g.ntail) a.g.xpose[(int64_t)a.g.tail[q / 7] * 7 + q % 7] = xv;
+        for (int q = 0; q < 16; q++) xp = fma(li[q], sz[16 * g + q], xp);
+        sp[g * 64 + c] = xp;
+        lds_barrier();
+        if (tid < 64) {
+            const double xv = ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c];
+            xs[c] = xv;
+            st_coh(a.x + (int64_t)j * T + c, xv);
+            const int q = j * T + c;  // the pose-indexed copy the back rounds read (no scatter launch)
+            if (a.g.xpose && q < 7 * a.g.ntail) a.g.xpose[(int64_t)a.g.tail[q / 7] * 7 + q % 7] = xv;
+        }
+        lds_barrier();
+    };
+    bstamp(1);
+    finish(jh, yh, acc_h, lih, sxh);
+    bstamp(2);
+    if (two) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc_l = fma(lhl[q], sxh[16 * g + q], acc_l);
+        finish(jl, yl, acc_l, lil, sx);
     }
-    publish(a, xflag(nt, j));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_store(a.ready + xflag(nt, jh), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (two) __hip_atomic_store(a.ready + xflag(nt, jl), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    bstamp(3);
 }
 
 __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
@@ -826,10 +892,11 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
         cstamp(nt - 1, 3);
         return;
     }
-    const int ntasks = a.ntiles + (a.x != nullptr ? nt : 0);
+    const int ntasks = a.ntiles + (a.x != nullptr ? (nt + 1) / 2 : 0);
     for (int t = blockIdx.x - 1; t < ntasks; t += gridDim.x - 1) {
         if (t >= a.ntiles) {
-            back_task(a, nt - 1 - (t - a.ntiles), X);
+            const int jh = nt - 1 - 2 * (t - a.ntiles);
+            back_pair(a, jh, jh - 1, X);
             continue;
         }
         int j = 0, rem = t;

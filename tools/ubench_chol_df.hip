@@ -49,12 +49,12 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dLinv, chol_linv_bytes(npad)));
     CK(hipMalloc(&dX, npad * 8));
     CK(hipMalloc(&dflags, 64 * 4));
-    CK(hipMalloc(&dtr, (ntiles * 4 + 32 + 8 * nt) * 8));
+    CK(hipMalloc(&dtr, (ntiles * 4 + 32 + 12 * nt) * 8));
     CK(hipMemset(dtr, 0, (ntiles * 4 + 32 + 8 * nt) * 8));
     CK(hipMemcpy(dH0, H.data(), H.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemset(dflags, 0, 64 * 4));
     CK(hipMemset(chol_ready_ptr(dLinv, npad), 0, chol_ready_bytes(npad)));
-    std::vector<long long> tr(ntiles * 4 + 32 + 8 * nt);
+    std::vector<long long> tr(ntiles * 4 + 32 + 12 * nt);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -95,6 +95,12 @@ int main(int argc, char** argv) {
         printf("col %2d  C %7.2f %7.2f %7.2f\n", j, (ct[4 * j] - t0) * 0.01, (ct[4 * j + 1] - t0) * 0.01,
                (ct[4 * j + 2] - t0) * 0.01);
     printf("C end %.2f\n", (ct[4 * (nt - 1) + 3] - t0) * 0.01);
+    printf("back-substitution pairs (us from the chain's start): loaded / all x in / x_jh / published\n");
+    for (int p = 0; p < (nt + 1) / 2; p++) {
+        const long long* b = ct + 8 * nt + 4 * p;
+        printf("  pair %2d (%2d,%2d) %8.2f %8.2f %8.2f %8.2f\n", p, nt - 1 - 2 * p, nt - 2 - 2 * p, (b[0] - t0) * 0.01,
+               (b[1] - t0) * 0.01, (b[2] - t0) * 0.01, (b[3] - t0) * 0.01);
+    }
     printf("per column (us): P loads+staging / L_{j,j-1} GEMM / store+stage / syrk / potrf+inverse / to next\n");
     for (int j = 1; j < nt; j++) {
         const long long* f = ct + 4 * nt + 4 * j;
