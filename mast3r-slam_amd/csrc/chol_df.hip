@@ -831,7 +831,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             d4 accd[4];
             if (j >= 2) {
                 if (tid == 0) wait_ready(a.ready + hflag(nt, j), a.epoch, a.flags, a.spin_limit);
-                __syncthreads();
+                lds_barrier();  // (not __syncthreads: Linv_{j-1}'s stores stay in flight until the publish)
             }
             cstamp(j, 0);
             if (j == 0) {
@@ -862,7 +862,11 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 store_acc_coh(tile(j, j - 1), ld, accs);
                 lds_barrier();  // the GEMM's reads of X and Y are done (the stores stay in flight)
                 acc_to_lds(X, accs);
+#if !M3S_DF_CC
                 for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;  // Linv_{j-1} read: Y -> the new Li
+#endif
+                // (potrf_cc writes every block of Li it reads -- the diagonal and lower 16x16 blocks --
+                // and the Linv store below writes the upper ones as zeros: no zeroing pass on the chain)
                 if (tid < 8) Sync[tid] = 0;
                 lds_barrier();
                 fstamp(j, 2);
@@ -885,7 +889,8 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
 #pragma unroll
             for (int q = 0; q < 16; q++) {
                 const int id = tid + NT * q;
-                st_coh(Lk + id, Y[(id >> 6) * LD + (id & 63)]);
+                const int r = id >> 6, cl = id & 63;
+                st_coh(Lk + id, (cl >> 4) > (r >> 4) ? 0.0 : Y[r * LD + cl]);  // upper blocks: zeros
             }
         }
         publish(a, (nt - 1) * nt + (nt - 1));
