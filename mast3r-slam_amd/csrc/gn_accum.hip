@@ -919,7 +919,7 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
                                             int k0, int k1, const RelXf& T, const AccParams& P,
                                             const float* __restrict__ Zs, float* __restrict__ acc,
                                             const RawSrc& raw = RawSrc{}) {
-    static_assert(!FIRST || NP == 4, "the fused first iteration handles 4 points per step");
+    static_assert(NP == 4 || NP == 2, "4 or 2 points per step");
     constexpr int S = NP * kAccThreads;
     AccStage<MODE, RC, true, NP> cur;
     cur.width = P.width;
@@ -932,7 +932,29 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
     }
     // the records of NP points: one int4 per two
     auto records = [&](int kk, int4& a, int4& b) {
-        if constexpr (FIRST) {
+        if constexpr (FIRST && NP == 2) {
+            // (rays / points: 2 points per step) gn_pack_kernel's record, operation for operation
+            const uchar2 vm2 = *reinterpret_cast<const uchar2*>(raw.valid + kk);
+            const longlong2 id01 = *reinterpret_cast<const longlong2*>(raw.idx + kk);
+            const float2 q2 = *reinterpret_cast<const float2*>(raw.Q + kk);
+            const float2 cj2 =
+                raw.cj_all ? make_float2(0.f, 0.f) : *reinterpret_cast<const float2*>(raw.Cj_b + kk);
+            const bool vm[2] = {vm2.x != 0, vm2.y != 0};
+            const int64_t ids[2] = {id01.x, id01.y};
+            const float qs[2] = {q2.x, q2.y};
+            const float cjs[2] = {cj2.x, cj2.y};
+            int code[2], sqb[2];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int ind = match_index(ids[s], vm[s], P.HW);
+                const bool ok = vm[s] && (qs[s] > P.Q_thresh) && (raw.ci_all || raw.Ci_b[ind] > P.C_thresh) &&
+                                (raw.cj_all || cjs[s] > P.C_thresh);
+                code[s] = pack_code(ind, ok, P);
+                sqb[s] = __float_as_int(sqrt_cr(qs[s]));
+            }
+            a = int4{code[0], sqb[0], code[1], sqb[1]};
+            raw.pk_w[kk / 2] = a;
+        } else if constexpr (FIRST) {
             const uchar4 vm4 = *reinterpret_cast<const uchar4*>(raw.valid + kk);
             const longlong2 id01 = *reinterpret_cast<const longlong2*>(raw.idx + kk);
             const longlong2 id23 = *reinterpret_cast<const longlong2*>(raw.idx + kk + 2);
@@ -1057,7 +1079,7 @@ void gn_accum_packed_kernel(
         if (RCOK && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
             accum_steps<MODE, true, 4, true>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc, raw);
         else
-            accum_steps<MODE, false, 4, true>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc, raw);
+            accum_steps<MODE, false, acc_np<MODE>(), true>(Xj_b, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc, raw);
     } else if (RCOK && MODE == GN_CALIB && flags[kFlagNotRay] == 0 && (P.width & 3) == 0)
         // calib with ray-constrained keyframe points (gn_depth_kernel's check): Xj from its depth
         accum_steps<MODE, true, acc_np<MODE>()>(Zs + (int64_t)jx * HW, Xi_b, Zi_b, pk_b, k0, k1, T, P, Zs, acc);
@@ -1141,10 +1163,18 @@ hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float*
                                const int4* sched, float* partials, const int* flags, const float* px,
                                const int* pcnt, int* ecnt, double* edgeblk, const EdgeSrc* first_es,
                                const float* Cs, const int* cok) {
-    if (first_es != nullptr) {  // the first iteration builds the records (calib, positional stream)
-        if (mode != GN_CALIB || px != nullptr) return hipErrorInvalidValue;
+    if (first_es != nullptr) {  // the first iteration builds the records (positional stream)
+        if (px != nullptr) return hipErrorInvalidValue;
         const FirstSrc fs{*first_es, Cs, cok, const_cast<int4*>(pack)};
-        if (P.raycheck)
+        if (mode == GN_RAYS)
+            hipLaunchKernelGGL((gn_accum_packed_kernel<GN_RAYS, false, false, true>), grid, dim3(kAccThreads), 0, st,
+                               Twc, Xs, Zs, ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt,
+                               edgeblk, fs);
+        else if (mode == GN_POINTS)
+            hipLaunchKernelGGL((gn_accum_packed_kernel<GN_POINTS, false, false, true>), grid, dim3(kAccThreads), 0, st,
+                               Twc, Xs, Zs, ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt,
+                               edgeblk, fs);
+        else if (P.raycheck)
             hipLaunchKernelGGL((gn_accum_packed_kernel<GN_CALIB, false, true, true>), grid, dim3(kAccThreads), 0, st,
                                Twc, Xs, Zs, ii_loc, jj_loc, pack, P, sched, partials, flags, px, pcnt, ecnt,
                                edgeblk, fs);

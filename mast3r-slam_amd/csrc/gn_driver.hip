@@ -1106,12 +1106,12 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     std::memset(h + (L.ecnt - lo), 0, sizeof(int) * (size_t)a.E_local);  // (the kernel re-zeroes them)
     std::memset(h + (L.cok - lo), 1, sizeof(int) * (size_t)std::max<int64_t>(a.N, 1));  // gn_cpass_kernel clears
     M3S_HIP_CHECK(stagings().ws.upload(c.ws + lo, h, L.sched - lo, c.st));
-    // M3S_GN_PACK_FIRST (default 1): a calib call's first accumulate builds the packed records
+    // M3S_GN_PACK_FIRST (default 1): a call's first accumulate builds the packed records
     // from the reference's inputs itself (gn_accum_packed_kernel<..., FIRST>): 13 B read + 8 B
     // written per point-edge inside the first iteration instead of a separate 21-B pack pass
     // followed by the first iteration's 8-B record reads (run() only: its early pack)
-    c.first_pack = early_pack && c.packed && !c.compact && !c.ref_order && a.mode == M3S_GN_CALIB &&
-                   a.max_iter > 0 && env_int("M3S_GN_PACK_FIRST", 1) != 0;
+    c.first_pack = early_pack && c.packed && !c.compact && !c.ref_order && a.max_iter > 0 &&
+                   env_int("M3S_GN_PACK_FIRST", 1) != 0;
     if (early_pack) {
         rc = prepare_iterations(a, c);
         if (rc) return rc;

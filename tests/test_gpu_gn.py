@@ -286,13 +286,15 @@ def test_confidence_pass_skips_only_passing_keyframes(backend, monkeypatch, mode
     assert np.array_equal(H0, H2, equal_nan=True) and np.array_equal(b0, b2, equal_nan=True)
 
 
-@pytest.mark.parametrize("ray_constrained", [True, False])
-def test_first_iteration_builds_the_packed_records(backend, monkeypatch, ray_constrained):
-    """A calib call's first accumulate builds the packed records from the reference's inputs
+@pytest.mark.parametrize("mode,ray_constrained", [("calib", True), ("calib", False), ("rays", False),
+                                                  ("points", False)])
+def test_first_iteration_builds_the_packed_records(backend, monkeypatch, mode, ray_constrained):
+    """A call's first accumulate builds the packed records from the reference's inputs
     (M3S_GN_PACK_FIRST=1, default) instead of a separate pack pass: the same records, so the
     poses and dx after 3 iterations are bitwise those of the separate pass -- with confidences
-    at / below C_thresh, a NaN confidence, Q below Q_thresh and unmatched points; both the
-    ray-constrained (depth-only Xj) and the positional stream."""
+    at / below C_thresh, a NaN confidence, Q below Q_thresh and unmatched points; calib on both
+    the ray-constrained (depth-only Xj) and the positional stream, rays and points (2 points per
+    lane and step)."""
     g = _graph("calib", N=6, E=8)
     if not ray_constrained:
         g.Xs = (g.Xs * 1.0001).contiguous()  # off the rays: the positional stream
@@ -309,10 +311,19 @@ def test_first_iteration_builds_the_packed_records(backend, monkeypatch, ray_con
         monkeypatch.setenv("M3S_GN_PACK_FIRST", first)
         Twc = g.Twc.clone().cuda()
         c = lambda t: t.cuda()
-        (dx,) = backend.gauss_newton_calib(Twc, c(g.Xs), c(g.Cs), c(g.K), c(g.ii), c(g.jj), c(g.idx),
-                                           c(g.valid), c(g.Q), g.H, g.W, Lc["pixel_border"],
-                                           Lc["depth_eps"], Lc["sigma_pixel"], Lc["sigma_depth"],
-                                           Lc["C_conf"], Lc["Q_conf"], 3, 0.0)
+        if mode == "calib":
+            (dx,) = backend.gauss_newton_calib(Twc, c(g.Xs), c(g.Cs), c(g.K), c(g.ii), c(g.jj), c(g.idx),
+                                               c(g.valid), c(g.Q), g.H, g.W, Lc["pixel_border"],
+                                               Lc["depth_eps"], Lc["sigma_pixel"], Lc["sigma_depth"],
+                                               Lc["C_conf"], Lc["Q_conf"], 3, 0.0)
+        elif mode == "rays":
+            (dx,) = backend.gauss_newton_rays(Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx), c(g.valid),
+                                              c(g.Q), Lc["sigma_ray"], Lc["sigma_dist"], Lc["C_conf"],
+                                              Lc["Q_conf"], 3, 0.0)
+        else:
+            (dx,) = backend.gauss_newton_points(Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx),
+                                                c(g.valid), c(g.Q), Lc["sigma_point"], Lc["C_conf"],
+                                                Lc["Q_conf"], 3, 0.0)
         torch.cuda.synchronize()
         out.append((Twc.cpu().numpy(), dx.cpu().numpy()))
     assert np.isfinite(out[1][0]).all()

@@ -1,0 +1,10 @@
+#!/bin/bash
+# rays / points first accumulate builds the records (no pack pass): tests + cfg4 A/B (M3S_GN_PACK_FIRST)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_gn.py tests/test_gpu_dist.py tests/test_gpu_factor_graph.py tests/test_gpu_gn_stress.py > gpurun_out/r04ac_pytest.log 2>&1 || { echo "pytest rc=$?"; tail -30 gpurun_out/r04ac_pytest.log; exit 1; }
+tail -1 gpurun_out/r04ac_pytest.log
+for v in 1 0 1 0; do
+M3S_GN_PACK_FIRST=$v timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-matching > gpurun_out/r04ac_bench_f$v.json 2> gpurun_out/r04ac_bench_f$v.err || { echo "bench rc=$?"; tail -5 gpurun_out/r04ac_bench_f$v.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/r04ac_bench_f$v.json')); c=d.get('cfg4',{}); print('first=$v cfg3', round(d['value']), round(d['ms_per_step'],3), 'cfg4', round(c.get('value',0)), round(c.get('ms_per_step'),3), {k: round(x,4) for k,x in c.get('phase_ms_per_iter').items()})"
+done
