@@ -30,6 +30,12 @@
 #ifndef M3S_DF_CC
 #define M3S_DF_CC 1  // 1: the column-cyclic tile factor (potrf_cc); 0: the 8-column panel steps (potrf_inverse)
 #endif
+#ifndef M3S_DF_BC
+#define M3S_DF_BC 1  // 1: batch-cyclic tile factor (potrf_bc_w); 0: 16-column blocks per wave (potrf_cc_w)
+#endif
+#ifndef M3S_DF_BC_W
+#define M3S_DF_BC_W 4  // columns per batch of potrf_bc_w (4; 8 measured slower)
+#endif
 #ifndef M3S_DF_STAMPS
 #define M3S_DF_STAMPS 0  // diagnostics (tools/ubench_potrf64.hip): cycle stamps inside the potrf steps
 #endif
@@ -404,6 +410,9 @@ __device__ __forceinline__ void diag_inv16(const double* A, double* Li, const do
     Li[(c0 + 8 + r) * LD + c0 + c] = -x;
 }
 
+// LDS ints of the tile factor: [0] columns published, [1 + w] X_ww written, [8 + w] wave w's
+// batches written to the tile (potrf_bc_w)
+constexpr int kDfSync = 12;
 // LDS scratch of potrf_cc (doubles): per wave 64 + a 16x17 block, then per wave a [64][4] batch
 constexpr int kCcScrBase = 4 * 64 + 4 * 16 * 17;
 constexpr int kCcScr = kCcScrBase + 4 * 256;
@@ -551,15 +560,197 @@ __device__ __forceinline__ void potrf_cc_w(double* A, double* Li, double* Lc, do
     }
 }
 
+// Batch-cyclic variant (M3S_DF_BC=1): the tile's 16 batches of 4 columns go round-robin to the
+// 4 waves (batch b -> wave b % 4; wave w holds columns 16 lb + 4 w + p in registers, lane = row).
+// The owner of batch b applies batch b-1 to its 4 columns only, factors them (pivots by
+// v_readlane, as potrf_cc) and publishes them as a row-major [64][4] copy (Lb + 256 b; the
+// consumers read a target row's 4 values with two uniform ds_read_b128) plus into the tile (the
+// inverse reads L there); every wave applies each published batch to its own later columns off
+// the critical path.  The pivot chain thus hands over every 4 columns instead of every 16, and
+// between two of its columns the owner issues 4 FMAs of rank-4 update instead of the whole
+// 16-column block's -- the owner's issue, not the hand-off, bounded potrf_cc (~260 cycles per
+// column).  The inverse (X_WW by wave W, then the column-block products) follows the last batch;
+// it reads L from the tile, which each wave writes after its publish (off the critical path) and
+// announces on its own counter (sync[8 + w]: batches written).  Measured (ubench_potrf64 /
+// ubench_chol_df, profiles/r04_ak_*): ~940 cycles per batch hand-off + factor, tile factor +
+// inverse 8.0 us vs potrf_cc's 10.2 us in the chain; 8-column batches (M3S_DF_BC_W=8) 9.6 us.
+template <int W, int BW>
+__device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, double* scratch, int* sync, double* Dinv,
+                                           int* flags, long long* pt) {
+    constexpr int NL = 16 / BW;  // local batches per wave
+    const int lane = threadIdx.x & 63;
+    auto wstamp = [&](int k) {
+#if M3S_DF_STAMPS
+        if (pt && lane == 0) pt[8 * W + k] = (long long)__builtin_amdgcn_s_memtime();
+#endif
+    };
+    wstamp(0);
+    double a[16];  // a[BW lb + p]: column BW (4 lb + W) + p
+#pragma unroll
+    for (int lb = 0; lb < NL; lb++)
+#pragma unroll
+        for (int p = 0; p < BW; p++) a[BW * lb + p] = A[lane * LD + BW * (4 * lb + W) + p];
+    bool bad = false;
+    // batch b (published) applied to my local batches lb0 .. lb1 - 1
+    auto apply = [&](int b, int lb0, int lb1) {
+        const double* Lr = Lb + 64 * BW * b;
+        double2 r[BW / 2];
+#pragma unroll
+        for (int k = 0; k < BW / 2; k++) r[k] = *reinterpret_cast<const double2*>(Lr + lane * BW + 2 * k);
+#pragma unroll
+        for (int lb = 0; lb < NL; lb++) {
+            if (lb < lb0 || lb >= lb1) continue;
+            double2 cv[BW][BW / 2];
+#pragma unroll
+            for (int p = 0; p < BW; p++)
+#pragma unroll
+                for (int k = 0; k < BW / 2; k++)
+                    cv[p][k] = *reinterpret_cast<const double2*>(Lr + (BW * (4 * lb + W) + p) * BW + 2 * k);
+#pragma unroll
+            for (int p = 0; p < BW; p++) {
+                double v = a[BW * lb + p];
+#pragma unroll
+                for (int k = 0; k < BW / 2; k++) {
+                    v = fma(-r[k].x, cv[p][k].x, v);
+                    v = fma(-r[k].y, cv[p][k].y, v);
+                }
+                a[BW * lb + p] = v;
+            }
+        }
+    };
+    int next = 0;  // the next batch to apply to my columns
+#pragma unroll
+    for (int lb = 0; lb < NL; lb++) {
+        const int nb = 4 * lb + W;
+        // the other waves' earlier batches, to all my remaining columns (off the critical path)
+#pragma unroll 1
+        for (; next < nb - 1; next++) {
+            lds_wait_geq(sync, BW * (next + 1), flags);
+            apply(next, lb, NL);
+        }
+        if (nb >= 1) {  // the previous batch: to this batch's columns first (the critical path)
+            lds_wait_geq(sync, BW * nb, flags);
+            apply(nb - 1, lb, lb + 1);
+        }
+        // factor the batch: pivot chain inside it by v_readlane
+        const int c0 = BW * nb;
+        double y[BW];
+#pragma unroll
+        for (int p = 0; p < BW; p++) {
+            const int jj = BW * lb + p, c = c0 + p;
+            const double d = rdlane(a[jj], c);
+            bad |= d <= 0.0;  // SimplicialLLT: fails iff a pivot <= 0 (NaN passes)
+            double r = __builtin_amdgcn_rsq(d);
+            r = r * fma(-0.5 * d * r, r, 1.5);
+            y[p] = r;
+            a[jj] *= r;
+#pragma unroll
+            for (int q = p + 1; q < BW; q++) a[BW * lb + q] = fma(-a[jj], rdlane(a[jj], c0 + q), a[BW * lb + q]);
+        }
+        // publish: the row-major copy, then the counter (a wave's LDS operations execute in order)
+        double* Lr = Lb + 64 * BW * nb;
+#pragma unroll
+        for (int k = 0; k < BW / 2; k++)
+            *reinterpret_cast<double2*>(Lr + lane * BW + 2 * k) = double2{a[BW * lb + 2 * k], a[BW * lb + 2 * k + 1]};
+        lds_publish(sync, BW * (nb + 1));
+        wstamp(1 + lb);
+        // the columns into the tile and 1 / l_pp (the inverse reads both): off the critical path,
+        // published by this wave's own counter
+#pragma unroll
+        for (int p = 0; p < BW; p++) A[lane * LD + c0 + p] = a[BW * lb + p];
+        {
+            double yl = y[0];
+#pragma unroll
+            for (int p = 1; p < BW; p++) yl = lane == p ? y[p] : yl;
+            if (lane < BW) Dinv[c0 + lane] = yl;
+        }
+        lds_publish(sync + 8 + W, lb + 1);
+        // the previous batch and my own, to my later columns
+        if (lb < NL - 1) {
+            if (nb >= 1) apply(nb - 1, lb + 1, NL);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my copy of batch nb is in LDS
+            apply(nb, lb + 1, NL);
+        }
+        next = nb + 1;
+    }
+    if (lane == 0 && bad) flags[kFlagFail] = 1;
+    // the inverse, as potrf_cc's step 3, with L read from the tile
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int C0 = 16 * W;
+    double* scr = scratch + 64 * W;
+    double* sT = scratch + 4 * 64 + 16 * 17 * W;
+    // columns < C of L written to the tile: each wave's batches below C / BW (in order per wave)
+    auto wait_written = [&](int C) {
+        int need[4], spins = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) need[q] = C / BW > q ? (C / BW - q + 3) / 4 : 0;
+        for (;;) {  // the four counters read together: one LDS round trip per poll
+            int n[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) n[q] = __hip_atomic_load(sync + 8 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (n[0] >= need[0] && n[1] >= need[1] && n[2] >= need[2] && n[3] >= need[3]) break;
+            __builtin_amdgcn_s_sleep(0);
+            if (++spins > (1 << 24)) {  // cannot happen (the producers are this workgroup's waves)
+                flags[kFlagFail] = 1;
+                break;
+            }
+        }
+        asm volatile("" ::: "memory");
+    };
+    wait_written(16 * (W + 1));  // block column W of L complete in the tile
+    diag_inv16(A, Li, Dinv, C0, scr);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_publish(sync + 1 + W, 1);
+    wstamp(5);
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int V = W + 1; V < 4; V++) {
+        wait_written(16 * V);
+        d4 acc[4];
+#pragma unroll
+        for (int m = W; m < V; m++) {
+            acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int st = 0; st < 4; st++)
+                acc[m] = mfma(A[(16 * V + r16) * LD + 16 * m + 4 * st + kq], Li[(16 * m + 4 * st + kq) * LD + C0 + r16],
+                              acc[m]);
+        }
+        d4 t = acc[W];
+#pragma unroll
+        for (int m = W + 1; m < V; m++) t += acc[m];
+#pragma unroll
+        for (int e = 0; e < 4; e++) sT[(kq + 4 * e) * 17 + r16] = t[e];
+        lds_wait_geq(sync + 1 + V, 1, flags);  // X_VV
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        d4 x = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 4; st++)
+            x = mfma(-Li[(16 * V + r16) * LD + 16 * V + 4 * st + kq], sT[(4 * st + kq) * 17 + r16], x);
+#pragma unroll
+        for (int e = 0; e < 4; e++) Li[(16 * V + kq + 4 * e) * LD + C0 + r16] = x[e];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    wstamp(6);
+}
+
 // the column-cyclic factor + inverse of the tile (Li zeroed, sync[0..4] zeroed, both visible)
 __device__ __forceinline__ void potrf_cc(double* A, double* Li, double* Lc, double* scratch, int* sync, double* Dinv,
                                          int* flags, long long* pt = nullptr) {
+#if M3S_DF_BC
+    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+        case 0: potrf_bc_w<0, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        case 1: potrf_bc_w<1, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        case 2: potrf_bc_w<2, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        default: potrf_bc_w<3, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+    }
+#else
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
         case 0: potrf_cc_w<0>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
         case 1: potrf_cc_w<1>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
         case 2: potrf_cc_w<2>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
         default: potrf_cc_w<3>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
     }
+#endif
     __syncthreads();
 }
 
@@ -810,7 +1001,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
     __shared__ __attribute__((aligned(16))) double Z[T * LD];
     __shared__ double Dinv[T];
     __shared__ double Scr[kCcScr];
-    __shared__ int Sync[8];
+    __shared__ int Sync[kDfSync];
     const int tid = threadIdx.x;
     const int nt = a.nt;
     const int64_t ld = a.npad;
@@ -838,7 +1029,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 load_src(accd, a, 0, 0);
                 acc_to_lds(Z, accd);
                 for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;
-                if (tid < 8) Sync[tid] = 0;
+                if (tid < kDfSync) Sync[tid] = 0;
                 __syncthreads();
             } else {
                 d4 accs[4];
@@ -867,7 +1058,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
 #endif
                 // (potrf_cc writes every block of Li it reads -- the diagonal and lower 16x16 blocks --
                 // and the Linv store below writes the upper ones as zeros: no zeroing pass on the chain)
-                if (tid < 8) Sync[tid] = 0;
+                if (tid < kDfSync) Sync[tid] = 0;
                 lds_barrier();
                 fstamp(j, 2);
                 syrk_lower(Z, X);  // A'_jj = P_d(j) - L_{j,j-1} L_{j,j-1}^T (lower blocks)

@@ -52,12 +52,12 @@ __global__ __launch_bounds__(NT) void k_potrf_cc(const double* __restrict__ A0, 
     __shared__ __attribute__((aligned(16))) double Z[T * LD];
     __shared__ double Dinv[T];
     __shared__ double Scr[kCcScr];
-    __shared__ int Sync[8];
+    __shared__ int Sync[kDfSync];
     const int tid = threadIdx.x;
     const double* A = A0 + (size_t)blockIdx.x * T * T;
     for (int id = tid; id < T * T; id += NT) Z[(id >> 6) * LD + (id & 63)] = A[id];
     for (int id = tid; id < T * LD; id += NT) Y[id] = 0.0;
-    if (tid < 8) Sync[tid] = 0;
+    if (tid < kDfSync) Sync[tid] = 0;
     __syncthreads();
     long long* p = pt + (size_t)blockIdx.x * 64;
     const long long t0 = (long long)__builtin_amdgcn_s_memtime();
@@ -213,7 +213,11 @@ int main(int argc, char** argv) {
         printf("potrf_cc tile 0, cycles from start: wave: applied / factored / diag-inv start / X_ww / X_Vw...\n");
         for (int w = 0; w < 4; w++) {
             printf("  wave %d:", w);
+#if M3S_DF_BC
+            for (int k = 1; k <= 6; k++) printf(" %7lld", pc[8 * w + k] - pc[60]);  // batches lb 0-3 / X_ww / end
+#else
             for (int k = 1; k < 4 + 3 - w; k++) printf(" %7lld", pc[8 * w + k] - pc[60]);
+#endif
             printf("\n");
         }
         printf("  end: %lld\n", pc[61] - pc[60]);
