@@ -33,6 +33,9 @@
 #ifndef M3S_DF_BC
 #define M3S_DF_BC 1  // 1: batch-cyclic tile factor (potrf_bc_w); 0: 16-column blocks per wave (potrf_cc_w)
 #endif
+#ifndef M3S_DF_BC_SPEC
+#define M3S_DF_BC_SPEC 1  // potrf_bc_w: poll the counter and read the batch in one LDS round trip
+#endif
 #ifndef M3S_DF_BC_W
 #define M3S_DF_BC_W 4  // columns per batch of potrf_bc_w (4; 8 measured slower)
 #endif
@@ -584,6 +587,16 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
         if (pt && lane == 0) pt[8 * W + k] = (long long)__builtin_amdgcn_s_memtime();
 #endif
     };
+    // per-batch stamps (ubench_potrf64 only: M3S_DF_BSTAMPS): pt[20 + 2 nb] the critical wait
+    // done, pt[21 + 2 nb] the critical apply done
+    auto bstamp = [&](int k) {
+#if M3S_DF_STAMPS && M3S_DF_BSTAMPS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (pt && lane == 0) pt[20 + k] = (long long)__builtin_amdgcn_s_memtime();
+#else
+        (void)k;
+#endif
+    };
     wstamp(0);
     double a[16];  // a[BW lb + p]: column BW (4 lb + W) + p
 #pragma unroll
@@ -618,6 +631,38 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
             }
         }
     };
+    constexpr int C0 = 16 * W;
+    double* scr = scratch + 64 * W;
+    double* sT = scratch + 4 * 64 + 16 * 17 * W;
+    // columns < C of L written to the tile: each wave's batches below C / BW (in order per wave)
+    auto wait_written = [&](int C) {
+        int need[4], spins = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) need[q] = C / BW > q ? (C / BW - q + 3) / 4 : 0;
+        for (;;) {  // the four counters read together: one LDS round trip per poll
+            int n[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) n[q] = __hip_atomic_load(sync + 8 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (n[0] >= need[0] && n[1] >= need[1] && n[2] >= need[2] && n[3] >= need[3]) break;
+            __builtin_amdgcn_s_sleep(0);
+            if (++spins > (1 << 24)) {  // cannot happen (the producers are this workgroup's waves)
+                flags[kFlagFail] = 1;
+                break;
+            }
+        }
+        asm volatile("" ::: "memory");
+    };
+    // X_WW = (L_WW)^-1 once block column W of L is in the tile.  (Doing it for waves 0 and 1
+    // inside the batch loop, as soon as their block is complete, measured slower: 292 vs 283 us
+    // on the cfg4-size chain -- the column-block products, not X_WW, end the tile.)
+    auto diag_block = [&]() {
+        wait_written(16 * (W + 1));
+        bstamp(32 + W);
+        diag_inv16(A, Li, Dinv, C0, scr);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_publish(sync + 1 + W, 1);
+        wstamp(5);
+    };
     int next = 0;  // the next batch to apply to my columns
 #pragma unroll
     for (int lb = 0; lb < NL; lb++) {
@@ -629,10 +674,51 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
             apply(next, lb, NL);
         }
         if (nb >= 1) {  // the previous batch: to this batch's columns first (the critical path)
+#if M3S_DF_BC_SPEC
+            // the counter and the batch's values read together, the values kept once the counter
+            // shows the batch published (the producer stored them before the counter, and a wave's
+            // LDS reads execute in order): one LDS round trip per hand-off instead of two (wait +
+            // apply ~490 -> ~400 cycles per batch, bitwise the same L; profiles/r04_ao_*)
+            const double* Lr = Lb + 64 * BW * (nb - 1);
+            double2 r[BW / 2], cv[BW][BW / 2];
+            for (int spins = 0;; spins++) {
+                const int n = __hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int k = 0; k < BW / 2; k++) r[k] = *reinterpret_cast<const double2*>(Lr + lane * BW + 2 * k);
+#pragma unroll
+                for (int p = 0; p < BW; p++)
+#pragma unroll
+                    for (int k = 0; k < BW / 2; k++)
+                        cv[p][k] = *reinterpret_cast<const double2*>(Lr + (BW * nb + p) * BW + 2 * k);
+                if (n >= BW * nb) break;
+                __builtin_amdgcn_s_sleep(0);
+                if (spins > (1 << 24)) {  // cannot happen (the producer is this workgroup's wave)
+                    flags[kFlagFail] = 1;
+                    break;
+                }
+            }
+            bstamp(2 * nb);
+#pragma unroll
+            for (int p = 0; p < BW; p++) {
+                double v = a[BW * lb + p];
+#pragma unroll
+                for (int k = 0; k < BW / 2; k++) {
+                    v = fma(-r[k].x, cv[p][k].x, v);
+                    v = fma(-r[k].y, cv[p][k].y, v);
+                }
+                a[BW * lb + p] = v;
+            }
+#else
             lds_wait_geq(sync, BW * nb, flags);
+            bstamp(2 * nb);
             apply(nb - 1, lb, lb + 1);
+#endif
+            bstamp(2 * nb + 1);
         }
-        // factor the batch: pivot chain inside it by v_readlane
+        // factor the batch: pivot chain inside it by v_readlane.  (Reading the batch's diagonal
+        // block once and factoring it as wave-uniform values -- bitwise the same L -- measured
+        // no faster: ~600 cycles per batch either way.)
         const int c0 = BW * nb;
         double y[BW];
 #pragma unroll
@@ -676,32 +762,7 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
     if (lane == 0 && bad) flags[kFlagFail] = 1;
     // the inverse, as potrf_cc's step 3, with L read from the tile
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    constexpr int C0 = 16 * W;
-    double* scr = scratch + 64 * W;
-    double* sT = scratch + 4 * 64 + 16 * 17 * W;
-    // columns < C of L written to the tile: each wave's batches below C / BW (in order per wave)
-    auto wait_written = [&](int C) {
-        int need[4], spins = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) need[q] = C / BW > q ? (C / BW - q + 3) / 4 : 0;
-        for (;;) {  // the four counters read together: one LDS round trip per poll
-            int n[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) n[q] = __hip_atomic_load(sync + 8 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (n[0] >= need[0] && n[1] >= need[1] && n[2] >= need[2] && n[3] >= need[3]) break;
-            __builtin_amdgcn_s_sleep(0);
-            if (++spins > (1 << 24)) {  // cannot happen (the producers are this workgroup's waves)
-                flags[kFlagFail] = 1;
-                break;
-            }
-        }
-        asm volatile("" ::: "memory");
-    };
-    wait_written(16 * (W + 1));  // block column W of L complete in the tile
-    diag_inv16(A, Li, Dinv, C0, scr);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    lds_publish(sync + 1 + W, 1);
-    wstamp(5);
+    diag_block();
     const int r16 = lane & 15, kq = lane >> 4;
 #pragma unroll
     for (int V = W + 1; V < 4; V++) {

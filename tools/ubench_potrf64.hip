@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -191,7 +192,15 @@ int main(int argc, char** argv) {
             for (int r = 0; r < 64; r++)
                 for (int c = r + 1; c < 64; c++) e2 = std::max(e2, std::fabs(li[r * 64 + c]));  // upper Li must be 0
         }
-        printf("%s: max |L L^T - A| %.3e, max |Li L - I| (and upper Li) %.3e\n", name, e1, e2);
+        unsigned long long hsh = 0;  // bit pattern digest of L and Li (variants that claim bitwise equality)
+        for (size_t k = 0; k < L.size(); k++) {
+            unsigned long long u, v;
+            memcpy(&u, &L[k], 8);
+            memcpy(&v, &Li[k], 8);
+            hsh = (hsh ^ u) * 0x100000001b3ull;
+            hsh = (hsh ^ v) * 0x100000001b3ull;
+        }
+        printf("%s: max |L L^T - A| %.3e, max |Li L - I| (and upper Li) %.3e, digest %016llx\n", name, e1, e2, hsh);
     };
     CK(hipMemset(dpt, 0, (size_t)ntile * 64 * 8));
     for (int rep = 0; rep < 3; rep++) {
@@ -221,6 +230,17 @@ int main(int argc, char** argv) {
             printf("\n");
         }
         printf("  end: %lld\n", pc[61] - pc[60]);
+#if M3S_DF_BC && M3S_DF_BSTAMPS
+        printf("per batch (cycles): previous publish -> wait done -> critical apply done -> publish\n");
+        for (int nb = 1; nb < 16; nb++) {
+            auto pub = [&](int b) { return pc[8 * (b & 3) + 1 + (b >> 2)]; };
+            printf("  batch %2d: %5lld %5lld %5lld\n", nb, pc[20 + 2 * nb] - pub(nb - 1),
+                   pc[21 + 2 * nb] - pc[20 + 2 * nb], pub(nb) - pc[21 + 2 * nb]);
+        }
+        printf("inverse (cycles from start): wave: written-wait done / X_ww done / end\n");
+        for (int w = 0; w < 4; w++)
+            printf("  wave %d: %6lld %6lld %6lld\n", w, pc[52 + w] - pc[60], pc[8 * w + 5] - pc[60], pc[8 * w + 6] - pc[60]);
+#endif
     }
     // cycles (s_memtime) for tile 0: per panel step, relative to the previous step's barrier
     const long long* p = &pt[0];
