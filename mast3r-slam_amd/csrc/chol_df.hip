@@ -36,6 +36,9 @@
 #ifndef M3S_DF_BC_SPEC
 #define M3S_DF_BC_SPEC 1  // potrf_bc_w: poll the counter and read the batch in one LDS round trip
 #endif
+#ifndef M3S_DF_BC_RL
+#define M3S_DF_BC_RL 1  // potrf_bc_w: the inverse's column-block products right-looking
+#endif
 #ifndef M3S_DF_BC_W
 #define M3S_DF_BC_W 4  // columns per batch of potrf_bc_w (4; 8 measured slower)
 #endif
@@ -764,6 +767,38 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     diag_block();
     const int r16 = lane & 15, kq = lane >> 4;
+#if M3S_DF_BC_RL
+    // block column W of Li, right-looking: once X_mW is known, its products L_Vm X_mW go into
+    // every later block row's accumulator (t_V = sum_m L_Vm X_mW), the next row's first; then
+    // X_{m+1,W} = -X_{m+1,m+1} t_{m+1}.  Only the last product waits on X_33, instead of the whole
+    // t_3W (up to 12 MFMAs) being issued after X_20 / X_21.  The same products summed in another
+    // order than the left-looking form below (the acc[m] chains added in m order): not bitwise.
+    // (L's block column m is in the tile: for m = W diag_block waited for it, for m > W the wave
+    // that published X_mm did.)
+    d4 acc[4];
+#pragma unroll
+    for (int V = 0; V < 4; V++) acc[V] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int m = W; m < 3; m++) {
+#pragma unroll
+        for (int V = m + 1; V < 4; V++)
+#pragma unroll
+            for (int st = 0; st < 4; st++)
+                acc[V] = mfma(A[(16 * V + r16) * LD + 16 * m + 4 * st + kq], Li[(16 * m + 4 * st + kq) * LD + C0 + r16],
+                              acc[V]);
+        const int V = m + 1;
+#pragma unroll
+        for (int e = 0; e < 4; e++) sT[(kq + 4 * e) * 17 + r16] = acc[V][e];
+        lds_wait_geq(sync + 1 + V, 1, flags);  // X_VV
+        d4 x = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 4; st++)
+            x = mfma(-Li[(16 * V + r16) * LD + 16 * V + 4 * st + kq], sT[(4 * st + kq) * 17 + r16], x);
+#pragma unroll
+        for (int e = 0; e < 4; e++) Li[(16 * V + kq + 4 * e) * LD + C0 + r16] = x[e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
 #pragma unroll
     for (int V = W + 1; V < 4; V++) {
         wait_written(16 * V);
@@ -791,6 +826,7 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
         for (int e = 0; e < 4; e++) Li[(16 * V + kq + 4 * e) * LD + C0 + r16] = x[e];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+#endif
     wstamp(6);
 }
 
