@@ -655,9 +655,10 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
         }
         asm volatile("" ::: "memory");
     };
-    // X_WW = (L_WW)^-1 once block column W of L is in the tile.  (Doing it for waves 0 and 1
-    // inside the batch loop, as soon as their block is complete, measured slower: 292 vs 283 us
-    // on the cfg4-size chain -- the column-block products, not X_WW, end the tile.)
+    // X_WW = (L_WW)^-1 once block column W of L is in the tile.  (Measured slower: doing it for
+    // waves 0 and 1 inside the batch loop as soon as their block is complete, 292 vs 283 us on the
+    // cfg4-size chain; X_WW as 16 forward substitutions of 16 rows by lanes 0-15 instead of
+    // diag_inv16's two 8x8 inverses + products, ~2.8k vs ~1.8k cycles, 284 vs 278 us.)
     auto diag_block = [&]() {
         wait_written(16 * (W + 1));
         bstamp(32 + W);
