@@ -28,7 +28,7 @@
 #include "gn_kernels.h"
 
 #ifndef M3S_DF_CC
-#define M3S_DF_CC 1  // 1: the column-cyclic tile factor (potrf_cc); 0: the 8-column panel steps (potrf_inverse)
+#define M3S_DF_CC 1  // 1: the register tile factor (potrf_cc: batch- or column-cyclic, M3S_DF_BC); 0: the 8-column panel steps (potrf_inverse)
 #endif
 #ifndef M3S_DF_BC
 #define M3S_DF_BC 1  // 1: batch-cyclic tile factor (potrf_bc_w); 0: 16-column blocks per wave (potrf_cc_w)
@@ -831,7 +831,8 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
     wstamp(6);
 }
 
-// the column-cyclic factor + inverse of the tile (Li zeroed, sync[0..4] zeroed, both visible)
+// the register factor + inverse of the tile: batch-cyclic (potrf_bc_w, M3S_DF_BC=1, default) or
+// column-cyclic (potrf_cc_w); sync[0 .. kDfSync) zeroed and visible
 __device__ __forceinline__ void potrf_cc(double* A, double* Li, double* Lc, double* scratch, int* sync, double* Dinv,
                                          int* flags, long long* pt = nullptr) {
 #if M3S_DF_BC

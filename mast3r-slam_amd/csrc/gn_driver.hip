@@ -1404,7 +1404,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
                                           sp.iptr(sp.i_tc3), sp.iptr(sp.i_rc4), A, b, Ls, W, y, flags));
     }
     // M3S_HYB_CORE=1 (default): the hybrid's dense core (<= 27 poses) is factored and solved by
-    // the dataflow launch (chol_df.hip: column-cyclic tile factor, ~150 ns per column on the
+    // the dataflow launch (chol_df.hip: batch-cyclic tile factor, ~100 ns per column on the
     // pivot chain, back-substitution in the same launch) instead of gn_solve's in-register pose
     // steps (~330-430 ns per column); gn_solve then only back-substitutes through the rounds
     // and retracts.  0: the in-register core.
