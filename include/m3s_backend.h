@@ -127,10 +127,16 @@ int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D1
 void m3s_gn_debug_flags(int* out4);
 
 /* Deferred error report.  A GN call whose solver has bounded device-side waits (the dataflow
- * factorisation) exports its timeout flag without a host wait; M3S_ERR_TIMEOUT for it is
- * returned by the next GN call on the same host thread (before it does any work) or by this
- * function, which synchronises `stream` (hipStream_t) first.  Env M3S_GN_TIMEOUT_SYNC=1 reports it
- * from the call itself.  Returns M3S_OK, M3S_ERR_TIMEOUT (then cleared) or M3S_ERR_HIP. */
+ * factorisation) exports its timeout flag without a host wait.  A call whose wait timed out
+ * restores Twc to the poses it started from on the device (its result is discarded; every rank of
+ * a sharded call restores), so it never commits poses.  M3S_ERR_TIMEOUT for it is returned by this
+ * function, which synchronises `stream` (hipStream_t) first, or else by the next
+ * m3s_gauss_newton_* call on the same host thread: that call checks the flag once its per-call
+ * setup has synchronised the stream -- after the setup's own work (the edge-range exchange of a
+ * sharded call, the plan uploads, the workspace allocation), before its first GN iteration -- and
+ * returns without running an iteration.  m3s_gn_build_system and m3s_gn_edge_hessians do not
+ * check it.  Env M3S_GN_TIMEOUT_SYNC=1 reports it from the call itself.  Returns M3S_OK,
+ * M3S_ERR_TIMEOUT (then cleared) or M3S_ERR_HIP. */
 int m3s_gn_check(void* stream);
 
 enum { M3S_GN_POINTS = 0, M3S_GN_RAYS = 1, M3S_GN_CALIB = 2 };

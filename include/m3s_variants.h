@@ -34,6 +34,10 @@ int m3s_refine_variant_f16(int variant, const uint16_t* D11, const uint16_t* D21
  * the lattice kernel; enable != 0 turns counting on. */
 void m3s_refine_variant_stats(int enable, unsigned long long* out3);
 const char* m3s_variants_last_error(void);
+/* Test hook (not a refine variant): launch `nblocks` 64-thread workgroups on `stream`, each
+ * holding `lds_bytes` of LDS (256 .. 160 KiB) for `usec` microseconds (<= 2 s, bounded by the
+ * real-time counter), so that a test can take CUs away from a concurrent launch.  0 = launched. */
+int m3s_test_hold_cus(int nblocks, int lds_bytes, int usec, void* stream);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,7 @@
 // potrf ran the rank-8 trailing updates and the inverse on VALU from LDS (~30 us per tile).
 // Here every lower tile (i, j) of the (npad + 64) x npad bordered matrix (the border row tile
 // nt carries the RHS, so the forward substitution rides along) is owned by one workgroup of a
-// single co-resident (cooperative) launch, processed left-looking:
+// single launch (a plain launch of a grid the occupancy query keeps co-resident), processed left-looking:
 //   acc = A_ij;  for k < j: wait L_ik, L_jk final -> acc -= L_ik L_jk^T  (f64 MFMA)
 //   i == j: potrf of acc in LDS (8-column panels, per-lane 8x8 factor + row solve, MFMA rank-8
 //           trailing updates) and L_jj^-1 by doubling (8x8 blocks from the panel step, MFMA for
@@ -22,6 +22,7 @@
 // not a bit-exact path (parity through poses, tests/test_gpu_gn.py).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 
@@ -1268,15 +1269,23 @@ size_t chol_ready_bytes(int npad) {
 
 hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
                                 int epoch, int* flags, double* x, const DfScatter* g) {
-    static int maxg = 0;
+    // the grid cap that keeps every workgroup resident, per device: computed once per
+    // device id, published with an atomic store (concurrent first calls compute the same value)
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> maxg_dev[kMaxDev];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    int maxg = maxg_dev[dev].load(std::memory_order_acquire);
     if (maxg == 0) {
-        int dev = 0, ncu = 0, per = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        int ncu = 0, per = 0;
+        e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)chol_df_kernel, NT, 0);
         if (e != hipSuccess) return e;
         maxg = ncu * per;
         if (maxg <= 0) return hipErrorLaunchFailure;
+        maxg_dev[dev].store(maxg, std::memory_order_release);
     }
     DfArgs a{};
     a.Hd = Hd;

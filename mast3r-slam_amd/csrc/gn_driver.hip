@@ -228,7 +228,7 @@ int chunk_points(int64_t HW, int nchunks) {
 
 struct Layout {
     size_t partials, edgeblk, compact, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent, blk_ref, grad_ptr,
-        grad_ent, ecnt, cok, sched, pack, packx, pcnt, zs, total;
+        grad_ent, ecnt, cok, sched, pack, packx, pcnt, zs, twc_save, total;
     int nchunks, npad, nblk_max;
 };
 
@@ -261,6 +261,7 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     // allocations: see Ctx::alloc_dense and upload_sparse_plan)
     L.x = take(sizeof(double) * (size_t)L.npad);
     L.flags = take(sizeof(int) * kNumFlags);
+    L.twc_save = take(sizeof(float) * 8 * (size_t)std::max<int64_t>(N, 1));  // Twc at the call's start
     L.ii_loc = take(sizeof(int) * (size_t)E_local);
     L.jj_loc = take(sizeof(int) * (size_t)E_local);
     L.blk_ptr = take(sizeof(int) * ((size_t)L.nblk_max + 1));
@@ -1565,6 +1566,8 @@ int run(const m3s_gn_args& a) {
         rc = enqueue_system(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
+        // the poses the call started from, so that a timed-out call can restore them (below)
+        if (itr == 0) M3S_HIP_CHECK(launch_twc_save(c.st, a.Twc, c.at<float>(L.twc_save), (int)(8 * a.N)));
         rc = enqueue_solve(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
@@ -1577,29 +1580,36 @@ int run(const m3s_gn_args& a) {
     if (c.may_timeout && a.max_iter > 0) {
         // A bounded device-side wait that gave up discarded that iteration's solve (dx = 0): an
         // error, not a singular system (the reference's host Eigen solve cannot time out).  The
-        // flag leaves the device without a host wait (a kernel writes it to pinned memory): the
-        // error is reported by the next call on this thread or by m3s_gn_check, like an
-        // asynchronous kernel fault.  Waiting here instead left the GPU idle between calls for
-        // the host's per-call work (cfg3: 694 vs 318 us call-to-call gap, rocprofv3 trace).
-        // M3S_GN_TIMEOUT_SYNC=1: report it from this call (one stream synchronisation).
+        // call then restores the poses it started from, on the device (twc_guard_kernel), so a
+        // timed-out call never commits poses -- whatever its caller does next -- and
+        // every rank of a sharded call ends with the same Twc.  The flag leaves the device without
+        // a host wait (the same kernel writes it to pinned memory): the error is reported by the
+        // next GN call on this thread (once setup() has synchronised the stream) or by
+        // m3s_gn_check, like an asynchronous kernel fault.  Waiting here instead left the GPU idle
+        // between calls for the host's per-call work (cfg3: 694 vs 318 us call-to-call gap,
+        // rocprofv3 trace).  M3S_GN_TIMEOUT_SYNC=1: report it from this call (one stream
+        // synchronisation).
         Stagings& sg = stagings();
         char* h = sg.tmo.get(64);
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
+        float* save = c.at<float>(L.twc_save);
+        const int n8 = (int)(8 * a.N);
         if (a.comm) {
             // edge-sharded: every rank ran the same replicated solve, but the flag is rank-local --
             // OR it over the ranks (a sum of 0 / 1) so that all fail together instead of one rank
-            // returning the error while the others go on to their next collective
+            // returning the error while the others go on to their next collective,
+            // and all restore their poses
             double* dv = c.at<double>(L.x);  // the solution buffer is free once the call retracted
             M3S_HIP_CHECK(launch_flag_export(c.st, flags + kFlagTimeout, dv, 1));
             rc = comm_allreduce_sum_f64(a.comm, dv, 1, c.st);
             if (rc) return rc;
-            M3S_HIP_CHECK(sg.tmo.dev ? launch_stage_copy(c.st, sg.tmo.dev, dv, sizeof(double))
-                                     : hipMemcpyAsync(h, dv, sizeof(double), hipMemcpyDeviceToHost, c.st));
+            M3S_HIP_CHECK(launch_twc_restore_on_flag(c.st, a.Twc, save, n8, dv, 1, sg.tmo.dev));
+            if (!sg.tmo.dev) M3S_HIP_CHECK(hipMemcpyAsync(h, dv, sizeof(double), hipMemcpyDeviceToHost, c.st));
             sg.tmo_armed = 2;
         } else {
-            M3S_HIP_CHECK(sg.tmo.dev ? launch_flag_export(c.st, flags + kFlagTimeout, sg.tmo.dev, 0)
-                                     : hipMemcpyAsync(h, flags + kFlagTimeout, sizeof(int),
-                                                      hipMemcpyDeviceToHost, c.st));
+            M3S_HIP_CHECK(launch_twc_restore_on_flag(c.st, a.Twc, save, n8, flags + kFlagTimeout, 0, sg.tmo.dev));
+            if (!sg.tmo.dev)
+                M3S_HIP_CHECK(hipMemcpyAsync(h, flags + kFlagTimeout, sizeof(int), hipMemcpyDeviceToHost, c.st));
             sg.tmo_armed = 1;
         }
         M3S_HIP_CHECK(sg.tmo.mark(c.st));

@@ -227,6 +227,12 @@ hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
 hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes);
 // flag[0] != 0 as an int (as_f64 = 0) or a double (as_f64 = 1) at dst (device-accessible)
 hipError_t launch_flag_export(hipStream_t st, const int* flag, void* dst, int as_f64);
+// save[0..n) = Twc[0..n) (before a call's first retraction)
+hipError_t launch_twc_save(hipStream_t st, const float* Twc, float* save, int n);
+// if the timeout flag (an int, or a double > 0 when flag_f64) is set: Twc[0..n) = save; the flag
+// goes to dst (int 0/1, or the double) when dst != null
+hipError_t launch_twc_restore_on_flag(hipStream_t st, float* Twc, const float* save, int n, const void* flag,
+                                      int flag_f64, void* dst);
 hipError_t launch_retract(hipStream_t st, float* Twc, const double* x, float* dx, int N,
                           float delta_thresh, int* flags, int contract);
 

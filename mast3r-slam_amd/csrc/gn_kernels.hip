@@ -570,12 +570,45 @@ __global__ void flag_export_kernel(const int* __restrict__ flag, void* dst, int 
     }
 }
 
+// A timed-out call never commits its poses: Twc is saved before the call's first
+// retraction (mode 0) and restored at its end when the call's timeout flag -- the rank-local int,
+// or the ranks' sum as a double -- is set (mode 1), which then also exports the flag to dst (an
+// int, or the double as is) when dst is not null.  All on the device: no host wait.
+__global__ __launch_bounds__(256) void twc_guard_kernel(float* __restrict__ Twc, float* __restrict__ save, int n,
+                                                        int mode, const void* flag, int flag_f64, void* dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (mode == 0) {
+        if (i < n) save[i] = Twc[i];
+        return;
+    }
+    const double f = flag_f64 ? *static_cast<const double*>(flag) : (double)*static_cast<const int*>(flag);
+    if (f > 0.0 && i < n) Twc[i] = save[i];
+    if (dst && i == 0) {
+        if (flag_f64) *static_cast<double*>(dst) = f;
+        else *static_cast<int*>(dst) = f > 0.0 ? 1 : 0;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // launchers (host)
 // ---------------------------------------------------------------------------
 
 hipError_t launch_flag_export(hipStream_t st, const int* flag, void* dst, int as_f64) {
     hipLaunchKernelGGL(flag_export_kernel, dim3(1), dim3(64), 0, st, flag, dst, as_f64);
+    return hipGetLastError();
+}
+
+hipError_t launch_twc_save(hipStream_t st, const float* Twc, float* save, int n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(twc_guard_kernel, dim3((n + 255) / 256), dim3(256), 0, st, const_cast<float*>(Twc), save,
+                       n, 0, nullptr, 0, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_twc_restore_on_flag(hipStream_t st, float* Twc, const float* save, int n, const void* flag,
+                                      int flag_f64, void* dst) {
+    hipLaunchKernelGGL(twc_guard_kernel, dim3(n > 0 ? (n + 255) / 256 : 1), dim3(256), 0, st, Twc,
+                       const_cast<float*>(save), n, 1, flag, flag_f64, dst);
     return hipGetLastError();
 }
 

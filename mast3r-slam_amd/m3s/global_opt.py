@@ -196,6 +196,16 @@ class FactorGraph:
         Xs, T_WCs, Cs = self.get_poses_points(unique_kf_idx)
         return pin, unique_kf_idx, Xs, T_WCs, Cs
 
+    @staticmethod
+    def _check_solved(be, pose_data):
+        """Raise a deferred solver error of the call just made before its poses are written back
+        (ADVICE r04): a timed-out factorisation restores Twc on the device, and this makes the
+        caller see the error in the same solve_GN_* call, as the reference's synchronous op would
+        (its driver synchronises the host every iteration, gn_kernels.cu:1199-1222)."""
+        check = getattr(be, "gn_check", None)
+        if check is not None and pose_data.is_cuda:
+            check(pose_data.device)
+
     def solve_GN_rays(self, backend=None):
         be = backend or mast3r_slam_backends
         prep = self._prepare()
@@ -210,6 +220,7 @@ class FactorGraph:
             c["sigma_ray"], c["sigma_dist"], c["C_conf"], c["Q_conf"], c["max_iters"],
             c["delta_norm"],
         )
+        self._check_solved(be, pose_data)
         self.frames.update_T_WCs(T_WCs[pin:], unique_kf_idx[pin:])
 
     def solve_GN_calib(self, backend=None):
@@ -228,6 +239,7 @@ class FactorGraph:
             c["pixel_border"], c["depth_eps"], c["sigma_pixel"], c["sigma_depth"], c["C_conf"],
             c["Q_conf"], c["max_iters"], c["delta_norm"],
         )
+        self._check_solved(be, pose_data)
         self.frames.update_T_WCs(T_WCs[pin:], unique_kf_idx[pin:])
 
 
@@ -380,6 +392,7 @@ class DeviceFactorGraph(FactorGraph):
         mast3r_slam_backends._run_gn(
             mode, pose_data, Xs, Cs, ii, jj, idx_f, valid_f, Q_f, c["max_iters"], c["delta_norm"],
             s0, s1, c["C_conf"], c["Q_conf"], second_half=self.edges.backward(), **kw)
+        self._check_solved(mast3r_slam_backends, pose_data)
         if keep is not None:
             pose_data[1:pin] = keep
         if not in_place:

@@ -22,6 +22,7 @@ lib.m3s_refine_variant_f16.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [
 lib.m3s_refine_variant_stats.argtypes = [ctypes.c_int, ctypes.c_void_p]
 lib.m3s_refine_variant_stats.restype = None
 lib.m3s_variants_last_error.restype = ctypes.c_char_p
+lib.m3s_test_hold_cus.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 
 
 def refine_matches_variant(kind, D11, D21, p1, window_size, dilation_max):
@@ -53,3 +54,11 @@ def variant_stats(enable=True):
 
 def mfma_issued():
     return getattr(variant_stats, "mfma", 0)
+
+
+def hold_cus(nblocks, lds_bytes, usec, stream):
+    """Test hook: ``nblocks`` workgroups on ``stream`` (a torch.cuda.Stream) that each hold
+    ``lds_bytes`` of LDS for ``usec`` microseconds -- CUs taken away from a concurrent launch."""
+    rc = lib.m3s_test_hold_cus(int(nblocks), int(lds_bytes), int(usec), ctypes.c_void_p(stream.cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"hold_cus: rc {rc}")

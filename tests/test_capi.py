@@ -25,11 +25,12 @@ def test_library_exports_every_declared_symbol(backend):
 
 
 def test_variants_library_exports_its_header():
-    """The measurement-only refine variants live in their own library (not the drop-in one)."""
+    """The measurement-only refine variants (and the test hook) live in their own library (not the
+    drop-in one)."""
     src = open(os.path.join(ROOT, "include", "m3s_variants.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     syms = sorted(set(re.findall(r"\b(m3s_[a-z0-9_]+)\s*\(", src)))
-    assert len(syms) == 3, syms
+    assert len(syms) == 4, syms
     path = os.path.join(ROOT, "mast3r-slam_amd", "lib", "libm3s_variants.so")
     lib = ctypes.CDLL(path)
     assert all(hasattr(lib, s) for s in syms)

@@ -202,13 +202,18 @@ def _timeout_worker(rank, world, port, out_q):
         c = lambda t: t.cuda().contiguous()
         comm = HostComm()
         err = None
+        Twc = c(g.Twc)
         try:
-            gauss_newton_sharded("rays", c(g.Twc), c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx[lo:hi]),
+            gauss_newton_sharded("rays", Twc, c(g.Xs), c(g.Cs), c(g.ii), c(g.jj), c(g.idx[lo:hi]),
                                  c(g.valid[lo:hi]), c(g.Q[lo:hi]), lo, comm, 2, 0.0, **_params(g, "rays"))
             mb.gn_check()  # the deferred report (include/m3s_backend.h m3s_gn_check)
         except RuntimeError as e:
             err = str(e)
-        out_q.put((rank, err, comm.calls, None))
+        torch.cuda.synchronize()
+        # every rank restored the poses the call started from (no rank keeps a pose
+        # set the others do not have)
+        restored = bool(torch.equal(Twc.cpu(), g.Twc))
+        out_q.put((rank, err, comm.calls, None if restored else "Twc not restored"))
         comm.close()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001 -- reported to the parent

@@ -179,3 +179,26 @@ def test_device_factor_graph_pin_2_keeps_pinned_rows(mode):
     assert torch.equal(s_dev.T_WC[ids[:2]], before[ids[:2]])
     assert torch.equal(s_ref.T_WC, s_dev.T_WC)
     assert not torch.equal(s_dev.T_WC[ids[2:]], before[ids[2:]])
+
+
+@pytest.mark.parametrize("device_graph", [False, True], ids=["FactorGraph", "DeviceFactorGraph"])
+def test_timed_out_solve_is_not_committed(monkeypatch, device_graph):
+    """A solve whose factorisation times out (forced with the test hook on the dataflow dense
+    solver) raises from solve_GN_* itself and leaves the keyframe store's poses untouched: the op
+    restores Twc on the device and the caller checks the deferred error before writing back
+    (ADVICE r04); the next solve without the hook works again."""
+    ids = [3, 4, 5, 6, 7, 8]
+    fg, dg, (s_ref, s_dev) = _device_setup("rays", ids)
+    graph, store = (dg, s_dev) if device_graph else (fg, s_ref)
+    before = store.T_WC.clone()
+    monkeypatch.setenv("M3S_SOLVER_DENSE", "1")
+    monkeypatch.setenv("M3S_CHOL_DF", "1")
+    monkeypatch.setenv("M3S_TEST_FORCE_TIMEOUT", "1")
+    with pytest.raises(RuntimeError, match="timed out"):
+        graph.solve_GN_rays()
+    torch.cuda.synchronize()
+    assert torch.equal(store.T_WC, before)
+    monkeypatch.delenv("M3S_TEST_FORCE_TIMEOUT")
+    graph.solve_GN_rays()
+    torch.cuda.synchronize()
+    assert not torch.equal(store.T_WC[ids[1:]], before[ids[1:]])

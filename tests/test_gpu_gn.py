@@ -601,7 +601,10 @@ def test_factorisation_timeout_is_an_error_not_a_singular_system(backend, monkey
     backend.gn_check()  # nothing pending
     monkeypatch.setenv("M3S_TEST_FORCE_TIMEOUT", "1")
     # the report is deferred (no host wait at the end of the call): gn_check raises it ...
-    _run_gpu(backend, g, "rays", 2)
+    T_to, _ = _run_gpu(backend, g, "rays", 2)
+    # ... and the timed-out call committed nothing: the device restored the poses it started from
+    # (ADVICE r04), so a caller that writes Twc back before checking never stores a failed solve
+    assert np.array_equal(T_to, g.Twc.numpy())
     with pytest.raises(RuntimeError, match="timed out"):
         backend.gn_check()
     backend.gn_check()  # ... once
@@ -639,3 +642,33 @@ def test_factorisation_timeout_sync_report(backend, monkeypatch):
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True,
                        timeout=240)
     assert "RAISED" in r.stdout and "timed out" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+@pytest.mark.parametrize("nblocks", [128, 256])
+def test_dataflow_factor_with_cus_held_by_another_stream(backend, monkeypatch, nblocks):
+    """chol_df is a plain launch whose spin waits assume its whole grid is resident (the
+    occupancy query sizes it for an idle GPU).  SURVEY.md §8(b): the tracker and the backend
+    launch on the same GPU concurrently.  Here workgroups on a second stream hold 64 KiB of LDS on
+    about half / all of the CUs for 30 ms -- chol_df's 131-KiB workgroups do not fit beside them,
+    so part (or all) of its grid starts late while the resident part waits.  The op must either
+    finish with bitwise the poses of an unhindered run or raise M3S_ERR_TIMEOUT with the poses
+    restored -- never return other poses."""
+    from mast3r_slam_backends import variants
+
+    g = synth.make_graph("cfg4", H=24, W=32, seed=6)
+    monkeypatch.setenv("M3S_SOLVER", "2")
+    monkeypatch.setenv("M3S_CHOL_DF", "1")
+    T_ref, dx_ref = _run_gpu(backend, g, "rays", 3)
+    backend.gn_check()
+    side = torch.cuda.Stream()
+    variants.hold_cus(nblocks, 64 * 1024, 30000, side)
+    T_h, dx_h = _run_gpu(backend, g, "rays", 3)  # (the error, if any, is deferred)
+    try:
+        backend.gn_check()
+    except RuntimeError as e:
+        assert "timed out" in str(e), e
+        assert np.array_equal(T_h, g.Twc.numpy())
+        print("timed out (poses restored)")
+    else:
+        assert np.array_equal(T_h, T_ref) and np.array_equal(dx_h, dx_ref)
+    torch.cuda.synchronize()
