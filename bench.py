@@ -220,6 +220,8 @@ def main():
                                    cpu_baseline.last_step, cpu_baseline.exact_step)
         if os.environ.get("M3S_BENCH_REF_ORDER", "1") != "0":
             out["accuracy"]["reference_order_mode"] = reference_order_block(g, mode, Twc0, args, iters)
+        if mode == "calib" and os.environ.get("M3S_BENCH_STRESS", "1") != "0":
+            out["accuracy"]["stress_1iter"] = stress_block(dev)
     # BASELINE.json configs[3] (1024 edges, the config SURVEY §8(e) sets the scaling target on):
     # with --gpus N it is edge-sharded like the headline config, so the driver's SCALE run
     # measures it at every N.  Its own block; ``value`` stays the headline config's.
@@ -401,6 +403,55 @@ def reference_order_block(g, mode, Twc0, args, iters, reps=3):
         "ms_per_call": dt * 1e3,
         "calls_timed": reps,
         "pose_max_rel_err_vs_oracle_1iter": float(np.abs(T1 - To).max() / np.abs(To).max()),
+    }
+
+
+def stress_block(dev):
+    """Mid-convergence parity, restated by every bench run: the headline
+    topology started 10 deg / 25 cm / 0.1 log-scale from the truth with 10 % gross outlier matches
+    (tests/test_gpu_gn_stress.py), ONE iteration.  The timed (fast) path's and the reference-order
+    mode's poses against the CPU oracle (the reference's float order) and against the exactly summed
+    system (the same float terms summed in double); sigma = the oracle's own distance from the
+    exact sums, i.e. the reference order's rounding noise, below which no other order can land."""
+    import numpy as np
+
+    import mast3r_slam_backends as mb
+    from m3s import synth
+    from m3s.geometry import constrain_points_to_ray
+    from oracle import oracle as O
+
+    g = synth.make_graph("cfg3", device=dev, init_perturb=(10.0, 0.25, 0.1), outlier_frac=0.10)
+    g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    L = LOCAL
+
+    def gpu():
+        Twc = g.Twc.clone()
+        mb.gauss_newton_calib(Twc, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
+                              L["pixel_border"], L["depth_eps"], L["sigma_pixel"], L["sigma_depth"],
+                              L["C_conf"], L["Q_conf"], 1, 0.0)
+        torch.cuda.synchronize()
+        return Twc.cpu().numpy().astype(np.float64)
+
+    T_fast = gpu()
+    prev = mb.set_gn_order("reference")
+    try:
+        T_ref = gpu()
+    finally:
+        mb.set_gn_order(prev)
+    c = lambda t: t.cpu().numpy()
+    P = O.make_params("calib", L["sigma_pixel"], L["sigma_depth"], L["C_conf"], L["Q_conf"], K=c(g.K), height=g.H,
+                      width=g.W, pixel_border=L["pixel_border"], z_eps=L["depth_eps"], max_iter=1, delta_thresh=0.0)
+    arrs = [c(t) for t in (g.Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q)]
+    T_o = O.gauss_newton(P, *arrs)[0].astype(np.float64)
+    with O.exact_sums():
+        T_x = O.gauss_newton(P, *arrs)[0].astype(np.float64)
+    rel = lambda a, b: float(np.abs(a - b).max() / np.abs(b).max())
+    return {
+        "graph": "cfg3 topology, 512x384, start 10 deg / 25 cm / 0.1 log-scale, 10 % outlier matches, 1 iteration",
+        "fast_vs_oracle": rel(T_fast, T_o),
+        "fast_vs_exact": rel(T_fast, T_x),
+        "reference_order_vs_oracle": rel(T_ref, T_o),
+        "sigma_oracle_vs_exact": rel(T_o, T_x),
     }
 
 

@@ -67,6 +67,11 @@ struct DfArgs {
     long long* trace;  // diagnostics (tools/ubench_chol_df.hip): 4 timestamps per tile, else null
     double* x;         // != null: the back-substitution L^T x = y runs in this launch too (x: npad)
     DfScatter g;       // g.xpose != null: the back-substitution also writes x pose-indexed
+    // the back-substitution's in-launch hand-off of x: per entry two 8-B granules {epoch, 32 bits of
+    // the double} (lo, hi), stored and polled as 64-bit agent-scope atomics -- the data is the flag
+    // (cdna_hip_programming.md Guideline 16, R2): no store drain, barrier and flag before the
+    // consumer sees x, and no flag poll + second load after it
+    unsigned long long* xg;
 };
 
 // workgroup barrier ordering LDS only (__syncthreads also waits for every outstanding global
@@ -955,9 +960,41 @@ __device__ __forceinline__ void publish(const DfArgs& a, int idx) {
     if (threadIdx.x == 0) __hip_atomic_store(a.ready + idx, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// x_j[c] -> its two granules (one lane each call)
+__device__ __forceinline__ void publish_x(const DfArgs& a, int j, int c, double xv) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(xv);
+    const unsigned long long tag = (unsigned long long)(unsigned)a.epoch << 32;
+    unsigned long long* g = a.xg + 2 * ((int64_t)j * T + c);
+    __hip_atomic_store(g, tag | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, tag | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one wave: x_k, lane c = entry c, once every lane's two granules carry this factorisation's epoch
+// (bounded like wait_ready: a timeout fails the solve and raises the sticky timeout flag)
+__device__ __forceinline__ double wait_x(const DfArgs& a, int k) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long* g = a.xg + 2 * ((int64_t)k * T + lane);
+    const unsigned ep = (unsigned)a.epoch;
+    unsigned long long lo = 0, hi = 0;
+    for (int spins = 0;;) {
+        lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((unsigned)(lo >> 32) == ep && (unsigned)(hi >> 32) == ep)) break;
+        if (a.spin_limit < 0 || ++spins > a.spin_limit) {
+            if (lane == 0) {
+                __hip_atomic_store(a.flags + kFlagTimeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.flags + kFlagFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+        }
+        if ((spins & 1023) == 0 && __hip_atomic_load(a.flags + kFlagFail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return __hiloint2double((int)(unsigned)hi, (int)(unsigned)lo);
+}
 // Back-substitution task of the tile columns jh and jl = jh - 1 (jl < 0: jh alone), after the
 // factor tasks in the helpers' lists, in descending order: z_j = y_j - sum_{k>j} L_kj^T x_k,
-// x_j = Linv_j^T z_j, published with ready words (xflag).  Each x_k is applied as soon as it is
+// x_j = Linv_j^T z_j, published as data-tagged granules (publish_x / wait_x).  Each x_k is applied as soon as it is
 // published, so when the previous pair's x arrive only their terms, the sums and the Linv
 // products are left -- and x_jh feeds x_jl inside the workgroup (L_{jh,jl}^T x_jh): one hand-off
 // per two tile columns on the back-substitution chain (a hand-off -- write-through store, flag,
@@ -965,7 +1002,6 @@ __device__ __forceinline__ void publish(const DfArgs& a, int idx) {
 // Thread (c, g): column c, rows 16g .. 16g+15 of each tile; the 4 row-group partials are summed
 // in fixed order (deterministic).  Every wait targets a task earlier in some co-resident
 // workgroup's list: no deadlock.
-__host__ __device__ inline int xflag(int nt, int j) { return (nt + 1) * nt + nt + j; }
 __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
     const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
     const int nt = a.nt;
@@ -1024,15 +1060,12 @@ __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
     const double yl = (two && tid < 64) ? ld_coh(a.Hd + (int64_t)ld * ld + (int64_t)jl * T + c) : 0.0;
     bstamp(0);
     for (int k = nt - 1; k > jh; k--) {
-        if (tid == 0) {
-            wait_ready(a.ready + xflag(nt, k), a.epoch, a.flags, a.spin_limit);
-            if (k - 1 > jh) {
-                wait_ready(a.ready + (k - 1) * nt + jh, a.epoch, a.flags, a.spin_limit);
-                if (two) wait_ready(a.ready + (k - 1) * nt + jl, a.epoch, a.flags, a.spin_limit);
-            }
+        if (tid == 0 && k - 1 > jh) {  // the next tiles' words (final long ago: no wait in practice)
+            wait_ready(a.ready + (k - 1) * nt + jh, a.epoch, a.flags, a.spin_limit);
+            if (two) wait_ready(a.ready + (k - 1) * nt + jl, a.epoch, a.flags, a.spin_limit);
         }
+        if (tid < 64) sx[tid] = wait_x(a, k);  // wave 0 polls x_k's granules until all are this epoch's
         __syncthreads();
-        if (tid < 64) sx[tid] = ld_coh(a.x + (int64_t)k * T + tid);
         double ch[16], cl[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) {
@@ -1071,7 +1104,8 @@ __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
         if (tid < 64) {
             const double xv = ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c];
             xs[c] = xv;
-            st_coh(a.x + (int64_t)j * T + c, xv);
+            publish_x(a, j, c, xv);  // the granules: the next pair task polls them
+            a.x[(int64_t)j * T + c] = xv;  // the copy later launches read
             const int q = j * T + c;  // the pose-indexed copy the back rounds read (no scatter launch)
             if (a.g.xpose && q < 7 * a.g.ntail) a.g.xpose[(int64_t)a.g.tail[q / 7] * 7 + q % 7] = xv;
         }
@@ -1084,12 +1118,6 @@ __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
 #pragma unroll
         for (int q = 0; q < 16; q++) acc_l = fma(lhl[q], sxh[16 * g + q], acc_l);
         finish(jl, yl, acc_l, lil, sx);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __hip_atomic_store(a.ready + xflag(nt, jh), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (two) __hip_atomic_store(a.ready + xflag(nt, jl), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     bstamp(3);
 }
@@ -1262,10 +1290,12 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
 
 }  // namespace
 
-size_t chol_ready_bytes(int npad) {
+// ready words (tiles, H_j), then the x granules (16 B per entry, 16-B aligned)
+static size_t chol_words_bytes(int npad) {
     const int nt = npad / T;
-    return sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + 2 * (size_t)nt);  // tiles, H_j, x_j
+    return ((sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + (size_t)nt)) + 15) / 16 * 16;
 }
+size_t chol_ready_bytes(int npad) { return chol_words_bytes(npad) + 16 * (size_t)npad; }
 
 hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
                                 int epoch, int* flags, double* x, const DfScatter* g) {
@@ -1297,6 +1327,7 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
     a.ntiles = num_tasks(a.nt);
     a.epoch = epoch;
     a.x = x;
+    a.xg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ready) + chol_words_bytes(npad));
     if (g) a.g = *g;
     // M3S_TEST_FORCE_TIMEOUT=1 (tests only): every ready wait gives up at once, to exercise the
     // timeout -> M3S_ERR_TIMEOUT path without a real hang

@@ -591,8 +591,11 @@ RoundPolicy fused_policy() {
             std::min(kTailPoseMax, env_int("M3S_SPARSE_TAILCAP", kTailPoseMax)),
             env_int("M3S_SPARSE_KMIN", 4), env_int("M3S_SPARSE_MMD", 1) != 0};
 }
+// multi: dcap 32 (round 5: cfg4 -- 255 free poses, 1007 pose pairs -- 4 rounds and a 125-pose
+// core instead of 3 rounds and 141 poses; solve 0.307 -> 0.288 ms per iteration on one box, dcap
+// 24 0.292, 64 0.301: profiles/r05_b_dcap*.json)
 RoundPolicy multi_policy() {
-    return {false, env_int("M3S_MULTI_DCAP", 16), env_int("M3S_MULTI_RMIN", 2),
+    return {false, env_int("M3S_MULTI_DCAP", 32), env_int("M3S_MULTI_RMIN", 2),
             env_int("M3S_MULTI_RMAX", 64), 0, 0, env_int("M3S_MULTI_MMD", 0) != 0};
 }
 // hybrid: multi-launch rounds in minimum-degree order down to a core that fits the in-register
