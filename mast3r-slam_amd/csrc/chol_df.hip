@@ -73,6 +73,7 @@ struct DfArgs {
     // consumer sees x, and no flag poll + second load after it
     unsigned long long* xg;
     int prefetch;  // the chain loads its next column's P tiles during potrf (M3S_DF_PREFETCH)
+    int xgran;     // x hand-off by granules (M3S_DF_XGRAN, default 1) or by ready words (0)
 };
 
 // workgroup barrier ordering LDS only (__syncthreads also waits for every outstanding global
@@ -970,6 +971,7 @@ __device__ __forceinline__ void publish(const DfArgs& a, int idx) {
     if (threadIdx.x == 0) __hip_atomic_store(a.ready + idx, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__host__ __device__ inline int xflag(int nt, int j) { return (nt + 1) * nt + nt + j; }  // (M3S_DF_XGRAN=0)
 // x_j[c] -> its two granules (one lane each call)
 __device__ __forceinline__ void publish_x(const DfArgs& a, int j, int c, double xv) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(xv);
@@ -1074,8 +1076,14 @@ __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
             wait_ready(a.ready + (k - 1) * nt + jh, a.epoch, a.flags, a.spin_limit);
             if (two) wait_ready(a.ready + (k - 1) * nt + jl, a.epoch, a.flags, a.spin_limit);
         }
-        if (tid < 64) sx[tid] = wait_x(a, k);  // wave 0 polls x_k's granules until all are this epoch's
-        __syncthreads();
+        if (a.xgran) {
+            if (tid < 64) sx[tid] = wait_x(a, k);  // wave 0 polls x_k's granules until all are this epoch's
+            __syncthreads();
+        } else {
+            if (tid == 0) wait_ready(a.ready + xflag(nt, k), a.epoch, a.flags, a.spin_limit);
+            __syncthreads();
+            if (tid < 64) sx[tid] = ld_coh(a.x + (int64_t)k * T + tid);
+        }
         double ch[16], cl[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) {
@@ -1114,8 +1122,12 @@ __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
         if (tid < 64) {
             const double xv = ((sp[c] + sp[64 + c]) + sp[128 + c]) + sp[192 + c];
             xs[c] = xv;
-            publish_x(a, j, c, xv);  // the granules: the next pair task polls them
-            a.x[(int64_t)j * T + c] = xv;  // the copy later launches read
+            if (a.xgran) {
+                publish_x(a, j, c, xv);  // the granules: the next pair task polls them
+                a.x[(int64_t)j * T + c] = xv;  // the copy later launches read
+            } else {
+                st_coh(a.x + (int64_t)j * T + c, xv);
+            }
             const int q = j * T + c;  // the pose-indexed copy the back rounds read (no scatter launch)
             if (a.g.xpose && q < 7 * a.g.ntail) a.g.xpose[(int64_t)a.g.tail[q / 7] * 7 + q % 7] = xv;
         }
@@ -1128,6 +1140,14 @@ __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
 #pragma unroll
         for (int q = 0; q < 16; q++) acc_l = fma(lhl[q], sxh[16 * g + q], acc_l);
         finish(jl, yl, acc_l, lil, sx);
+    }
+    if (!a.xgran) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_store(a.ready + xflag(nt, jh), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (two) __hip_atomic_store(a.ready + xflag(nt, jl), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     bstamp(3);
 }
@@ -1332,10 +1352,10 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
 
 }  // namespace
 
-// ready words (tiles, H_j), then the x granules (16 B per entry, 16-B aligned)
+// ready words (tiles, H_j, x_j), then the x granules (16 B per entry, 16-B aligned)
 static size_t chol_words_bytes(int npad) {
     const int nt = npad / T;
-    return ((sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + (size_t)nt)) + 15) / 16 * 16;
+    return ((sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + 2 * (size_t)nt)) + 15) / 16 * 16;
 }
 size_t chol_ready_bytes(int npad) { return chol_words_bytes(npad) + 16 * (size_t)npad; }
 
@@ -1380,6 +1400,11 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
         return e ? atoi(e) : 1;
     }();
     a.prefetch = prefetch;
+    static const int xgran = [] {
+        const char* e = getenv("M3S_DF_XGRAN");
+        return e ? atoi(e) : 1;
+    }();
+    a.xgran = xgran;
     const int grid = 1 + a.ntiles < maxg ? 1 + a.ntiles : maxg;  // workgroup 0 = the diagonal chain
     // A plain launch of a grid the occupancy query admits (one workgroup per CU here: 131 KB of
     // LDS) gives the same residency as a cooperative one (MI355X_MICROARCH.md, "Residency and
