@@ -72,8 +72,7 @@ struct DfArgs {
     // (cdna_hip_programming.md Guideline 16, R2): no store drain, barrier and flag before the
     // consumer sees x, and no flag poll + second load after it
     unsigned long long* xg;
-    int prefetch;  // the chain loads its next column's P tiles during potrf (M3S_DF_PREFETCH)
-    int xgran;     // x hand-off by granules (M3S_DF_XGRAN, default 1) or by ready words (0)
+    int xgran;  // x hand-off by granules (M3S_DF_XGRAN, default 1) or by ready words (0)
 };
 
 // workgroup barrier ordering LDS only (__syncthreads also waits for every outstanding global
@@ -588,15 +587,9 @@ __device__ __forceinline__ void potrf_cc_w(double* A, double* Li, double* Lc, do
 // announces on its own counter (sync[8 + w]: batches written).  Measured (ubench_potrf64 /
 // ubench_chol_df, profiles/r04_ak_*): ~940 cycles per batch hand-off + factor, tile factor +
 // inverse 8.0 us vs potrf_cc's 10.2 us in the chain; 8-column batches (M3S_DF_BC_W=8) 9.6 us.
-struct NoHook {
-    __device__ void operator()() const {}
-};
-// hook: called by every wave before the factor of its local batches NL / 2 and NL / 2 + 1 (about
-// halfway through the tile factor): the chain issues its next column's tile loads there once their
-// ready word is set
-template <int W, int BW, class Hook = NoHook>
+template <int W, int BW>
 __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, double* scratch, int* sync, double* Dinv,
-                                           int* flags, long long* pt, const Hook& hook = Hook()) {
+                                           int* flags, long long* pt) {
     constexpr int NL = 16 / BW;  // local batches per wave
     const int lane = threadIdx.x & 63;
     auto wstamp = [&](int k) {
@@ -685,7 +678,6 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
 #pragma unroll
     for (int lb = 0; lb < NL; lb++) {
         const int nb = 4 * lb + W;
-        if (lb == NL / 2 || lb == NL / 2 + 1) hook();  // (the hook loads once: a second call checks again)
         // the other waves' earlier batches, to all my remaining columns (off the critical path)
 #pragma unroll 1
         for (; next < nb - 1; next++) {
@@ -848,18 +840,16 @@ __device__ __forceinline__ void potrf_bc_w(double* A, double* Li, double* Lb, do
 
 // the register factor + inverse of the tile: batch-cyclic (potrf_bc_w, M3S_DF_BC=1, default) or
 // column-cyclic (potrf_cc_w); sync[0 .. kDfSync) zeroed and visible
-template <class Hook = NoHook>
 __device__ __forceinline__ void potrf_cc(double* A, double* Li, double* Lc, double* scratch, int* sync, double* Dinv,
-                                         int* flags, long long* pt = nullptr, const Hook& hook = Hook()) {
+                                         int* flags, long long* pt = nullptr) {
 #if M3S_DF_BC
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-        case 0: potrf_bc_w<0, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt, hook); break;
-        case 1: potrf_bc_w<1, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt, hook); break;
-        case 2: potrf_bc_w<2, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt, hook); break;
-        default: potrf_bc_w<3, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt, hook); break;
+        case 0: potrf_bc_w<0, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        case 1: potrf_bc_w<1, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        case 2: potrf_bc_w<2, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
+        default: potrf_bc_w<3, M3S_DF_BC_W>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
     }
 #else
-    (void)hook;
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
         case 0: potrf_cc_w<0>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
         case 1: potrf_cc_w<1>(A, Li, Lc, scratch, sync, Dinv, flags, pt); break;
@@ -1176,19 +1166,11 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
     };
     if (blockIdx.x == 0) {
         // ---- the diagonal chain
-        // a.prefetch (env M3S_DF_PREFETCH, default 1): column j+1's P_s / P_d tiles (written by helper task H_{j+1},
-        // ready a few us into potrf(j)) are loaded into registers by each wave halfway through
-        // potrf(j) when their ready word is already set -- off the chain -- instead of after it.
-        // Each wave loads (and, without a prefetch, waits for) its own 16-row block rows: no
-        // workgroup barrier between the ready word and the loads.
-        d4 pfs[4], pfd[4];
-        bool pf = false;  // wave-uniform: this wave holds column j's P tiles in pfs / pfd
         for (int j = 0; j < nt; j++) {
             d4 accd[4];
-            if (j >= 2 && !pf) {
-                if ((tid & 63) == 0) wait_ready(a.ready + hflag(nt, j), a.epoch, a.flags, a.spin_limit);
-                // (the wave reconverges after lane 0's wait; no barrier: Linv_{j-1}'s stores stay in
-                // flight until the publish)
+            if (j >= 2) {
+                if (tid == 0) wait_ready(a.ready + hflag(nt, j), a.epoch, a.flags, a.spin_limit);
+                lds_barrier();  // (not __syncthreads: Linv_{j-1}'s stores stay in flight until the publish)
             }
             cstamp(j, 0);
             if (j == 0) {
@@ -1202,17 +1184,12 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 if (j == 1) {
                     load_src(accs, a, 1, 0);
                     load_src(accd, a, 1, 1);
-                } else if (pf) {
-#pragma unroll
-                    for (int J = 0; J < 4; J++) {
-                        accs[J] = pfs[J];
-                        accd[J] = pfd[J];
-                    }
                 } else {
                     load_acc<true>(accs, tile(j, j - 1), ld);
                     load_acc<true>(accd, tile(j, j), ld);
                 }
-                pf = false;
+                // the loads drained the queue: Linv_{j-1}'s stores have landed
+                publish(a, (j - 1) * nt + (j - 1));
                 acc_to_lds(X, accs);
                 acc_to_lds(Z, accd);
                 lds_barrier();
@@ -1221,10 +1198,6 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
                 for (int J = 0; J < 4; J++) accs[J] = d4{0.0, 0.0, 0.0, 0.0};
                 gemm_nt<true>(X, Y, accs, 1.0);  // L_{j,j-1}
                 fstamp(j, 1);
-                // Linv_{j-1}: its write-through stores drained during the GEMM (with the P tiles
-                // prefetched, no load waits for them any more: published before the GEMM, their
-                // ~1 us drain sat on the chain)
-                publish(a, (j - 1) * nt + (j - 1));
                 store_acc_coh(tile(j, j - 1), ld, accs);
                 lds_barrier();  // the GEMM's reads of X and Y are done (the stores stay in flight)
                 acc_to_lds(X, accs);
@@ -1245,22 +1218,7 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
 #if M3S_DF_CC
             if (j >= 1 && tid == 0)  // L_{j,j-1}: every wave waited for its stores before the barrier
                 __hip_atomic_store(a.ready + j * nt + (j - 1), a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (a.prefetch && j + 1 >= 2 && j + 1 < nt) {
-                const int jn = j + 1;
-                auto hook = [&]() {
-                    if (pf) return;
-                    int f = __hip_atomic_load(a.ready + hflag(nt, jn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    f = __builtin_amdgcn_readfirstlane(f);
-                    if (f >= a.epoch) {
-                        load_acc<true>(pfs, tile(jn, jn - 1), ld);
-                        load_acc<true>(pfd, tile(jn, jn), ld);
-                        pf = true;
-                    }
-                };
-                potrf_cc(Z, Y, X, Scr, Sync, Dinv, a.flags, nullptr, hook);  // X (L_{j,j-1}) is free: the column buffer
-            } else {
-                potrf_cc(Z, Y, X, Scr, Sync, Dinv, a.flags);
-            }
+            potrf_cc(Z, Y, X, Scr, Sync, Dinv, a.flags);  // X (L_{j,j-1}) is free: the column buffer
 #else
             potrf_inverse(Z, Y, X, Dinv, a.flags, a.trace && j == 0 ? a.trace + 4 * a.ntiles : nullptr,
                           j >= 1 ? a.ready + j * nt + (j - 1) : nullptr, a.epoch);
@@ -1395,11 +1353,8 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
     // timeout -> M3S_ERR_TIMEOUT path without a real hang
     const char* ft = getenv("M3S_TEST_FORCE_TIMEOUT");
     a.spin_limit = (ft && atoi(ft) != 0) ? -1 : (1 << 22);
-    static const int prefetch = [] {
-        const char* e = getenv("M3S_DF_PREFETCH");
-        return e ? atoi(e) : 1;
-    }();
-    a.prefetch = prefetch;
+    // M3S_DF_XGRAN (default 1): the back-substitution's x hand-off by granules; 0: ready words
+    // (round-5 A/B on cfg4, one box: solve 0.293 vs 0.296 ms per iteration, profiles/r05_d_*)
     static const int xgran = [] {
         const char* e = getenv("M3S_DF_XGRAN");
         return e ? atoi(e) : 1;
