@@ -84,8 +84,18 @@ template <int CM>
 __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
     const float* __restrict__ rays, const float* __restrict__ pts, const float* __restrict__ p_init,
     float* __restrict__ p_new, uint8_t* __restrict__ converged, int H, int W, int64_t N,
-    int64_t total, int max_iter, float lambda_init, float cost_thresh) {
-    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    int64_t total, int max_iter, float lambda_init, float cost_thresh, int xcd_band) {
+    // xcd_band: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, dispatch),
+    // so block b runs on XCD b % 8; block b takes the logical block (b % 8) * per + b / 8 instead,
+    // and each XCD walks ONE contiguous band of pixels -- its bilinear gathers stay in a band of
+    // the ray image that its own L2 holds, instead of every XCD touching every row (speed only:
+    // the mapping is a bijection whatever the placement)
+    int64_t lb = blockIdx.x;
+    if (xcd_band) {
+        const int64_t per = (int64_t)gridDim.x / 8;  // gridDim.x is a multiple of 8 here
+        lb = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    }
+    const int64_t g = lb * kBlock + threadIdx.x;
     if (g >= total) return;
     const int64_t b = g / N;
     const float* __restrict__ img = rays + b * (int64_t)H * W * 9;
@@ -338,10 +348,17 @@ extern "C" int m3s_iter_proj_ex(const float* rays, const float* pts, const float
     const int64_t total = B * N;
     if (total == 0) return M3S_OK;
     M3S_REQUIRE(rays && pts && p_init && p_new && converged, "iter_proj: null pointer");
+    // M3S_IP_XCD (default 1): the XCD-banded block order above; 0: blocks in pixel order
+    static const int xcd_band = [] {
+        const char* e = getenv("M3S_IP_XCD");
+        return e ? atoi(e) : 1;
+    }();
+    const int64_t nblk = (total + kBlock - 1) / kBlock;
+    const unsigned ip_grid = (unsigned)(xcd_band ? (nblk + 7) / 8 * 8 : nblk);
 #define M3S_IP(CM)                                                                                      \
-    hipLaunchKernelGGL(iter_proj_kernel<CM>, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream, \
+    hipLaunchKernelGGL(iter_proj_kernel<CM>, dim3(ip_grid), dim3(kBlock), 0, (hipStream_t)stream,       \
                        rays, pts, p_init, p_new, converged, (int)H, (int)W, N, total, max_iter,            \
-                       lambda_init, cost_thresh)
+                       lambda_init, cost_thresh, xcd_band)
     if (contract == M3S_CONTRACT_OFF) M3S_IP(M3S_CONTRACT_OFF);
     else if (contract == M3S_CONTRACT_NVCC) M3S_IP(M3S_CONTRACT_NVCC);
     else M3S_IP(M3S_CONTRACT_NVCC_RIGHT);
