@@ -556,9 +556,10 @@ struct SparsePlan {
     // block-format system: b (npose x 7, padded to bpad doubles), then 49-f64 blocks
     int bpad = 0;
     size_t o_sys = 0, o_y = 0, o_L = 0, o_W = 0, o_xd = 0, o_Lg = 0, o_int = 0;
-    // the plan integers, one array: [nodes fptr fronts tail tmap rounds] (nints_back: what the
-    // core + back-substitution launch stages in LDS) [tg tc rtg rc] (nints: the whole plan of
-    // the single-workgroup solve) [tc3 rc4] (multi-launch rounds only)
+    // the plan integers, one array: [nodes fptr fronts tail rounds | tmap] (nints_back: what the
+    // core + back-substitution launch stages in LDS; without tmap: a back-substitution-only launch)
+    // [tg tc rtg rc] (nints: the whole plan of the single-workgroup solve) [tc3 rc4] (multi-launch
+    // rounds only)
     size_t i_nodes = 0, i_fptr = 0, i_fronts = 0, i_tg = 0, i_tc = 0, i_rtg = 0, i_rc = 0,
            i_tail = 0, i_tmap = 0, i_rounds = 0, i_tc3 = 0, i_rc4 = 0, i_inl = 0, nints = 0, nints_back = 0;
     template <typename T>
@@ -845,7 +846,8 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         sp.o_linv = take(chol_linv_bytes(sp.npad_tail));
     }
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
-    // the plan integers in one array (layout: SparsePlan), the rounds after tmap
+    // the plan integers in one array (layout: SparsePlan), the rounds BEFORE tmap: a launch that
+    // only back-substitutes stages [nodes fptr fronts tail rounds] and not the core map
     std::vector<const std::vector<int>*> parts = {&sp.nodes, &sp.fptr, &sp.fronts, &sp.tail,
                                                   &sp.tmap, &sp.tg, &sp.tc, &sp.rtg, &sp.rc,
                                                   &sp.tc3, &sp.rc4, &sp.inl};
@@ -853,7 +855,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
                       &sp.i_tc, &sp.i_rtg, &sp.i_rc, &sp.i_tc3, &sp.i_rc4, &sp.i_inl};
     size_t n = 0;
     for (size_t k = 0; k < parts.size(); k++) {
-        if (k == 5) {
+        if (k == 4) {
             sp.i_rounds = n;
             n += 8 * sp.rounds.size();
         }
@@ -960,6 +962,7 @@ struct Ctx {
     const double* eblk_all() const { return eall ? eall : at<double>(L.edgeblk); }
     int chol_epoch = 0;  // dataflow factorisations enqueued in this call (chol_df.hip ready words)
     bool may_timeout = false;  // a solver with bounded device-side waits ran (kFlagTimeout)
+    bool retract_in_solve = false;  // the multi plan's back-substitution launch also retracted
     template <typename T>
     T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
     template <typename T>
@@ -1407,6 +1410,31 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
             M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_inl), R.tbeg + R.rbeg, R.nbt, R.nrt,
                                           sp.iptr(sp.i_tc3), sp.iptr(sp.i_rc4), A, b, Ls, W, y, flags));
     }
+    // M3S_MULTI_BACK (default 1): a multi-launch plan's back-substitution through the rounds and
+    // the retraction run in ONE single-workgroup launch (gn_solve's back phase, x in LDS) after the
+    // core's dataflow factorisation, instead of one launch per round plus a retraction launch
+    static const bool multi_back = env_int("M3S_MULTI_BACK", 1) != 0;
+    const size_t nmeta_back = sp.nints_back - sp.tmap.size();
+    if (!sp.hybrid && multi_back && !coop && sp.ntail > 0 && npose <= solve_max_poses() &&
+        solve_lds_bytes((int)nmeta_back) <= (size_t)kSolveMaxLds) {
+        c.may_timeout = true;  // chol_df's bounded waits
+        c.retract_in_solve = true;
+        M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
+                                          sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
+        M3S_HIP_CHECK(launch_dense_factor_solve(c.st, sp.npad_tail, sp.dptr<double>(sp.o_dense),
+                                                sp.dptr<double>(sp.o_linv), sp.dptr<double>(sp.o_xd), flags,
+                                                ++c.chol_epoch));
+        S.xd = sp.dptr<double>(sp.o_xd);
+        S.Hd = nullptr;
+        S.nmeta = (int)nmeta_back;
+        S.meta_lds = 1;
+        S.do_fwd = 0;
+        S.do_tail = 0;
+        S.do_back = 1;
+        S.x_tail_global = 1;
+        M3S_HIP_CHECK(launch_gn_solve_dbg(c.st, S));
+        return M3S_OK;
+    }
     // M3S_HYB_CORE=1 (default): the hybrid's dense core (<= 27 poses) is factored and solved by
     // the dataflow launch (chol_df.hip: batch-cyclic tile factor, ~100 ns per column on the
     // pivot chain, back-substitution in the same launch) instead of gn_solve's in-register pose
@@ -1574,7 +1602,7 @@ int run(const m3s_gn_args& a) {
         rc = enqueue_solve(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
-        if (!c.sp.fused && !c.sp.hybrid)  // gn_solve retracts inside its launch
+        if (!c.sp.fused && !c.sp.hybrid && !c.retract_in_solve)  // gn_solve retracts inside its launch
             M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
                                          a.delta_thresh, flags, a.contract));
         g_prof.mark(c.st);
