@@ -962,7 +962,6 @@ struct Ctx {
     const double* eblk_all() const { return eall ? eall : at<double>(L.edgeblk); }
     int chol_epoch = 0;  // dataflow factorisations enqueued in this call (chol_df.hip ready words)
     bool may_timeout = false;  // a solver with bounded device-side waits ran (kFlagTimeout)
-    bool retract_in_solve = false;  // the multi plan's back-substitution launch also retracted
     template <typename T>
     T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
     template <typename T>
@@ -1410,31 +1409,6 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
             M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_inl), R.tbeg + R.rbeg, R.nbt, R.nrt,
                                           sp.iptr(sp.i_tc3), sp.iptr(sp.i_rc4), A, b, Ls, W, y, flags));
     }
-    // M3S_MULTI_BACK (default 1): a multi-launch plan's back-substitution through the rounds and
-    // the retraction run in ONE single-workgroup launch (gn_solve's back phase, x in LDS) after the
-    // core's dataflow factorisation, instead of one launch per round plus a retraction launch
-    static const bool multi_back = env_int("M3S_MULTI_BACK", 1) != 0;
-    const size_t nmeta_back = sp.nints_back - sp.tmap.size();
-    if (!sp.hybrid && multi_back && !coop && sp.ntail > 0 && npose <= solve_max_poses() &&
-        solve_lds_bytes((int)nmeta_back) <= (size_t)kSolveMaxLds) {
-        c.may_timeout = true;  // chol_df's bounded waits
-        c.retract_in_solve = true;
-        M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
-                                          sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
-        M3S_HIP_CHECK(launch_dense_factor_solve(c.st, sp.npad_tail, sp.dptr<double>(sp.o_dense),
-                                                sp.dptr<double>(sp.o_linv), sp.dptr<double>(sp.o_xd), flags,
-                                                ++c.chol_epoch));
-        S.xd = sp.dptr<double>(sp.o_xd);
-        S.Hd = nullptr;
-        S.nmeta = (int)nmeta_back;
-        S.meta_lds = 1;
-        S.do_fwd = 0;
-        S.do_tail = 0;
-        S.do_back = 1;
-        S.x_tail_global = 1;
-        M3S_HIP_CHECK(launch_gn_solve_dbg(c.st, S));
-        return M3S_OK;
-    }
     // M3S_HYB_CORE=1 (default): the hybrid's dense core (<= 27 poses) is factored and solved by
     // the dataflow launch (chol_df.hip: batch-cyclic tile factor, ~100 ns per column on the
     // pivot chain, back-substitution in the same launch) instead of gn_solve's in-register pose
@@ -1602,7 +1576,7 @@ int run(const m3s_gn_args& a) {
         rc = enqueue_solve(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
-        if (!c.sp.fused && !c.sp.hybrid && !c.retract_in_solve)  // gn_solve retracts inside its launch
+        if (!c.sp.fused && !c.sp.hybrid)  // gn_solve retracts inside its launch
             M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
                                          a.delta_thresh, flags, a.contract));
         g_prof.mark(c.st);
