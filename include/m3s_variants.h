@@ -20,8 +20,10 @@ enum {
     M3S_REFINE_VARIANT_LDS = 1,  /* candidate box of a 32x16 pixel tile staged in LDS */
     M3S_REFINE_VARIANT_MFMA = 2, /* approximate scores on v_mfma_f32_16x16x32_f16 + exact re-score */
     M3S_REFINE_VARIANT_DOT2 = 3, /* approximate scores with v_dot2 + exact re-score */
-    M3S_REFINE_VARIANT_LATTICE = 4 /* MFMA over per-level lattice buckets of the tile + exact re-score
+    M3S_REFINE_VARIANT_LATTICE = 4, /* MFMA over per-level lattice buckets of the tile + exact re-score
                                       (dilation_max <= 5) */
+    M3S_REFINE_VARIANT_BOX = 5     /* a 16x16 tile's candidate box staged per level as plane-major
+                                      8-B pieces in LDS (round 5) */
 };
 
 /* refine_matches (fp16, F = 24, radius 3, N = H*W) with one of the variants; returns M3S_OK or an

@@ -864,6 +864,210 @@ __global__ __launch_bounds__(kLdsThreads) void refine_lds_kernel(
         atomicAdd(stats, n_global_levels);  // diagnostics: levels that did not fit the LDS tile
 }
 
+
+// ---------------------------------------------------------------------------------
+// refine_matches, plane-major LDS box (M3S_REFINE_VARIANT_BOX, round 5).
+//
+// A 256-thread workgroup takes a 16x16 pixel tile (lane = pixel, the product kernel's XCD-banded
+// tile order).  Per dilation level it stages the bounding box of its pixels' image-clipped
+// candidate windows in LDS once -- coalesced 16-B global loads, 48 B per cell -- as 6 planes of
+// 8-B pieces (plane p holds halves 4p .. 4p+3 of every cell: a candidate is 6 ds_read_b64, 32
+// lanes per LDS cycle, bank pair 2 * cell mod 64), then scores every candidate from LDS with the
+// product kernel's exact c10::Half chain (score_f16_multi) in the reference's candidate order, a
+// window column of 7 at a time, the next column's reads issued before the current one is scored.
+// The 16x16 tile keeps the largest box (d = 5: ~54 x 54 cells) under the 3300-cell cap, where
+// the former LDS variant's 32 x 16 tile sent every d = 5 level to its slow global fallback; a
+// level whose box still exceeds the cap gathers its candidates from global memory, a window
+// column at a time as the product kernel does.  Bitwise the product kernel's matches.
+// ---------------------------------------------------------------------------------
+constexpr int kBoxCap = 3300;  // cells: 6 planes x 8 B x 3300 = 158,400 B of the CU's 160 KiB
+
+__device__ __forceinline__ void box_minmax4(int (&v)[4], int* red /* [4 waves][4] */) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        v[0] = min(v[0], __shfl_xor(v[0], off, 64));
+        v[1] = max(v[1], __shfl_xor(v[1], off, 64));
+        v[2] = min(v[2], __shfl_xor(v[2], off, 64));
+        v[3] = max(v[3], __shfl_xor(v[3], off, 64));
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) red[wave * 4 + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        v[0] = min(v[0], red[w * 4 + 0]);
+        v[1] = max(v[1], red[w * 4 + 1]);
+        v[2] = min(v[2], red[w * 4 + 2]);
+        v[3] = max(v[3], red[w * 4 + 3]);
+    }
+    __syncthreads();  // red is rewritten by the next level
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void refine_box_kernel(const uint16_t* __restrict__ D11,
+                                                           const uint16_t* __restrict__ D21,
+                                                           const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new,
+                                                           int64_t* __restrict__ lin, int H, int W, int64_t N,
+                                                           int64_t B, TileMap tm, int dilation_max,
+                                                           unsigned long long* __restrict__ stats) {
+    constexpr int F = 24, SC = 2 * R + 1;
+    __shared__ uint2 box[6 * kBoxCap];
+    __shared__ int red[16];
+    // tile_pixel's XCD-banded order, keeping the lanes of a partial tile in the workgroup (barriers)
+    const int64_t nblk = (int64_t)gridDim.x;
+    const int64_t per = (nblk + 7) / 8;
+    const int64_t lb = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (lb >= (int64_t)tm.ntiles * B) return;  // workgroup-uniform
+    const int64_t b = lb / tm.ntiles;
+    const int t = (int)(lb - b * tm.ntiles);
+    const int ty = t / tm.tiles_x, tx = t - ty * tm.tiles_x;
+    const int pu = tx * kTile + (threadIdx.x & (kTile - 1)), pv = ty * kTile + (threadIdx.x / kTile);
+    const bool active = pu < W && pv < H;
+    const int64_t g = b * (int64_t)H * W + (int64_t)pv * W + pu;
+    const uint16_t* __restrict__ img = D11 + b * (int64_t)H * W * F;
+
+    half2_t q2[F / 2];
+    int64_t u0 = 0, v0 = 0;
+    if (active) {
+        const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
+#pragma unroll
+        for (int c = 0; c < F / 8; c++) {
+            const uint4 w = src[c];
+            const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
+#pragma unroll
+            for (int k = 0; k < 4; k++) q2[c * 4 + k] = hp[k];
+        }
+        u0 = p1[g * 2 + 0];
+        v0 = p1[g * 2 + 1];
+    }
+    half_t max_score = (half_t)kRefineHalfMaxInit;
+    int64_t u_new = u0, v_new = v0;
+    unsigned n_global = 0;
+    for (int d = dilation_max; d > 0; d--) {
+        const int64_t rd = (int64_t)R * d;
+        int w4[4] = {INT_MAX, INT_MIN, INT_MAX, INT_MIN};
+        if (active) {
+            const int64_t ulo = max(u0 - rd, (int64_t)0), uhi = min(u0 + rd, (int64_t)W - 1);
+            const int64_t vlo = max(v0 - rd, (int64_t)0), vhi = min(v0 + rd, (int64_t)H - 1);
+            if (ulo <= uhi && vlo <= vhi) {
+                w4[0] = (int)ulo;
+                w4[1] = (int)uhi;
+                w4[2] = (int)vlo;
+                w4[3] = (int)vhi;
+            }
+        }
+        box_minmax4(w4, red);
+        const int umin = w4[0], vmin = w4[2];
+        const bool any = w4[0] <= w4[1];
+        const int Rw = any ? w4[1] - w4[0] + 1 : 0, Rh = any ? w4[3] - w4[2] + 1 : 0;
+        const bool fits = any && Rw * Rh <= kBoxCap;  // workgroup-uniform
+        if (fits) {
+            // stage: cell c = (r, x) of the box, 4 cells (12 x 16-B loads) in flight per lane
+            const int n = Rw * Rh;
+            const float inv = 1.0f / (float)Rw;
+            for (int c0 = threadIdx.x; c0 < n; c0 += 4 * kBlock) {
+                uint4 v[4][3];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int c = min(c0 + k * kBlock, n - 1);
+                    const int r = (int)(((float)c + 0.5f) * inv);
+                    const uint4* src = reinterpret_cast<const uint4*>(
+                        img + ((int64_t)(vmin + r) * W + umin + (c - r * Rw)) * F);
+#pragma unroll
+                    for (int q = 0; q < 3; q++) v[k][q] = src[q];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int c = c0 + k * kBlock;
+                    if (c < n) {
+#pragma unroll
+                        for (int q = 0; q < 3; q++) {
+                            box[(2 * q) * kBoxCap + c] = make_uint2(v[k][q].x, v[k][q].y);
+                            box[(2 * q + 1) * kBoxCap + c] = make_uint2(v[k][q].z, v[k][q].w);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            if (active) {
+                uint4 ra[SC][3], rb[SC][3];
+                bool oka[SC], okb[SC];
+                auto fetch = [&](int i, uint4 (&rw)[SC][3], bool (&okk)[SC]) {
+                    const int64_t u = u0 - rd + (int64_t)i * d;
+#pragma unroll
+                    for (int j = 0; j < SC; j++) {
+                        const int64_t v = v0 - rd + (int64_t)j * d;
+                        okk[j] = inside_image(u, v, W, H);
+                        const int cell = okk[j] ? (int)(v - vmin) * Rw + (int)(u - umin) : 0;
+#pragma unroll
+                        for (int q = 0; q < 3; q++) {
+                            const uint2 lo = box[(2 * q) * kBoxCap + cell];
+                            const uint2 hi = box[(2 * q + 1) * kBoxCap + cell];
+                            rw[j][q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+                        }
+                    }
+                };
+                auto consume = [&](int i, const uint4 (&rw)[SC][3], const bool (&okk)[SC]) {
+                    half_t score[SC];
+                    score_f16_multi<F, SC>(q2, rw, score);
+                    const int64_t u = u0 - rd + (int64_t)i * d;
+#pragma unroll
+                    for (int j = 0; j < SC; j++) {  // v offset inner (matching_kernels.cu:55)
+                        if (okk[j] && score[j] > max_score) {
+                            max_score = score[j];
+                            u_new = u;
+                            v_new = v0 - rd + (int64_t)j * d;
+                        }
+                    }
+                };
+                fetch(0, ra, oka);
+#pragma unroll
+                for (int i = 0; i < SC; i += 2) {  // u offset outer (matching_kernels.cu:54)
+                    if (i + 1 < SC) fetch(i + 1, rb, okb);
+                    consume(i, ra, oka);
+                    if (i + 1 < SC) {
+                        if (i + 2 < SC) fetch(i + 2, ra, oka);
+                        consume(i + 1, rb, okb);
+                    }
+                }
+            }
+            __syncthreads();  // the next level's staging overwrites the box
+        } else if (active && any) {
+            n_global++;
+            for (int i = 0; i < SC; i++) {
+                const int64_t u = u0 - rd + (int64_t)i * d;
+                uint4 rows[SC][3];
+                bool ok[SC];
+#pragma unroll
+                for (int j = 0; j < SC; j++) {
+                    const int64_t v = v0 - rd + (int64_t)j * d;
+                    ok[j] = inside_image(u, v, W, H);
+                    const uint4* src = reinterpret_cast<const uint4*>(img + (ok[j] ? (v * W + u) * F : 0));
+#pragma unroll
+                    for (int q = 0; q < 3; q++) rows[j][q] = src[q];
+                }
+                half_t score[SC];
+                score_f16_multi<F, SC>(q2, rows, score);
+#pragma unroll
+                for (int j = 0; j < SC; j++) {
+                    if (ok[j] && score[j] > max_score) {
+                        max_score = score[j];
+                        u_new = u;
+                        v_new = v0 - rd + (int64_t)j * d;
+                    }
+                }
+            }
+        }
+        u0 = u_new;
+        v0 = v_new;
+    }
+    if (active) store_match(p1_new, lin, g, W, u_new, v_new);
+    if (stats && n_global) atomicAdd(stats + 2, (unsigned long long)n_global);  // diagnostics
+}
+
 // Generic F (any descriptor width), fp16, f32 or f64 (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
 // matching_kernels.cu:103), scalar loads.
 }  // namespace
@@ -891,12 +1095,25 @@ extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const ui
     M3S_REQUIRE(F == 24 && aligned && N == H * W && radius == 3,
                 "refine variant: needs F = 24, 16-B aligned descriptors, N = H*W and radius 3");
     M3S_REQUIRE(variant == M3S_REFINE_VARIANT_LDS || variant == M3S_REFINE_VARIANT_MFMA ||
-                    variant == M3S_REFINE_VARIANT_DOT2 || variant == M3S_REFINE_VARIANT_LATTICE,
+                    variant == M3S_REFINE_VARIANT_DOT2 || variant == M3S_REFINE_VARIANT_LATTICE ||
+                    variant == M3S_REFINE_VARIANT_BOX,
                 "refine variant: unknown kind %d", variant);
     M3S_REQUIRE(variant != M3S_REFINE_VARIANT_LATTICE || dilation_max <= kLatMaxD,
                 "refine variant: the lattice kernel handles dilation_max <= %d", kLatMaxD);
     hipStream_t st = (hipStream_t)stream;
     int64_t* lin = nullptr;
+    if (variant == M3S_REFINE_VARIANT_BOX) {
+        TileMap tm;
+        tm.tiles_x = (int)((W + kTile - 1) / kTile);
+        tm.tiles_y = (int)((H + kTile - 1) / kTile);
+        tm.ntiles = tm.tiles_x * tm.tiles_y;
+        const int64_t nblk = (int64_t)tm.ntiles * B;
+        const int64_t grid = (nblk + 7) / 8 * 8;
+        hipLaunchKernelGGL((refine_box_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1, p1_new,
+                           lin, (int)H, (int)W, N, B, tm, dilation_max, (unsigned long long*)nullptr);
+        M3S_LAUNCH_CHECK();
+        return M3S_OK;
+    }
     if (variant != M3S_REFINE_VARIANT_LDS) {
         TileMap tm;
         tm.tiles_x = (int)((W + kTile - 1) / kTile);

@@ -34,7 +34,19 @@ for B in (1, 8):
         if r >= 3:
             t_ip += ev[0].elapsed_time(ev[1]) / reps
             t_rf += ev[1].elapsed_time(ev[2]) / reps
-    out[f"B{B}"] = {"iter_proj_ms": t_ip, "refine_ms": t_rf,
+    from mast3r_slam_backends import variants as mv
+    var = {}
+    for name, kind in (("lds", mv.LDS), ("box", mv.BOX)):
+        t = 0.0
+        for r in range(reps + 3):
+            ev[1].record()
+            o = mv.refine_matches_variant(kind, D11, D21, p1, 3, 5)[0]
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r >= 3:
+                t += ev[1].elapsed_time(ev[2]) / reps
+        var[name] = {"ms": t, "bitwise_product": bool(torch.equal(o, pr))}
+    out[f"B{B}"] = {"iter_proj_ms": t_ip, "refine_ms": t_rf, "refine_variants": var,
                     "iter_proj_GBps_65B": 65 * B * h * w / (t_ip * 1e-3) / 1e9,
                     "p_checksum": float(pn.double().sum()), "conv": int(cv.sum()),
                     "refine_checksum": int(pr.sum())}
