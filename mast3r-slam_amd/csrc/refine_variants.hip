@@ -906,7 +906,7 @@ __device__ __forceinline__ void box_minmax4(int (&v)[4], int* red /* [4 waves][4
     __syncthreads();  // red is rewritten by the next level
 }
 
-template <int R>
+template <int R, int DIAG = 0>
 __global__ __launch_bounds__(kBlock) void refine_box_kernel(const uint16_t* __restrict__ D11,
                                                            const uint16_t* __restrict__ D21,
                                                            const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new,
@@ -968,7 +968,7 @@ __global__ __launch_bounds__(kBlock) void refine_box_kernel(const uint16_t* __re
             // stage: cell c = (r, x) of the box, 4 cells (12 x 16-B loads) in flight per lane
             const int n = Rw * Rh;
             const float inv = 1.0f / (float)Rw;
-            for (int c0 = threadIdx.x; c0 < n; c0 += 4 * kBlock) {
+            for (int c0 = threadIdx.x; c0 < (DIAG == 1 ? 0 : n); c0 += 4 * kBlock) {
                 uint4 v[4][3];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -992,7 +992,7 @@ __global__ __launch_bounds__(kBlock) void refine_box_kernel(const uint16_t* __re
                 }
             }
             __syncthreads();
-            if (active) {
+            if (active && DIAG != 2) {
                 uint4 ra[SC][3], rb[SC][3];
                 bool oka[SC], okb[SC];
                 auto fetch = [&](int i, uint4 (&rw)[SC][3], bool (&okk)[SC]) {
@@ -1109,8 +1109,20 @@ extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const ui
         tm.ntiles = tm.tiles_x * tm.tiles_y;
         const int64_t nblk = (int64_t)tm.ntiles * B;
         const int64_t grid = (nblk + 7) / 8 * 8;
-        hipLaunchKernelGGL((refine_box_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1, p1_new,
-                           lin, (int)H, (int)W, N, B, tm, dilation_max, (unsigned long long*)nullptr);
+        // M3S_BOX_DIAG (diagnostics, wrong matches): 1 = no staging loads, 2 = no scoring
+        static const int diag = [] {
+            const char* e = getenv("M3S_BOX_DIAG");
+            return e ? atoi(e) : 0;
+        }();
+        if (diag == 1)
+            hipLaunchKernelGGL((refine_box_kernel<3, 1>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
+                               p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, (unsigned long long*)nullptr);
+        else if (diag == 2)
+            hipLaunchKernelGGL((refine_box_kernel<3, 2>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1,
+                               p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max, (unsigned long long*)nullptr);
+        else
+            hipLaunchKernelGGL((refine_box_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, D11, D21, p1, p1_new,
+                               lin, (int)H, (int)W, N, B, tm, dilation_max, (unsigned long long*)nullptr);
         M3S_LAUNCH_CHECK();
         return M3S_OK;
     }
