@@ -22,8 +22,10 @@ enum {
     M3S_REFINE_VARIANT_DOT2 = 3, /* approximate scores with v_dot2 + exact re-score */
     M3S_REFINE_VARIANT_LATTICE = 4, /* MFMA over per-level lattice buckets of the tile + exact re-score
                                       (dilation_max <= 5) */
-    M3S_REFINE_VARIANT_BOX = 5     /* a 16x16 tile's candidate box staged per level as plane-major
+    M3S_REFINE_VARIANT_BOX = 5,    /* a 16x16 tile's candidate box staged per level as plane-major
                                       8-B pieces in LDS (round 5) */
+    M3S_REFINE_VARIANT_PLANES = 6  /* the product kernel's gathers from a plane-major copy of D11
+                                      (3 planes of 16-B pieces, one copy pass per call) */
 };
 
 /* refine_matches (fp16, F = 24, radius 3, N = H*W) with one of the variants; returns M3S_OK or an

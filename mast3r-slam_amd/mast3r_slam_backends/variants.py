@@ -10,7 +10,7 @@ import torch
 
 from . import _check, _on_device, _ptr, _stream
 
-LDS, MFMA, DOT2, LATTICE, BOX = 1, 2, 3, 4, 5  # M3S_REFINE_VARIANT_*
+LDS, MFMA, DOT2, LATTICE, BOX, PLANES = 1, 2, 3, 4, 5, 6  # M3S_REFINE_VARIANT_*
 
 library_path = os.environ.get("M3S_VARIANTS_LIB", os.path.join(
     os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libm3s_variants.so"))

@@ -106,7 +106,7 @@ def test_refine_matches_f16_bit_exact(backend, oracle, B, H, W, dot2):
     assert np.array_equal(out_g, out_o), f"{(out_g != out_o).any(-1).sum()} matches differ"
 
 
-@pytest.mark.parametrize("variant", [1, 4, 5])  # variants.LDS, variants.LATTICE, variants.BOX
+@pytest.mark.parametrize("variant", [1, 4, 5, 6])  # variants.LDS, LATTICE, BOX, PLANES
 @pytest.mark.parametrize("scatter", [0, 3, 40, 10**6])
 def test_refine_lds_tile_and_fallback(backend, oracle, scatter, variant):
     """The LDS-tiled and the lattice-bucket MFMA variants against the oracle and against the

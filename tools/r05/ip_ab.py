@@ -36,7 +36,7 @@ for B in (1, 8):
             t_rf += ev[1].elapsed_time(ev[2]) / reps
     from mast3r_slam_backends import variants as mv
     var = {}
-    for name, kind in (("lds", mv.LDS), ("box", mv.BOX)):
+    for name, kind in (("lds", mv.LDS), ("box", mv.BOX), ("planes", mv.PLANES)):
         t = 0.0
         for r in range(reps + 3):
             ev[1].record()
