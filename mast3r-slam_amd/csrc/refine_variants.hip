@@ -1113,11 +1113,24 @@ __global__ __launch_bounds__(kBlock) void refine_planes_kernel(const uint4* __re
             for (int k = 0; k < 4; k++) q2[c * 4 + k] = hp[k];
         }
     }
-    const uint4* __restrict__ pl = P + b * 3 * HW;
+    // the three planes of this image (a tile lies in one image: b is workgroup-uniform) as ONE buffer
+    // descriptor in SGPRs, the plane offset as the uniform soffset and the cell as a 32-bit byte
+    // offset: buffer_load_dwordx4, no 64-bit address arithmetic per candidate (coordinates beyond
+    // +-2^20 or planes beyond 2 GiB take the 64-bit path)
+    const uint4* __restrict__ pl0 = P + b * 3 * HW;
+    const uint4* __restrict__ pl1 = pl0 + HW;
+    const uint4* __restrict__ pl2 = pl1 + HW;
+    const int bf = __builtin_amdgcn_readfirstlane((int)b);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(P + (int64_t)bf * 3 * HW), (short)0, (int)(3 * HW * 16 < ((int64_t)1 << 31) ? 3 * HW * 16 : 0), 0x00020000);
+    const unsigned plane_bytes = (unsigned)(HW * 16);
     int64_t u0 = p1[g * 2 + 0];
     int64_t v0 = p1[g * 2 + 1];
     half_t max_score = (half_t)kRefineHalfMaxInit;
     int64_t u_new = u0, v_new = v0;
+    constexpr int64_t kLim = 1 << 20;
+    const bool off32 = 3 * HW * 16 < ((int64_t)1 << 31) && dilation_max < 1024 &&
+                       __all(b == bf && u0 > -kLim && u0 < kLim && v0 > -kLim && v0 < kLim);
     for (int d = dilation_max; d > 0; d--) {
         const int64_t rd = (int64_t)R * d;
         for (int i = 0; i < SC; i++) {  // u offset outer (matching_kernels.cu:54)
@@ -1128,9 +1141,19 @@ __global__ __launch_bounds__(kBlock) void refine_planes_kernel(const uint4* __re
             for (int j = 0; j < SC; j++) {
                 const int64_t v = v0 - rd + (int64_t)j * d;
                 ok[j] = inside_image(u, v, W, H);
-                const int64_t cell = ok[j] ? v * W + u : 0;
+                if (off32) {
+                    const unsigned boff = ok[j] ? (unsigned)((int)v * W + (int)u) * 16u : 0u;
 #pragma unroll
-                for (int q = 0; q < 3; q++) rows[j][q] = pl[q * HW + cell];
+                    for (int q = 0; q < 3; q++) {
+                        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, q * plane_bytes, 0);
+                        rows[j][q] = make_uint4(w[0], w[1], w[2], w[3]);
+                    }
+                } else {
+                    const int64_t cell = ok[j] ? v * W + u : 0;
+                    rows[j][0] = pl0[cell];
+                    rows[j][1] = pl1[cell];
+                    rows[j][2] = pl2[cell];
+                }
             }
             half_t score[SC];
             score_f16_multi<F, SC>(q2, rows, score);
