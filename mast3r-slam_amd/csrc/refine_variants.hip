@@ -1068,6 +1068,87 @@ __global__ __launch_bounds__(kBlock) void refine_box_kernel(const uint16_t* __re
     if (stats && n_global) atomicAdd(stats + 2, (unsigned long long)n_global);  // diagnostics
 }
 
+
+// ---------------------------------------------------------------------------------
+// refine_matches on a plane-major copy of D11 (M3S_REFINE_VARIANT_PLANES, round 5).
+//
+// The product kernel gathers a candidate's 48-B row as 3 dwordx4 loads; the 64 lanes of one load
+// read 16 B from each of ~64 cells 48 B apart, so every load instruction touches all ~24-28 cache
+// lines of the wave's candidate rows (the L1/TA path, not the VALU, bounds it: DESIGN.md section 4).
+// Here D11 is first copied to 3 planes (plane q holds the 16-B piece q of every cell,
+// contiguously: [B][3][H*W] x 16 B), so load q of a wave reads 64 consecutive-ish 16-B pieces:
+// ~1/3 of the lines per instruction.  The copy is one pass over D11 (read 48 B + write 48 B per
+// cell).  Same candidate order, same c10::Half chain (score_f16_multi) => the product's matches.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void d11_planes_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          int64_t HW, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // cell (b, n)
+    if (i >= total) return;
+    const int64_t b = i / HW, n = i - b * HW;
+    const uint4 a0 = src[3 * i], a1 = src[3 * i + 1], a2 = src[3 * i + 2];
+    uint4* d = dst + b * 3 * HW + n;
+    d[0] = a0;
+    d[HW] = a1;
+    d[2 * HW] = a2;
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void refine_planes_kernel(const uint4* __restrict__ P, const uint16_t* __restrict__ D21,
+                                                              const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new,
+                                                              int64_t* __restrict__ lin, int H, int W, int64_t N, int64_t B,
+                                                              TileMap tm, int dilation_max) {
+    constexpr int F = 24, SC = 2 * R + 1;
+    int64_t g;
+    if (!tile_pixel(tm, B, W, H, g)) return;
+    const int64_t b = g / N;
+    const int64_t HW = (int64_t)H * W;
+    half2_t q2[F / 2];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
+#pragma unroll
+        for (int c = 0; c < F / 8; c++) {
+            const uint4 w = src[c];
+            const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
+#pragma unroll
+            for (int k = 0; k < 4; k++) q2[c * 4 + k] = hp[k];
+        }
+    }
+    const uint4* __restrict__ pl = P + b * 3 * HW;
+    int64_t u0 = p1[g * 2 + 0];
+    int64_t v0 = p1[g * 2 + 1];
+    half_t max_score = (half_t)kRefineHalfMaxInit;
+    int64_t u_new = u0, v_new = v0;
+    for (int d = dilation_max; d > 0; d--) {
+        const int64_t rd = (int64_t)R * d;
+        for (int i = 0; i < SC; i++) {  // u offset outer (matching_kernels.cu:54)
+            const int64_t u = u0 - rd + (int64_t)i * d;
+            uint4 rows[SC][3];
+            bool ok[SC];
+#pragma unroll
+            for (int j = 0; j < SC; j++) {
+                const int64_t v = v0 - rd + (int64_t)j * d;
+                ok[j] = inside_image(u, v, W, H);
+                const int64_t cell = ok[j] ? v * W + u : 0;
+#pragma unroll
+                for (int q = 0; q < 3; q++) rows[j][q] = pl[q * HW + cell];
+            }
+            half_t score[SC];
+            score_f16_multi<F, SC>(q2, rows, score);
+#pragma unroll
+            for (int j = 0; j < SC; j++) {  // v offset inner (:55)
+                if (ok[j] && score[j] > max_score) {
+                    max_score = score[j];
+                    u_new = u;
+                    v_new = v0 - rd + (int64_t)j * d;
+                }
+            }
+        }
+        u0 = u_new;
+        v0 = v_new;
+    }
+    store_match(p1_new, lin, g, W, u_new, v_new);
+}
+
 // Generic F (any descriptor width), fp16, f32 or f64 (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
 // matching_kernels.cu:103), scalar loads.
 }  // namespace
@@ -1096,12 +1177,30 @@ extern "C" int m3s_refine_variant_f16(int variant, const uint16_t* D11, const ui
                 "refine variant: needs F = 24, 16-B aligned descriptors, N = H*W and radius 3");
     M3S_REQUIRE(variant == M3S_REFINE_VARIANT_LDS || variant == M3S_REFINE_VARIANT_MFMA ||
                     variant == M3S_REFINE_VARIANT_DOT2 || variant == M3S_REFINE_VARIANT_LATTICE ||
-                    variant == M3S_REFINE_VARIANT_BOX,
+                    variant == M3S_REFINE_VARIANT_BOX || variant == M3S_REFINE_VARIANT_PLANES,
                 "refine variant: unknown kind %d", variant);
     M3S_REQUIRE(variant != M3S_REFINE_VARIANT_LATTICE || dilation_max <= kLatMaxD,
                 "refine variant: the lattice kernel handles dilation_max <= %d", kLatMaxD);
     hipStream_t st = (hipStream_t)stream;
     int64_t* lin = nullptr;
+    if (variant == M3S_REFINE_VARIANT_PLANES) {
+        TileMap tm;
+        tm.tiles_x = (int)((W + kTile - 1) / kTile);
+        tm.tiles_y = (int)((H + kTile - 1) / kTile);
+        tm.ntiles = tm.tiles_x * tm.tiles_y;
+        const int64_t nblk = (int64_t)tm.ntiles * B;
+        const int64_t grid = (nblk + 7) / 8 * 8;
+        const int64_t cells = B * H * W;
+        uint4* planes = nullptr;
+        M3S_HIP_CHECK(hipMallocAsync((void**)&planes, sizeof(uint4) * 3 * (size_t)cells, st));
+        hipLaunchKernelGGL(d11_planes_kernel, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           reinterpret_cast<const uint4*>(D11), planes, H * W, cells);
+        hipLaunchKernelGGL((refine_planes_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st, planes, D21, p1,
+                           p1_new, lin, (int)H, (int)W, N, B, tm, dilation_max);
+        M3S_LAUNCH_CHECK();
+        M3S_HIP_CHECK(hipFreeAsync(planes, st));
+        return M3S_OK;
+    }
     if (variant == M3S_REFINE_VARIANT_BOX) {
         TileMap tm;
         tm.tiles_x = (int)((W + kTile - 1) / kTile);
