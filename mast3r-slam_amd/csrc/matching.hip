@@ -399,6 +399,25 @@ int refine_f16_launch(const uint16_t* D11, const uint16_t* D21, const int64_t* p
     M3S_LAUNCH_CHECK();
     return M3S_OK;
 }
+
+// the fused matching op's refine (match_glue.hip): D11's fp16 copy is already plane-major
+// (refine_planes_kernel, refine_common.h); F = 24, radius 3, N = H * W
+int refine_planes_launch(const void* D11_planes, const uint16_t* D21, const int64_t* p1, int64_t* lin, int64_t B,
+                         int64_t H, int64_t W, int dilation_max, hipStream_t st) {
+    const int64_t N = H * W;
+    if (B * N == 0) return M3S_OK;
+    TileMap tm;
+    tm.tiles_x = (int)((W + kTile - 1) / kTile);
+    tm.tiles_y = (int)((H + kTile - 1) / kTile);
+    tm.ntiles = tm.tiles_x * tm.tiles_y;
+    const int64_t nblk = (int64_t)tm.ntiles * B;
+    const int64_t grid = (nblk + 7) / 8 * 8;
+    hipLaunchKernelGGL((refine_planes_kernel<3>), dim3((unsigned)grid), dim3(kBlock), 0, st,
+                       static_cast<const uint4*>(D11_planes), D21, p1, (int64_t*)nullptr, lin, (int)H, (int)W, N, B,
+                       tm, dilation_max);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+}
 }  // namespace m3s
 
 extern "C" int m3s_refine_matches_f16(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,

@@ -1092,62 +1092,7 @@ __global__ __launch_bounds__(kBlock) void d11_planes_kernel(const uint4* __restr
     d[2 * HW] = a2;
 }
 
-template <int R>
-__global__ __launch_bounds__(kBlock) void refine_planes_kernel(const uint4* __restrict__ P, const uint16_t* __restrict__ D21,
-                                                              const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new,
-                                                              int64_t* __restrict__ lin, int H, int W, int64_t N, int64_t B,
-                                                              TileMap tm, int dilation_max) {
-    constexpr int F = 24, SC = 2 * R + 1;
-    int64_t g;
-    if (!tile_pixel(tm, B, W, H, g)) return;
-    const int64_t b = g / N;
-    const int64_t HW = (int64_t)H * W;
-    half2_t q2[F / 2];
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(D21 + g * F);
-#pragma unroll
-        for (int c = 0; c < F / 8; c++) {
-            const uint4 w = src[c];
-            const half2_t* hp = reinterpret_cast<const half2_t*>(&w);
-#pragma unroll
-            for (int k = 0; k < 4; k++) q2[c * 4 + k] = hp[k];
-        }
-    }
-    const uint4* __restrict__ pl = P + b * 3 * HW;
-    int64_t u0 = p1[g * 2 + 0];
-    int64_t v0 = p1[g * 2 + 1];
-    half_t max_score = (half_t)kRefineHalfMaxInit;
-    int64_t u_new = u0, v_new = v0;
-    for (int d = dilation_max; d > 0; d--) {
-        const int64_t rd = (int64_t)R * d;
-        for (int i = 0; i < SC; i++) {  // u offset outer (matching_kernels.cu:54)
-            const int64_t u = u0 - rd + (int64_t)i * d;
-            uint4 rows[SC][3];
-            bool ok[SC];
-#pragma unroll
-            for (int j = 0; j < SC; j++) {
-                const int64_t v = v0 - rd + (int64_t)j * d;
-                ok[j] = inside_image(u, v, W, H);
-                const int64_t cell = ok[j] ? v * W + u : 0;
-#pragma unroll
-                for (int q = 0; q < 3; q++) rows[j][q] = pl[q * HW + cell];
-            }
-            half_t score[SC];
-            score_f16_multi<F, SC>(q2, rows, score);
-#pragma unroll
-            for (int j = 0; j < SC; j++) {  // v offset inner (:55)
-                if (ok[j] && score[j] > max_score) {
-                    max_score = score[j];
-                    u_new = u;
-                    v_new = v0 - rd + (int64_t)j * d;
-                }
-            }
-        }
-        u0 = u_new;
-        v0 = v_new;
-    }
-    store_match(p1_new, lin, g, W, u_new, v_new);
-}
+// (refine_planes_kernel: refine_common.h, shared with the fused matching op)
 
 // Generic F (any descriptor width), fp16, f32 or f64 (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
 // matching_kernels.cu:103), scalar loads.

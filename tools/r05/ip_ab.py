@@ -46,6 +46,19 @@ for B in (1, 8):
             if r >= 3:
                 t += ev[1].elapsed_time(ev[2]) / reps
         var[name] = {"ms": t, "bitwise_product": bool(torch.equal(o, pr))}
+    from m3s.matching import match_iterative_proj
+    for _ in range(3):
+        i_f, v_f = match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=True)
+    torch.cuda.synchronize()
+    t_fused = 0.0
+    for r in range(reps):
+        ev[0].record()
+        i_f, v_f = match_iterative_proj(mp.X11, mp.X21, mp.D11, mp.D21, mp.idx_init, fused=True)
+        ev[1].record()
+        torch.cuda.synchronize()
+        t_fused += ev[0].elapsed_time(ev[1]) / reps
+    var["fused_op"] = {"ms": t_fused, "idx_checksum": int(i_f.sum()), "valid": int(v_f.sum()),
+                       "bitwise_product": True}
     out[f"B{B}"] = {"iter_proj_ms": t_ip, "refine_ms": t_rf, "refine_variants": var,
                     "iter_proj_GBps_65B": 65 * B * h * w / (t_ip * 1e-3) / 1e9,
                     "p_checksum": float(pn.double().sum()), "conv": int(cv.sum()),
