@@ -8,8 +8,9 @@ iterations run.  Throughput = 256 pairs x 10 iterations x ste
 Inputs are synthetic (m3s.synth, fixed seed) and resident in HBM before timing.
 
 N > 1 (torchrun, one process per GPU): the SAME graph is edge-sharded across ranks and the
-per-iteration compact Hessian is summed with an RCCL all-reduce inside the op -> strong
-scaling; value = total pair-iterations / max-over-ranks wall time.
+per-iteration f64 per-edge records are exchanged with an RCCL all-gather inside the op (every
+rank then assembles all edges in edge order: DESIGN.md §6) -> strong scaling; value = total
+pair-iterations / max-over-ranks wall time.
 
 Extra fields: ``roofline`` for the dominant kernel (the per-iteration accumulate kernel,
 HBM-bound, timed with HIP events on its stream during the timed steps).  Its algorithmic bytes
@@ -111,7 +112,7 @@ def main():
     if os.environ.get("M3S_EXIT_MAPS"):
         _dump_maps_at_exit(os.environ["M3S_EXIT_MAPS"])
     # M3S_BENCH_COMM=host: a rehearsal of the N-rank flow on fewer GPUs (ranks may share one):
-    # gloo process group and the op's host-callback all-reduce instead of RCCL over xGMI
+    # gloo process group and the op's host-callback exchange instead of RCCL over xGMI
     rehearse = world > 1 and os.environ.get("M3S_BENCH_COMM", "rccl") == "host"
     if rehearse:
         local_rank = local_rank % max(torch.cuda.device_count(), 1)
@@ -184,8 +185,9 @@ def main():
             "H": g.H,
             "W": g.W,
             "gn_iters_per_step": iters,
-            "parallelism": f"edge-sharded x{world}" + ((" + host all-reduce (rehearsal: ranks share GPUs)"
-                                                         if rehearse else " + RCCL all-reduce") if world > 1 else ""),
+            "parallelism": f"edge-sharded x{world}" + ((" + host exchange (rehearsal: ranks share GPUs)"
+                                                         if rehearse else " + RCCL all-gather of the per-edge records")
+                                                        if world > 1 else ""),
         },
         "phase_ms_per_iter": {
             "accumulate": acc_ms,
@@ -349,7 +351,7 @@ def config_block(cfg, args, world, rank, rehearse, dev, comm):
         "directed_edges_this_rank": local,
         "n_ranks": world,
         "n_ranks_comm": comm_size(comm) if comm is not None else 1,
-        "comm": (("host all-reduce (rehearsal)" if rehearse else "RCCL") if world > 1 else None),
+        "comm": (("host exchange (rehearsal)" if rehearse else "RCCL") if world > 1 else None),
         "phase_ms_per_iter": {
             "accumulate": acc_ms,
             "reduce_compact_allreduce": r["ph"][1] / nph,

@@ -29,6 +29,7 @@
 #include "gn_kernels.h"
 #include "m3s_common.h"
 #include "m3s_comm.h"
+#include "sparse_plan.h"
 
 namespace m3s {
 
@@ -531,61 +532,14 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
 
 
 // ---------------------------------------------------------------------------------
-// Block-sparse elimination plan (gn_sparse.hip): rounds of independent low-degree poses,
-// then a dense core.  Built once per GN call (the pose graph is fixed across iterations).
+// Block-sparse elimination plan (sparse_plan.h builds it, gn_sparse.hip runs it): its round
+// policies and the upload.
 // ---------------------------------------------------------------------------------
-struct SpRound {
-    int node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount;
-};
-
-struct SparsePlan {
-    bool enabled = false;
-    bool fused = false;       // the whole solve in one gn_solve launch (else multi-launch)
-    bool fused_tail = false;  // the dense tail fits the in-register factorisation of gn_solve
-    bool hybrid = false;      // multi-launch rounds, then gn_solve's core + back-substitution
-    int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
-    std::vector<SpRound> rounds;
-    std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
-    // multi-launch rounds (sp_round_kernel), per contribution: (v, code_r, code_s) for block
-    // targets, (v, code_r, W id, owner node | -1) for RHS targets; code = block * 2 + transposed
-    std::vector<int> tc3, rc4;
-    std::vector<int> inl;  // multi-launch rounds: one kSpRec record per target (gn_kernels.h)
-    // device (one stream-ordered allocation per call)
-    char* dbuf = nullptr;
-    size_t o_dense = 0, o_linv = 0;  // the dense core (npad_tail + 64) x npad_tail and its tile inverses
-    // block-format system: b (npose x 7, padded to bpad doubles), then 49-f64 blocks
-    int bpad = 0;
-    size_t o_sys = 0, o_y = 0, o_L = 0, o_W = 0, o_xd = 0, o_Lg = 0, o_int = 0;
-    // the plan integers, one array: [nodes fptr fronts tail rounds | tmap] (nints_back: what the
-    // core + back-substitution launch stages in LDS; without tmap: a back-substitution-only launch)
-    // [tg tc rtg rc] (nints: the whole plan of the single-workgroup solve) [tc3 rc4] (multi-launch
-    // rounds only)
-    size_t i_nodes = 0, i_fptr = 0, i_fronts = 0, i_tg = 0, i_tc = 0, i_rtg = 0, i_rc = 0,
-           i_tail = 0, i_tmap = 0, i_rounds = 0, i_tc3 = 0, i_rc4 = 0, i_inl = 0, nints = 0, nints_back = 0;
-    template <typename T>
-    T* dptr(size_t off) const { return reinterpret_cast<T*>(dbuf + off); }
-    const int* iptr(size_t i) const { return reinterpret_cast<const int*>(dbuf + o_int) + i; }
-};
-
 int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
 }
 
-// Elimination-round policy.  fused (gn_solve, one workgroup): rounds stop once the rest fits
-// the in-register tail unless a round still removes >= kmin poses; a round's W blocks / y are
-// staged in LDS (capped), RHS contributions name the pose's slot in the round.  multi
-// (gn_sparse.hip): low-degree independent sets until fewer than rmin poses qualify, the rest
-// goes to the tiled dense Cholesky; RHS contributions name the pose.
-// mmd: multiple-minimum-degree candidates -- a round takes only poses of degree
-// <= max(2 d_min, d_min + 1) (d_min: the current minimum degree), which keeps the fill close to
-// a sequential minimum-degree ordering (cfg3: a 26-pose dense tail after 8 rounds, where taking
-// every independent pose of degree <= dcap leaves a 31-35-pose clique).
-struct RoundPolicy {
-    bool fused;
-    int dcap, rmin, rmax, tailcap, kmin;
-    bool mmd;
-};
 RoundPolicy fused_policy() {
     return {true, env_int("M3S_SPARSE_DCAP", 64), env_int("M3S_SPARSE_RMIN", 1),
             env_int("M3S_SPARSE_RMAX", 64),
@@ -606,226 +560,6 @@ RoundPolicy hybrid_policy() {
             env_int("M3S_HYB_RMAX", 64),
             std::min(kTailPoseMax, env_int("M3S_HYB_TAILCAP", kTailPoseMax)),
             env_int("M3S_HYB_KMIN", 4), env_int("M3S_HYB_MMD", 1) != 0};
-}
-
-void build_sparse_plan(const Plan& p, int npose, const RoundPolicy& pol, SparsePlan& sp) {
-    sp = SparsePlan();
-    {  // capacities from the pose graph's size: no reallocation while the lists grow
-        const size_t e = p.pairs.size() + (size_t)npose, big = 16 * e + 1024;
-        for (std::vector<int>* v : {&sp.tg, &sp.tc, &sp.tc3, &sp.rtg, &sp.rc, &sp.rc4, &sp.inl, &sp.fronts})
-            v->reserve(big);
-        sp.nodes.reserve(npose);
-        sp.fptr.reserve(npose + 1);
-    }
-    const int dcap = pol.dcap, rmin = pol.rmin, rmax = pol.rmax, tailcap = pol.tailcap, kmin = pol.kmin;
-    // adjacency as bitsets (one row of nw 64-bit words per pose), degrees, dense block ids
-    const int nw = (npose + 63) / 64;
-    std::vector<uint64_t> adj((size_t)npose * nw, 0);
-    std::vector<int> deg(npose, 0);
-    auto has = [&](int x, int y) { return (adj[(size_t)x * nw + (y >> 6)] >> (y & 63)) & 1; };
-    auto link = [&](int x, int y) {
-        uint64_t& w = adj[(size_t)x * nw + (y >> 6)];
-        const uint64_t m = 1ull << (y & 63);
-        if (!(w & m)) {
-            w |= m;
-            deg[x]++;
-        }
-    };
-    auto unlink = [&](int x, int y) {
-        uint64_t& w = adj[(size_t)x * nw + (y >> 6)];
-        const uint64_t m = 1ull << (y & 63);
-        if (w & m) {
-            w &= ~m;
-            deg[x]--;
-        }
-    };
-    auto neighbours = [&](int x, std::vector<int>& out) {  // ascending
-        out.clear();
-        for (int k = 0; k < nw; k++)
-            for (uint64_t w = adj[(size_t)x * nw + k]; w; w &= w - 1) out.push_back(64 * k + __builtin_ctzll(w));
-    };
-    std::vector<int> bidm((size_t)npose * npose, -1);  // upper triangle (x < y) used
-    for (size_t k = 0; k < p.pairs.size(); k++) {
-        const int a = p.pairs[k].first, b = p.pairs[k].second;
-        link(a, b);
-        link(b, a);
-        bidm[(size_t)a * npose + b] = npose + (int)k;
-    }
-    sp.nblocks = p.nblk;
-    auto block_of = [&](int x, int y) -> int {
-        if (x == y) return x;
-        int& id = bidm[(size_t)std::min(x, y) * npose + std::max(x, y)];
-        if (id < 0) id = sp.nblocks++;
-        return id;
-    };
-    std::vector<char> alive(npose, 1), blocked(npose, 0);
-    int nalive = npose;
-    sp.fptr.assign(1, 0);
-    std::vector<int> cand, chosen, nb, codes;
-    std::vector<std::vector<int>> F;
-    struct TC { int r, s, q, wx, wy, v, cr, cs; };
-    struct RC { int r, q, w, v, cr, owner; };
-    std::vector<TC> tcs;
-    std::vector<RC> rcs;
-    for (int round = 0; round < rmax && nalive > 0; round++) {
-        // a remaining clique is the dense tail (eliminating it pose by pose gains nothing)
-        bool clique = true;
-        for (int v = 0; v < npose && clique; v++)
-            if (alive[v] && deg[v] != nalive - 1) clique = false;
-        if (clique && nalive > 1) break;
-        cand.clear();
-        int dlim = dcap;
-        if (pol.mmd) {
-            int dmin = npose;
-            for (int v = 0; v < npose; v++)
-                if (alive[v]) dmin = std::min(dmin, deg[v]);
-            dlim = std::min(dcap, std::max(2 * dmin, dmin + 1));
-        }
-        for (int v = 0; v < npose; v++)
-            if (alive[v] && deg[v] <= dlim) cand.push_back(v);
-        std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return deg[a] < deg[b]; });
-        std::fill(blocked.begin(), blocked.end(), 0);
-        chosen.clear();
-        for (int v : cand) {
-            if (blocked[v]) continue;
-            chosen.push_back(v);
-            blocked[v] = 1;
-            for (int k = 0; k < nw; k++)
-                for (uint64_t w = adj[(size_t)v * nw + k]; w; w &= w - 1) blocked[64 * k + __builtin_ctzll(w)] = 1;
-        }
-        // a round's W blocks and y vectors are staged in LDS: cap its poses (the rest stay
-        // for the next round; any subset of an independent set is independent)
-        if (pol.fused) {
-            size_t k = 0, wsum = 0;
-            while (k < chosen.size() && (int)k < kSolveRoundPoses &&
-                   (wsum + deg[chosen[k]]) * 49 <= (size_t)kSolveWStage) {
-                wsum += deg[chosen[k]];
-                k++;
-            }
-            chosen.resize(k);
-        }
-        if ((int)chosen.size() < rmin && (int)chosen.size() != nalive) break;
-        // once the rest fits the in-register dense tail, a round must eliminate enough poses
-        // to beat the per-pose cost of the tail steps
-        if (nalive <= tailcap && (int)chosen.size() < kmin) break;
-        std::sort(chosen.begin(), chosen.end());
-        SpRound R;
-        R.node_begin = (int)sp.nodes.size();
-        R.nnodes = (int)chosen.size();
-        R.wbeg = sp.nW;
-        F.resize(chosen.size());
-        tcs.clear();
-        rcs.clear();
-        for (size_t q = 0; q < chosen.size(); q++) {
-            const int v = chosen[q];
-            neighbours(v, F[q]);
-            const int node = (int)sp.nodes.size();
-            sp.nodes.push_back(v);
-            const int w0 = sp.nW;
-            codes.clear();
-            for (int r : F[q]) {
-                const int blk = block_of(r, v);
-                sp.fronts.insert(sp.fronts.end(), {r, blk, r > v ? 1 : 0, sp.nW++});
-                codes.push_back(2 * blk + (r > v ? 1 : 0));
-            }
-            sp.fptr.push_back((int)sp.fronts.size() / 4);
-            for (size_t i = 0; i < F[q].size(); i++) {
-                for (size_t j = i; j < F[q].size(); j++)
-                    tcs.push_back({F[q][i], F[q][j], (int)q, w0 + (int)i, w0 + (int)j, v, codes[i],
-                                   codes[j]});
-                rcs.push_back({F[q][i], pol.fused ? (int)q : v, w0 + (int)i, v, codes[i],
-                               i == 0 ? node : -1});
-            }
-            // multi-launch rounds: a pose without fronts (its neighbours pinned or eliminated)
-            // still needs L_v and y_v for the back-substitution -- a contribution to no target
-            if (!pol.fused && F[q].empty()) rcs.push_back({-1, v, -1, v, 2 * v, node});
-        }
-        // targets in (r, s) order, contributions in pose order (deterministic sums)
-        std::sort(tcs.begin(), tcs.end(), [](const TC& x, const TC& y) {
-            return x.r != y.r ? x.r < y.r : x.s != y.s ? x.s < y.s : x.q < y.q;
-        });
-        std::stable_sort(rcs.begin(), rcs.end(), [](const RC& x, const RC& y) { return x.r < y.r; });
-        R.tbeg = (int)sp.tg.size() / 3;
-        for (size_t k = 0; k < tcs.size();) {
-            size_t e = k;
-            const int c0 = (int)sp.tc.size() / 2;
-            while (e < tcs.size() && tcs[e].r == tcs[k].r && tcs[e].s == tcs[k].s) {
-                sp.tc.insert(sp.tc.end(), {tcs[e].wx, tcs[e].wy});
-                if (!pol.fused) sp.tc3.insert(sp.tc3.end(), {tcs[e].v, tcs[e].cr, tcs[e].cs});
-                e++;
-            }
-            sp.tg.insert(sp.tg.end(), {block_of(tcs[k].r, tcs[k].s), c0, (int)sp.tc.size() / 2});
-            k = e;
-        }
-        R.nbt = (int)sp.tg.size() / 3 - R.tbeg;
-        R.rbeg = (int)sp.rtg.size() / 3;
-        for (size_t k = 0; k < rcs.size();) {
-            size_t e = k;
-            const int c0 = (int)sp.rc.size() / 2;
-            while (e < rcs.size() && rcs[e].r == rcs[k].r) {
-                sp.rc.insert(sp.rc.end(), {rcs[e].w, rcs[e].q});  // (W id, node slot | pose)
-                if (!pol.fused)
-                    sp.rc4.insert(sp.rc4.end(), {rcs[e].v, rcs[e].cr, rcs[e].w, rcs[e].owner});
-                e++;
-            }
-            sp.rtg.insert(sp.rtg.end(), {rcs[k].r, c0, (int)sp.rc.size() / 2});
-            k = e;
-        }
-        R.nrt = (int)sp.rtg.size() / 3 - R.rbeg;
-        if (!pol.fused) {
-            // the round's target records (block targets, then RHS targets), the first kSpInline
-            // contributions inline
-            auto record = [&](const int* T_, const std::vector<int>& lst, int w) {
-                const size_t o = sp.inl.size();
-                sp.inl.resize(o + kSpRec, 0);
-                sp.inl[o] = T_[0];
-                sp.inl[o + 1] = T_[1];
-                sp.inl[o + 2] = T_[2];
-                for (int k = 0; k < kSpInline && T_[1] + k < T_[2]; k++)
-                    for (int f = 0; f < w; f++) sp.inl[o + 4 + 4 * k + f] = lst[(size_t)w * (T_[1] + k) + f];
-            };
-            for (int t = 0; t < R.nbt; t++) record(&sp.tg[3 * (R.tbeg + t)], sp.tc3, 3);
-            for (int t = 0; t < R.nrt; t++) record(&sp.rtg[3 * (R.rbeg + t)], sp.rc4, 4);
-        }
-        R.wcount = sp.nW - R.wbeg;
-        sp.rounds.push_back(R);
-        // eliminate: drop the poses, connect each front into a clique (fill)
-        for (size_t q = 0; q < chosen.size(); q++) {
-            const int v = chosen[q];
-            for (int r : F[q]) unlink(r, v);
-            for (int r : F[q])
-                for (int s2 : F[q])
-                    if (r != s2) link(r, s2);
-            for (int r : F[q]) unlink(v, r);
-            alive[v] = 0;
-            nalive--;
-        }
-    }
-    (void)has;
-    for (int v = 0; v < npose; v++)
-        if (alive[v]) sp.tail.push_back(v);
-    sp.ntail = (int)sp.tail.size();
-    sp.zero_blk = sp.nblocks++;  // an all-zero block (zeroed with the fill blocks)
-    sp.npad_tail = sp.ntail > 0 ? (int)align_up((size_t)sp.ntail * 7, kCholTile) : 0;
-    sp.tmap.assign((size_t)sp.ntail * sp.ntail, -1);
-    for (int i = 0; i < sp.ntail; i++)
-        for (int j = 0; j < sp.ntail; j++) {
-            const int x = sp.tail[i], y = sp.tail[j];
-            int code = -1;
-            if (x == y) {
-                code = 2 * x;
-            } else {
-                const int id = bidm[(size_t)std::min(x, y) * npose + std::max(x, y)];
-                if (id >= 0) code = 2 * id + (x > y ? 1 : 0);
-            }
-            sp.tmap[(size_t)i * sp.ntail + j] = code;
-        }
-    sp.fused_tail = sp.ntail * 7 <= kTailMax;
-    sp.fused = pol.fused && sp.fused_tail;
-    sp.nints_back = sp.nodes.size() + sp.fptr.size() + sp.fronts.size() + sp.tail.size() +
-                    sp.tmap.size() + 8 * sp.rounds.size();
-    sp.nints = sp.nints_back + sp.tg.size() + sp.tc.size() + sp.rtg.size() + sp.rc.size();
-    sp.enabled = true;
 }
 
 int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
@@ -932,6 +666,15 @@ int validate(const m3s_gn_args& a) {
     return M3S_OK;
 }
 
+Plan& tls_plan() {
+    static thread_local Plan p;
+    return p;
+}
+SparsePlan& tls_sparse_plan() {
+    static thread_local SparsePlan sp;
+    return sp;
+}
+
 struct Ctx {
     bool need_slotmap = false;  // dense solver / debug system: upload the slot table
     bool packed = false;  // per-call packed stream (gn_pack_kernel) feeds the accumulate
@@ -943,8 +686,10 @@ struct Ctx {
     bool first_pack = false;
     RefParams R;
     Layout L;
-    Plan plan;
-    SparsePlan sp;
+    // the host plans, per thread across calls: their lists keep their capacity (fresh
+    // allocations of this size cost a page fault per 4 KiB on every call; sparse_plan.h)
+    Plan& plan = tls_plan();
+    SparsePlan& sp = tls_sparse_plan();
     AccParams P;
     EdgeSrc es{};
     bool vec;
@@ -980,12 +725,13 @@ struct Ctx {
         M3S_HIP_CHECK(hipMemsetAsync(chol_ready_ptr(dyn_at<double>(o_linv), npad), 0, chol_ready_bytes(npad), st));
         return M3S_OK;
     }
-    Ctx() = default;
+    Ctx() { sp.reset(); }  // (no earlier call's plan survives into this one)
     Ctx(const Ctx&) = delete;
     Ctx& operator=(const Ctx&) = delete;
     // every return path of a call releases its per-call buffers (stream-ordered)
     ~Ctx() {
         if (sp.dbuf) (void)hipFreeAsync(sp.dbuf, st);
+        sp.dbuf = nullptr;
         if (dyn) (void)hipFreeAsync(dyn, st);
         if (eall) (void)hipFreeAsync(eall, st);
     }
@@ -1524,11 +1270,16 @@ int run(const m3s_gn_args& a) {
         // short, e.g. edge-sharded over several GPUs) is skipped.
         bool planned = false;
         if (choice == 0 && hybrid_on) {
-            build_sparse_plan(c.plan, npose, hybrid_policy(), c.sp);
-            if ((int)c.sp.rounds.size() > max_fused_rounds) {
-                const bool hyb = c.sp.fused_tail && npose <= solve_max_poses() &&
-                                 solve_lds_bytes((int)c.sp.nints_back) <= (size_t)kSolveMaxLds;
-                if (!hyb) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
+            // the hybrid's rounds and core decided symbolically first (no lists): on a graph
+            // whose core does not fit the in-register factorisation (cfg4) building the hybrid's
+            // lists only to replace them by the multi plan cost ~1.5 ms of host time per call,
+            // exposed once the edges are sharded (the first accumulate no longer covers it)
+            static thread_local SparsePlan probe;
+            build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, hybrid_policy(), probe, true);
+            if ((int)probe.rounds.size() > max_fused_rounds) {
+                const bool hyb = probe.fused_tail && npose <= solve_max_poses() &&
+                                 solve_lds_bytes((int)probe.nints_back) <= (size_t)kSolveMaxLds;
+                build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, hyb ? hybrid_policy() : multi_policy(), c.sp);
                 c.sp.hybrid = hyb;
                 planned = true;
             }
@@ -1536,7 +1287,7 @@ int run(const m3s_gn_args& a) {
         t2a = now();
         bool fused_ok = false, meta_fits = false;
         if (!planned) {
-            build_sparse_plan(c.plan, npose, fused_policy(), c.sp);
+            build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, fused_policy(), c.sp);
             meta_fits = solve_lds_bytes((int)c.sp.nints) <= (size_t)kSolveMaxLds;
             fused_ok = c.sp.fused && meta_fits && npose <= solve_max_poses() &&
                        (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <= max_fused_rounds));
@@ -1548,11 +1299,11 @@ int run(const m3s_gn_args& a) {
             // M3S_SOLVER=3 / default: multi-launch rounds + the in-register core when it fits
             bool hyb = false;
             if (choice == 3 || (choice == 0 && hybrid_on)) {
-                build_sparse_plan(c.plan, npose, hybrid_policy(), c.sp);
+                build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, hybrid_policy(), c.sp);
                 hyb = c.sp.fused_tail && npose <= solve_max_poses() &&
                       solve_lds_bytes((int)c.sp.nints_back) <= (size_t)kSolveMaxLds;
             }
-            if (!hyb) build_sparse_plan(c.plan, npose, multi_policy(), c.sp);
+            if (!hyb) build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, multi_policy(), c.sp);
             c.sp.hybrid = hyb;
         }
         t2 = now();

@@ -3,7 +3,7 @@
 * ``m3s.matching`` / ``m3s.image``  -- ``mast3r_slam/matching.py`` + ``image.py`` (row a3)
 * ``m3s.geometry``                  -- ``constrain_points_to_ray`` / ``backproject``
 * ``m3s.global_opt``                -- ``FactorGraph.solve_GN_rays/calib`` flow (row a13)
-* ``m3s.dist``                      -- edge-sharded multi-GPU GN (RCCL all-reduce)
+* ``m3s.dist``                      -- edge-sharded multi-GPU GN (RCCL all-gather of per-edge records)
 * ``m3s.synth``                     -- deterministic synthetic 512x384 workloads
 * ``m3s.config``                    -- the hot-path parameters of config/base.yaml
 """
