@@ -252,6 +252,22 @@ int m3s_gn_build_system(const m3s_gn_args* args, double* H_host, double* b_host)
 int m3s_gn_edge_hessians(const m3s_gn_args* args, float* Hs_host, float* gs_host);
 
 /*
+ * Diagnostic (host only, no GPU): the elimination plan m3s_gauss_newton would build for this
+ * pose graph -- the step the reference leaves to Eigen's SimplicialLLT symbolic analysis on every
+ * solve (gn_kernels.cu:132-153).  ii, jj [E] host i64 global keyframe ids (as the op's), N
+ * poses (the first pinned).  info[8]: [0] solver (0 single-workgroup fused, 1 hybrid, 2
+ * multi-launch, -1 nothing to solve), [1] elimination rounds, [2] poses eliminated by the
+ * rounds, [3] poses in the dense core, [4] the core's padded unknowns, [5] pose pairs (graph
+ * blocks off the diagonal), [6] plan integers uploaded per call, [7] 1 if the core fits the
+ * dense solve limit.  order (optional, N-1 ints): the poses (0-based rows after the pinned one)
+ * round by round, each round ascending, then the core's.  round_ptr (optional, round_cap ints):
+ * where each round starts in order, then the core's start -- written when round_cap >=
+ * rounds + 1.  Environment knobs as for the op.
+ */
+int m3s_gn_plan_info(const int64_t* ii, const int64_t* jj, int64_t E, int64_t N, int32_t* info,
+                     int32_t* order, int32_t* round_ptr, int32_t round_cap);
+
+/*
  * Phase timing (bench.py): between m3s_prof_begin() and m3s_prof_end() every GN
  * iteration records HIP events on its stream.  out[0] = accumulate kernel ms,
  * out[1] = edge reduce + compact (+ all-reduce) ms, out[2] = solve ms, out[3] = retract

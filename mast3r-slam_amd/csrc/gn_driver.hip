@@ -358,6 +358,43 @@ void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_l
 
 int gn_order(const m3s_gn_args& a);
 
+// The pose graph's blocks from the edge lists (host copies): keyframe ids -> rows by
+// unique(cat(ii, jj)) sorted + searchsorted (gn_kernels.cu:161-170), the first row pinned
+// (num_fix = 1); diagonal blocks first (slot p <-> pose p), then the unordered pose pairs in order
+// of first appearance over ALL edges; slotmap is the dense (npose x npose) slot table.
+int plan_pairs(const int64_t* hii, const int64_t* hjj, int64_t E, int64_t N, Plan& plan, std::vector<int>& iopt,
+               std::vector<int>& jopt) {
+    std::vector<int64_t> u(hii, hii + E);
+    u.insert(u.end(), hjj, hjj + E);
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    auto row_of = [&](int64_t id) {
+        return (int)(std::lower_bound(u.begin(), u.end(), id) - u.begin());
+    };
+    M3S_REQUIRE((int64_t)u.size() <= N,
+                "gauss_newton: %lld unique keyframe ids in ii/jj but only %lld poses in Twc/Xs",
+                (long long)u.size(), (long long)N);
+    const int npose = (int)(N - 1);
+    iopt.resize(E);
+    jopt.resize(E);
+    for (int64_t e = 0; e < E; e++) {
+        iopt[e] = row_of(hii[e]) - 1;  // pin = num_fix = 1
+        jopt[e] = row_of(hjj[e]) - 1;
+    }
+    plan.slotmap.assign((size_t)std::max(npose, 0) * std::max(npose, 0), -1);
+    for (int q = 0; q < npose; q++) plan.slotmap[(size_t)q * npose + q] = q;
+    plan.nblk = npose;
+    plan.pairs.clear();
+    for (int64_t e = 0; e < E; e++) {
+        const int i = iopt[e], j = jopt[e];
+        if (i >= 0 && j >= 0 && i != j && plan.slotmap[(size_t)i * npose + j] < 0) {
+            plan.slotmap[(size_t)i * npose + j] = plan.slotmap[(size_t)j * npose + i] = plan.nblk++;
+            plan.pairs.push_back(std::make_pair(std::min(i, j), std::max(i, j)));
+        }
+    }
+    return M3S_OK;
+}
+
 int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     const int64_t E = a.E_total;
     // sharded call: gather the edge records (M3S_GN_GATHER=0: all-reduce the assembled system)
@@ -433,38 +470,10 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
         plan.K[3] = Kh[5];  // cy = K[1][2]
     }
 
-    // unique(cat(ii, jj)) sorted; searchsorted (gn_kernels.cu:161-170)
-    std::vector<int64_t> u(hii, hii + E);
-    u.insert(u.end(), hjj, hjj + E);
-    std::sort(u.begin(), u.end());
-    u.erase(std::unique(u.begin(), u.end()), u.end());
-    auto row_of = [&](int64_t id) {
-        return (int)(std::lower_bound(u.begin(), u.end(), id) - u.begin());
-    };
-    M3S_REQUIRE((int64_t)u.size() <= a.N,
-                "gauss_newton: %lld unique keyframe ids in ii/jj but only %lld poses in Twc/Xs",
-                (long long)u.size(), (long long)a.N);
-
     const int npose = (int)(a.N - 1);
-    std::vector<int> iopt(E), jopt(E);
-    for (int64_t e = 0; e < E; e++) {
-        iopt[e] = row_of(hii[e]) - 1;  // pin = num_fix = 1
-        jopt[e] = row_of(hjj[e]) - 1;
-    }
-
-    // block slots: diagonal blocks first (slot p <-> pose p), then unordered pairs in order of
-    // first appearance over ALL edges; slotmap is the dense (npose x npose) slot table
-    plan.slotmap.assign((size_t)std::max(npose, 0) * std::max(npose, 0), -1);
-    for (int q = 0; q < npose; q++) plan.slotmap[(size_t)q * npose + q] = q;
-    plan.nblk = npose;
-    plan.pairs.clear();
-    for (int64_t e = 0; e < E; e++) {
-        const int i = iopt[e], j = jopt[e];
-        if (i >= 0 && j >= 0 && i != j && plan.slotmap[(size_t)i * npose + j] < 0) {
-            plan.slotmap[(size_t)i * npose + j] = plan.slotmap[(size_t)j * npose + i] = plan.nblk++;
-            plan.pairs.push_back(std::make_pair(std::min(i, j), std::max(i, j)));
-        }
-    }
+    std::vector<int> iopt, jopt;
+    int rc = plan_pairs(hii, hjj, E, a.N, plan, iopt, jopt);
+    if (rc) return rc;
     auto slot = [&](int r, int c) { return plan.slotmap[(size_t)r * npose + c]; };
 
     // contributions of the LOCAL edges as CSR lists (update_lhs order per edge:
@@ -1225,6 +1234,90 @@ int take_deferred_timeout(const char* which) {
     return M3S_OK;
 }
 
+// The elimination plan the solve runs for this pose graph (M3S_SOLVER pins
+// one).  Default: the hybrid (multi-launch rounds + gn_solve's back-substitution) when its core
+// fits, else the multi-launch plan; the single-workgroup solve when the plan needs few rounds.
+void choose_sparse_plan(const Plan& plan, int npose, SparsePlan& sp) {
+    // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
+    // single-workgroup solve when its plan needs few rounds, else multi-launch
+    const int choice = env_int("M3S_SOLVER", 0);
+    const int max_fused_rounds = env_int("M3S_FUSED_MAX_ROUNDS", 3);
+    const bool hybrid_on = env_int("M3S_HYBRID", 1) != 0;
+    // Default choice: the hybrid plan first.  The fused policy is the hybrid's plus a cap on
+    // the poses per round (LDS staging), so it never needs fewer rounds; when the hybrid
+    // plan already needs more than max_fused_rounds, the fused solve would be rejected and
+    // building its plan (~0.23 ms of host time on cfg3, exposed once the per-call pack is
+    // short, e.g. edge-sharded over several GPUs) is skipped.
+    bool planned = false;
+    if (choice == 0 && hybrid_on) {
+        // the hybrid's rounds and core decided symbolically first (no lists): on a graph
+        // whose core does not fit the in-register factorisation (cfg4) building the hybrid's
+        // lists only to replace them by the multi plan cost ~1.5 ms of host time per call,
+        // exposed once the edges are sharded (the first accumulate no longer covers it)
+        static thread_local SparsePlan probe;
+        build_sparse_plan(plan.pairs, plan.nblk, npose, hybrid_policy(), probe, true);
+        if ((int)probe.rounds.size() > max_fused_rounds) {
+            const bool hyb = probe.fused_tail && npose <= solve_max_poses() &&
+                             solve_lds_bytes((int)probe.nints_back) <= (size_t)kSolveMaxLds;
+            build_sparse_plan(plan.pairs, plan.nblk, npose, hyb ? hybrid_policy() : multi_policy(), sp);
+            sp.hybrid = hyb;
+            planned = true;
+        }
+    }
+    bool fused_ok = false, meta_fits = false;
+    if (!planned) {
+        build_sparse_plan(plan.pairs, plan.nblk, npose, fused_policy(), sp);
+        meta_fits = solve_lds_bytes((int)sp.nints) <= (size_t)kSolveMaxLds;
+        fused_ok = sp.fused && meta_fits && npose <= solve_max_poses() &&
+                   (choice == 1 || (choice == 0 && (int)sp.rounds.size() <= max_fused_rounds));
+    }
+    if (env_int("M3S_SOLVE_DEBUG", 0) && !fused_ok && !planned)
+        fprintf(stderr, "fused solve rejected: fused_tail %d (ntail %d) rounds %zu nints %zu meta_fits %d\n",
+                (int)sp.fused, sp.ntail, sp.rounds.size(), sp.nints, (int)meta_fits);
+    if (!fused_ok && !planned) {
+        // M3S_SOLVER=3 / default: multi-launch rounds + the in-register core when it fits
+        bool hyb = false;
+        if (choice == 3 || (choice == 0 && hybrid_on)) {
+            build_sparse_plan(plan.pairs, plan.nblk, npose, hybrid_policy(), sp);
+            hyb = sp.fused_tail && npose <= solve_max_poses() &&
+                  solve_lds_bytes((int)sp.nints_back) <= (size_t)kSolveMaxLds;
+        }
+        if (!hyb) build_sparse_plan(plan.pairs, plan.nblk, npose, multi_policy(), sp);
+        sp.hybrid = hyb;
+    }
+}
+
+// m3s_gn_plan_info (include/m3s_backend.h): the plan choose_sparse_plan makes, from host lists
+int plan_info(const int64_t* ii, const int64_t* jj, int64_t E, int64_t N, int32_t* info, int32_t* order,
+              int32_t* round_ptr, int32_t round_cap) {
+    M3S_REQUIRE(info != nullptr && N >= 1 && E >= 0 && (E == 0 || (ii != nullptr && jj != nullptr)),
+                "gn_plan_info: bad arguments");
+    Plan plan;
+    std::vector<int> iopt, jopt;
+    int rc = plan_pairs(ii, jj, E, N, plan, iopt, jopt);
+    if (rc) return rc;
+    const int npose = (int)(N - 1);
+    SparsePlan sp;
+    if (npose > 0) choose_sparse_plan(plan, npose, sp);
+    info[0] = npose <= 0 ? -1 : sp.fused ? 0 : sp.hybrid ? 1 : 2;
+    info[1] = (int32_t)sp.rounds.size();
+    info[2] = (int32_t)sp.nodes.size();
+    info[3] = sp.ntail;
+    info[4] = sp.npad_tail;
+    info[5] = (int32_t)plan.pairs.size();
+    info[6] = (int32_t)sp.nints;
+    info[7] = sp.npad_tail <= kMaxNpad ? 1 : 0;
+    if (order) {
+        std::copy(sp.nodes.begin(), sp.nodes.end(), order);
+        std::copy(sp.tail.begin(), sp.tail.end(), order + sp.nodes.size());
+    }
+    if (round_ptr && round_cap >= (int32_t)sp.rounds.size() + 1) {
+        for (size_t k = 0; k < sp.rounds.size(); k++) round_ptr[k] = sp.rounds[k].node_begin;
+        round_ptr[sp.rounds.size()] = (int32_t)sp.nodes.size();
+    }
+    return M3S_OK;
+}
+
 int run(const m3s_gn_args& a) {
     // M3S_PROF_HOST: host-side phase times of the call (stderr)
     static const bool prof_host = env_int("M3S_PROF_HOST", 0) != 0;
@@ -1247,7 +1340,7 @@ int run(const m3s_gn_args& a) {
     if (npose <= 0) return M3S_OK;  // nothing to optimise (all poses pinned)
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
-    std::chrono::steady_clock::time_point t2 = t1, t2a = t1, t3 = t1;
+    std::chrono::steady_clock::time_point t2 = t1, t3 = t1;
     // M3S_EARLY_ACC (default 1): iteration 0's accumulate is enqueued before the host builds the
     // elimination plan (the GPU works while the host plans; the per-call pack alone no longer
     // covers the planning once the edges are sharded over several GPUs)
@@ -1258,54 +1351,7 @@ int run(const m3s_gn_args& a) {
         c.acc_enqueued = true;
     }
     if (env_int("M3S_SOLVER_DENSE", 0) == 0 || c.ref_order) {
-        // M3S_SOLVER: 1 = single-workgroup (gn_solve), 2 = multi-launch, 0 (default) = the
-        // single-workgroup solve when its plan needs few rounds, else multi-launch
-        const int choice = env_int("M3S_SOLVER", 0);
-        const int max_fused_rounds = env_int("M3S_FUSED_MAX_ROUNDS", 3);
-        const bool hybrid_on = env_int("M3S_HYBRID", 1) != 0;
-        // Default choice: the hybrid plan first.  The fused policy is the hybrid's plus a cap on
-        // the poses per round (LDS staging), so it never needs fewer rounds; when the hybrid
-        // plan already needs more than max_fused_rounds, the fused solve would be rejected and
-        // building its plan (~0.23 ms of host time on cfg3, exposed once the per-call pack is
-        // short, e.g. edge-sharded over several GPUs) is skipped.
-        bool planned = false;
-        if (choice == 0 && hybrid_on) {
-            // the hybrid's rounds and core decided symbolically first (no lists): on a graph
-            // whose core does not fit the in-register factorisation (cfg4) building the hybrid's
-            // lists only to replace them by the multi plan cost ~1.5 ms of host time per call,
-            // exposed once the edges are sharded (the first accumulate no longer covers it)
-            static thread_local SparsePlan probe;
-            build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, hybrid_policy(), probe, true);
-            if ((int)probe.rounds.size() > max_fused_rounds) {
-                const bool hyb = probe.fused_tail && npose <= solve_max_poses() &&
-                                 solve_lds_bytes((int)probe.nints_back) <= (size_t)kSolveMaxLds;
-                build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, hyb ? hybrid_policy() : multi_policy(), c.sp);
-                c.sp.hybrid = hyb;
-                planned = true;
-            }
-        }
-        t2a = now();
-        bool fused_ok = false, meta_fits = false;
-        if (!planned) {
-            build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, fused_policy(), c.sp);
-            meta_fits = solve_lds_bytes((int)c.sp.nints) <= (size_t)kSolveMaxLds;
-            fused_ok = c.sp.fused && meta_fits && npose <= solve_max_poses() &&
-                       (choice == 1 || (choice == 0 && (int)c.sp.rounds.size() <= max_fused_rounds));
-        }
-        if (env_int("M3S_SOLVE_DEBUG", 0) && !fused_ok && !planned)
-            fprintf(stderr, "fused solve rejected: fused_tail %d (ntail %d) rounds %zu nints %zu meta_fits %d\n",
-                    (int)c.sp.fused, c.sp.ntail, c.sp.rounds.size(), c.sp.nints, (int)meta_fits);
-        if (!fused_ok && !planned) {
-            // M3S_SOLVER=3 / default: multi-launch rounds + the in-register core when it fits
-            bool hyb = false;
-            if (choice == 3 || (choice == 0 && hybrid_on)) {
-                build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, hybrid_policy(), c.sp);
-                hyb = c.sp.fused_tail && npose <= solve_max_poses() &&
-                      solve_lds_bytes((int)c.sp.nints_back) <= (size_t)kSolveMaxLds;
-            }
-            if (!hyb) build_sparse_plan(c.plan.pairs, c.plan.nblk, npose, multi_policy(), c.sp);
-            c.sp.hybrid = hyb;
-        }
+        choose_sparse_plan(c.plan, npose, c.sp);
         t2 = now();
         M3S_REQUIRE(c.sp.npad_tail <= kMaxNpad,
                     "gauss_newton: the dense core of the elimination (%d unknowns) exceeds the "
@@ -1315,8 +1361,8 @@ int run(const m3s_gn_args& a) {
         t3 = now();
     }
     if (prof_host)
-        fprintf(stderr, "gn host: setup %.0f us, first plan %.0f us, second plan %.0f us, upload %.0f us\n",
-                us(t0, t1), us(t1, t2a), us(t2a, t2), us(t2, t3));
+        fprintf(stderr, "gn host: setup %.0f us, plan %.0f us, upload %.0f us\n", us(t0, t1), us(t1, t2),
+                us(t2, t3));
     for (int itr = 0; itr < a.max_iter; itr++) {
         if (!c.acc_enqueued) g_prof.mark(c.st);  // (iteration 0's mark preceded its early accumulate)
         rc = enqueue_system(a, c);
@@ -1432,6 +1478,11 @@ extern "C" size_t m3s_gn_workspace_bytes(int mode, int64_t N, int64_t HW, int64_
                                          int64_t E_local) {
     if (N < 1 || HW < 1 || E_total < 0 || E_local < 0) return 0;
     return make_layout(mode, N, HW, E_total, E_local).total;
+}
+
+extern "C" int m3s_gn_plan_info(const int64_t* ii, const int64_t* jj, int64_t E, int64_t N, int32_t* info,
+                                int32_t* order, int32_t* round_ptr, int32_t round_cap) {
+    return m3s::plan_info(ii, jj, E, N, info, order, round_ptr, round_cap);
 }
 
 extern "C" int m3s_gauss_newton(const m3s_gn_args* args) {

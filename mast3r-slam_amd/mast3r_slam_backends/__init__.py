@@ -28,6 +28,7 @@ __all__ = [
     "CholeskyError",
     "pointmap_update",
     "edge_confidence",
+    "gn_plan_info",
     "library_path",
     "set_gn_order",
     "set_gn_contract",
@@ -82,6 +83,7 @@ def _contract(c):
     return CONTRACT[c]
 lib.m3s_gn_workspace_bytes.restype = ctypes.c_size_t
 lib.m3s_gn_workspace_bytes.argtypes = [_i, _c_int64, _c_int64, _c_int64, _c_int64]
+lib.m3s_gn_plan_info.argtypes = [_vp, _vp, _c_int64, _c_int64, _vp, _vp, _vp, ctypes.c_int32]
 
 
 class GNArgs(ctypes.Structure):
@@ -218,6 +220,34 @@ def _raise(rc, what):
     if rc != 0:
         msg = lib.m3s_last_error().decode(errors="replace")
         raise RuntimeError(f"{what}: {msg} (code {rc})")
+
+
+def gn_plan_info(ii, jj, N):
+    """The elimination plan gauss_newton_* builds for a pose graph (host only, no GPU;
+    include/m3s_backend.h m3s_gn_plan_info).  ii, jj: the op's global keyframe ids (any int
+    sequence / CPU tensor), N poses.  Returns a dict: solver ("fused" | "hybrid" | "multi" |
+    None), rounds, eliminated, core_poses, core_unknowns_padded, pairs, plan_ints, core_fits,
+    order (the poses round by round, then the core's) and round_ptr (each round's start in
+    order, then the core's)."""
+    import numpy as np
+
+    ii = np.ascontiguousarray(np.asarray(ii, dtype=np.int64))
+    jj = np.ascontiguousarray(np.asarray(jj, dtype=np.int64))
+    if ii.shape != jj.shape or ii.ndim != 1:
+        raise ValueError("ii and jj must be 1-D of equal length")
+    info = np.zeros(8, dtype=np.int32)
+    npose = max(int(N) - 1, 0)
+    order = np.zeros(max(npose, 1), dtype=np.int32)
+    cap = npose + 2
+    rptr = np.zeros(cap, dtype=np.int32)
+    rc = lib.m3s_gn_plan_info(ii.ctypes.data, jj.ctypes.data, ii.shape[0], int(N), info.ctypes.data,
+                              order.ctypes.data, rptr.ctypes.data, cap)
+    _raise(rc, "gn_plan_info")
+    rounds = int(info[1])
+    return {"solver": {0: "fused", 1: "hybrid", 2: "multi"}.get(int(info[0])), "rounds": rounds,
+            "eliminated": int(info[2]), "core_poses": int(info[3]), "core_unknowns_padded": int(info[4]),
+            "pairs": int(info[5]), "plan_ints": int(info[6]), "core_fits": bool(info[7]),
+            "order": order[:npose].tolist(), "round_ptr": rptr[:rounds + 1].tolist()}
 
 
 def _stream(device):
