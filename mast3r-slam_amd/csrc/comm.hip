@@ -88,6 +88,11 @@ Comm* as_comm(void* h) {
 }  // namespace
 
 namespace m3s {
+bool comm_is_async(void* comm) {
+    const Comm* c = as_comm(comm);
+    return c != nullptr && c->kind == kCommRccl;
+}
+
 int comm_allreduce_sum_f64(void* comm, double* buf, size_t count, hipStream_t stream) {
     Comm* c = as_comm(comm);
     if (!c) {

@@ -160,6 +160,19 @@ struct Staging {
             return launch_stage_copy(st, dst, dev + (h - buf), bytes);
         return hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st);
     }
+    // D2H of bytes from src (device) into [h, h + bytes) (inside buf), stream-ordered: by the
+    // same copy kernel writing the pinned buffer through its device address (default; a DMA
+    // transfer's queue handshake costs more than the copy at these sizes), or by
+    // hipMemcpyAsync (M3S_STAGE_DMA=1, unaligned, or no device address)
+    hipError_t download(char* h, const void* src, size_t bytes, hipStream_t st) {
+        static const bool dma = [] {
+            const char* e = getenv("M3S_STAGE_DMA");
+            return e && atoi(e) != 0;
+        }();
+        if (!dma && dev && (bytes & 3) == 0 && ((uintptr_t)src & 15) == 0 && ((h - buf) & 15) == 0)
+            return launch_stage_copy(st, dev + (h - buf), src, bytes);
+        return hipMemcpyAsync(h, src, bytes, hipMemcpyDeviceToHost, st);
+    }
     hipError_t mark(hipStream_t st) {
         if (!done) {
             hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
@@ -229,7 +242,7 @@ int chunk_points(int64_t HW, int nchunks) {
 
 struct Layout {
     size_t partials, edgeblk, compact, x, flags, ii_loc, jj_loc, blk_ptr, blk_ent, blk_ref, grad_ptr,
-        grad_ent, ecnt, cok, sched, pack, packx, pcnt, zs, twc_save, total;
+        grad_ent, ecnt, cok, sorder, sched, pack, packx, pcnt, zs, twc_save, total;
     int nchunks, npad, nblk_max;
 };
 
@@ -273,6 +286,7 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.grad_ent = take(sizeof(int) * (size_t)std::max(E_local, E_total) * 2);
     L.ecnt = take(sizeof(int) * (size_t)E_local);  // fused edge reduce: finished chunks per edge
     L.cok = take(sizeof(int) * (size_t)std::max<int64_t>(N, 1));  // per keyframe: every c > C_thresh
+    L.sorder = take(sizeof(int) * (size_t)E_local);  // the accumulate schedule's edge order
     L.sched = take(sizeof(int) * 4 * (size_t)E_local * L.nchunks);  // {edge, chunk, ix, jx} per task
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
     // dense depth array of the keyframes (calib)
@@ -315,45 +329,44 @@ struct Plan {
 // depend on it).  Local directed edges sorted by (jx, ix) are split into 8 contiguous
 // groups, one per XCD (blocks b, b+8, ... share an XCD under round-robin dispatch); inside a
 // group tasks run chunk-major, so the few keyframes of a group stay L2-resident while all
-// of their edges stream the same point range.
-// Written straight into the upload image as the accumulate's task records {e, c, ii, jj}:
-// group g's list is chunk-major (element k: edge order[lo_g + k % n_g], chunk k / n_g) and the
-// groups are interleaved round-robin.
-void build_schedule(const std::vector<int>& ii_loc, const std::vector<int>& jj_loc, int nchunks,
-                    int* rec) {
+// of their edges stream the same point range.  The host orders the edges (two stable
+// counting sorts, by ix then by jx: the stable (jx, ix) order, O(E + N)) and sizes the groups;
+// the device expands the task records {e, c, ix, jx} (launch_sched_expand): group g's list is
+// chunk-major (element k: edge order[lo_g + k % n_g], chunk k / n_g) and the groups are
+// interleaved round-robin.  (Written record by record into pinned memory and read back over
+// PCIe, the schedule cost ~0.1 ms of host time per cfg4 call.)
+void build_schedule_order(const std::vector<int>& ii_loc, const std::vector<int>& jj_loc, int nkey, int* order,
+                          SchedGroups& G) {
     const int E = (int)ii_loc.size();
-    auto put = [&](int e, int c) {
-        rec[0] = e;
-        rec[1] = c;
-        rec[2] = ii_loc[e];
-        rec[3] = jj_loc[e];
-        rec += 4;
-    };
     static const bool off = [] {
         const char* e = getenv("M3S_ACC_SCHED");
         return e && atoi(e) == 0;
     }();
-    if (off) {
-        for (int e = 0; e < E; e++)
-            for (int c = 0; c < nchunks; c++) put(e, c);
-        return;
+    G = SchedGroups{};
+    G.off = off ? 1 : 0;
+    if (off || E == 0) return;
+    static thread_local std::vector<int> tmp, cnt;
+    tmp.resize(E);
+    auto pass = [&](const std::vector<int>& key, const int* src, int* dst) {
+        cnt.assign((size_t)nkey + 1, 0);
+        for (int k = 0; k < E; k++) cnt[key[src ? src[k] : k] + 1]++;
+        for (int v = 0; v < nkey; v++) cnt[v + 1] += cnt[v];
+        for (int k = 0; k < E; k++) {
+            const int e = src ? src[k] : k;
+            dst[cnt[key[e]]++] = e;
+        }
+    };
+    pass(ii_loc, nullptr, tmp.data());
+    pass(jj_loc, tmp.data(), order);
+    constexpr int NG = 8;
+    G.q = E;
+    for (int g = 0; g < NG; g++) {
+        G.lo[g] = (int)((int64_t)E * g / NG);
+        G.n[g] = (int)((int64_t)E * (g + 1) / NG) - G.lo[g];
+        G.q = std::min(G.q, G.n[g]);
     }
-    std::vector<int> order(E);
-    for (int e = 0; e < E; e++) order[e] = e;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-        return jj_loc[a] != jj_loc[b] ? jj_loc[a] < jj_loc[b] : ii_loc[a] < ii_loc[b];
-    });
-    constexpr int G = 8;
-    int lo[G], n[G];
-    int64_t len_max = 0;
-    for (int g = 0; g < G; g++) {
-        lo[g] = (int)((int64_t)E * g / G);
-        n[g] = (int)((int64_t)E * (g + 1) / G) - lo[g];
-        len_max = std::max(len_max, (int64_t)n[g] * nchunks);
-    }
-    for (int64_t k = 0; k < len_max; k++)
-        for (int g = 0; g < G; g++)
-            if (k < (int64_t)n[g] * nchunks) put(order[lo[g] + (int)(k % n[g])], (int)(k / n[g]));
+    for (int g = 0; g < NG; g++)
+        if (G.n[g] > G.q) G.big[G.nbig++] = g;
 }
 
 int gn_order(const m3s_gn_args& a);
@@ -364,23 +377,45 @@ int gn_order(const m3s_gn_args& a);
 // of first appearance over ALL edges; slotmap is the dense (npose x npose) slot table.
 int plan_pairs(const int64_t* hii, const int64_t* hjj, int64_t E, int64_t N, Plan& plan, std::vector<int>& iopt,
                std::vector<int>& jopt) {
-    std::vector<int64_t> u(hii, hii + E);
-    u.insert(u.end(), hjj, hjj + E);
-    std::sort(u.begin(), u.end());
-    u.erase(std::unique(u.begin(), u.end()), u.end());
-    auto row_of = [&](int64_t id) {
-        return (int)(std::lower_bound(u.begin(), u.end(), id) - u.begin());
-    };
-    M3S_REQUIRE((int64_t)u.size() <= N,
-                "gauss_newton: %lld unique keyframe ids in ii/jj but only %lld poses in Twc/Xs",
-                (long long)u.size(), (long long)N);
     const int npose = (int)(N - 1);
     iopt.resize(E);
     jopt.resize(E);
+    // keyframe ids are small non-negative integers in practice: rank them through a dense
+    // table (O(E + max id)); a comparison sort of the 2E ids took most of this function's
+    // ~0.2 ms per cfg4 call.  Other ids: sort + binary search.
+    int64_t lo = 0, hi = -1;
     for (int64_t e = 0; e < E; e++) {
-        iopt[e] = row_of(hii[e]) - 1;  // pin = num_fix = 1
-        jopt[e] = row_of(hjj[e]) - 1;
+        lo = std::min({lo, hii[e], hjj[e]});
+        hi = std::max({hi, hii[e], hjj[e]});
     }
+    size_t nuniq = 0;
+    if (lo >= 0 && hi < std::max<int64_t>(1 << 16, 8 * (E + N))) {
+        static thread_local std::vector<int> rank;
+        rank.assign((size_t)hi + 1, 0);
+        for (int64_t e = 0; e < E; e++) rank[hii[e]] = rank[hjj[e]] = 1;
+        for (int64_t id = 0; id <= hi; id++)
+            if (rank[id]) rank[id] = (int)nuniq++;
+        if ((int64_t)nuniq <= N)
+            for (int64_t e = 0; e < E; e++) {
+                iopt[e] = rank[hii[e]] - 1;  // pin = num_fix = 1
+                jopt[e] = rank[hjj[e]] - 1;
+            }
+    } else {
+        std::vector<int64_t> u(hii, hii + E);
+        u.insert(u.end(), hjj, hjj + E);
+        std::sort(u.begin(), u.end());
+        u.erase(std::unique(u.begin(), u.end()), u.end());
+        nuniq = u.size();
+        auto row_of = [&](int64_t id) { return (int)(std::lower_bound(u.begin(), u.end(), id) - u.begin()); };
+        if ((int64_t)nuniq <= N)
+            for (int64_t e = 0; e < E; e++) {
+                iopt[e] = row_of(hii[e]) - 1;
+                jopt[e] = row_of(hjj[e]) - 1;
+            }
+    }
+    M3S_REQUIRE((int64_t)nuniq <= N,
+                "gauss_newton: %lld unique keyframe ids in ii/jj but only %lld poses in Twc/Xs",
+                (long long)nuniq, (long long)N);
     plan.slotmap.assign((size_t)std::max(npose, 0) * std::max(npose, 0), -1);
     for (int q = 0; q < npose; q++) plan.slotmap[(size_t)q * npose + q] = q;
     plan.nblk = npose;
@@ -394,6 +429,8 @@ int plan_pairs(const int64_t* hii, const int64_t* hjj, int64_t E, int64_t N, Pla
     }
     return M3S_OK;
 }
+
+double g_plan_sync_us = 0;  // M3S_PROF_HOST: build_plan's edge-list copies + stream sync
 
 int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     const int64_t E = a.E_total;
@@ -416,22 +453,26 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
         hr[2 * grank] = (double)a.edge_offset;
         hr[2 * grank + 1] = (double)a.E_local;
         M3S_HIP_CHECK(hipMallocAsync((void**)&dr, sizeof(double) * 2 * (size_t)granks, st));
-        M3S_HIP_CHECK(hipMemcpyAsync(dr + 2 * grank, hr + 2 * grank, sizeof(double) * 2, hipMemcpyHostToDevice, st));
+        Staging& in = stagings().in;
+        M3S_HIP_CHECK(in.upload(dr + 2 * grank, reinterpret_cast<const char*>(hr + 2 * grank), sizeof(double) * 2, st));
         int rc = comm_allgather_f64(a.comm, dr, 2, st);
         if (rc) {
             (void)hipFreeAsync(dr, st);
             return rc;
         }
-        M3S_HIP_CHECK(hipMemcpyAsync(hr, dr, sizeof(double) * 2 * (size_t)granks, hipMemcpyDeviceToHost, st));
+        M3S_HIP_CHECK(in.download(reinterpret_cast<char*>(hr), dr, sizeof(double) * 2 * (size_t)granks, st));
         M3S_HIP_CHECK(hipFreeAsync(dr, st));
     }
+    const auto c0 = std::chrono::steady_clock::now();
+    Staging& in = stagings().in;
     if (E > 0) {
-        M3S_HIP_CHECK(hipMemcpyAsync(hii, a.ii, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
-        M3S_HIP_CHECK(hipMemcpyAsync(hjj, a.jj, sizeof(int64_t) * E, hipMemcpyDeviceToHost, st));
+        M3S_HIP_CHECK(in.download(reinterpret_cast<char*>(hii), a.ii, sizeof(int64_t) * E, st));
+        M3S_HIP_CHECK(in.download(reinterpret_cast<char*>(hjj), a.jj, sizeof(int64_t) * E, st));
     }
     if (a.mode == M3S_GN_CALIB)
-        M3S_HIP_CHECK(hipMemcpyAsync(Kh, a.K, sizeof(float) * 9, hipMemcpyDeviceToHost, st));
+        M3S_HIP_CHECK(in.download(reinterpret_cast<char*>(Kh), a.K, sizeof(float) * 9, st));
     M3S_HIP_CHECK(hipStreamSynchronize(st));
+    g_plan_sync_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count();
     // gathered position of every edge, when the ranks' ranges partition [0, E) (else: the
     // all-reduce of the assembled system, which sums whatever the ranks hold)
     std::vector<int> gpos;
@@ -691,6 +732,7 @@ struct Ctx {
     bool ref_order = false;  // M3S_GN_ORDER_REFERENCE: gn_refacc.hip accumulate + assembly
     bool pack_issued = false;  // prepare_iterations already enqueued (setup's early pack)
     bool acc_enqueued = false;  // iteration 0's accumulate enqueued before the planning
+    bool gathered = false;      // ... and, edge-sharded, its records' all-gather too
     // the first accumulate of the call builds the packed records (no separate pack pass)
     bool first_pack = false;
     RefParams R;
@@ -844,7 +886,7 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     // image in pinned memory: the edge lists / CSR lists first (what the pack reads), then the
     // accumulate's task records (built while the GPU packs)
     const size_t ntask = (size_t)a.E_local * L.nchunks;
-    const size_t lo = L.flags, hi = L.sched + sizeof(int) * 4 * ntask;
+    const size_t lo = L.flags, hi = L.sched;
     const size_t nslot = c.need_slotmap ? p.slotmap.size() : 0;
     if (c.need_slotmap) {
         rc = c.alloc_dense(L.npad, (int)std::max<int64_t>(a.N - 1, 0));
@@ -866,7 +908,12 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     put(L.grad_ent, p.grad_ent);
     std::memset(h + (L.ecnt - lo), 0, sizeof(int) * (size_t)a.E_local);  // (the kernel re-zeroes them)
     std::memset(h + (L.cok - lo), 1, sizeof(int) * (size_t)std::max<int64_t>(a.N, 1));  // gn_cpass_kernel clears
+    SchedGroups G;
+    build_schedule_order(p.ii_loc, p.jj_loc, (int)std::max<int64_t>(a.N, 1), reinterpret_cast<int*>(h + (L.sorder - lo)), G);
     M3S_HIP_CHECK(stagings().ws.upload(c.ws + lo, h, L.sched - lo, c.st));
+    // the accumulate's task records carry the edge's keyframes: one load, not three levels
+    M3S_HIP_CHECK(launch_sched_expand(c.st, c.at<int>(L.sorder), c.at<int>(L.ii_loc), c.at<int>(L.jj_loc), L.nchunks,
+                                      G, (int64_t)ntask, c.at<int>(L.sched)));
     // M3S_GN_PACK_FIRST (default 1): a call's first accumulate builds the packed records
     // from the reference's inputs itself (gn_accum_packed_kernel<..., FIRST>): 13 B read + 8 B
     // written per point-edge inside the first iteration instead of a separate 21-B pack pass
@@ -879,10 +926,6 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
         c.pack_issued = true;
     }
     const auto s2 = std::chrono::steady_clock::now();
-    // the accumulate's task records carry the edge's keyframes: one load, not three levels
-    build_schedule(p.ii_loc, p.jj_loc, L.nchunks, reinterpret_cast<int*>(h + (L.sched - lo)));
-    if (ntask > 0)
-        M3S_HIP_CHECK(stagings().ws.upload(c.ws + L.sched, h + (L.sched - lo), hi - L.sched, c.st));
     if (nslot) {  // the dense (npose x npose) slot table
         std::memcpy(h + (hi - lo), p.slotmap.data(), sizeof(int) * nslot);
         M3S_HIP_CHECK(hipMemcpyAsync(c.dyn + c.o_slot, h + (hi - lo), sizeof(int) * nslot,
@@ -893,8 +936,8 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
         auto us = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
             return std::chrono::duration<double, std::micro>(y - x).count();
         };
-        fprintf(stderr, "gn host: build_plan %.0f us, params+lists+pack %.0f us, schedule %.0f us\n",
-                us(s0, s1), us(s1, s2), us(s2, std::chrono::steady_clock::now()));
+        fprintf(stderr, "gn host: build_plan %.0f us (of which copies + sync %.0f us), params+lists+schedule+pack "
+                "%.0f us, rest %.0f us\n", us(s0, s1), g_plan_sync_us, us(s1, s2), us(s2, std::chrono::steady_clock::now()));
     }
     return M3S_OK;
 }
@@ -990,11 +1033,12 @@ int enqueue_assembly(const m3s_gn_args& a, Ctx& c) {
     const Layout& L = c.L;
     int* flags = c.at<int>(L.flags);
     const int npose = (int)(a.N - 1);
-    if (c.plan.gather) {
+    if (c.plan.gather && !c.gathered) {
         // every rank's edge records, then the assembly of ALL edges in edge order (no all-reduce)
         int rc = comm_allgather_f64(a.comm, c.eall, (size_t)c.plan.gchunk * kEdgeBlk, c.st);
         if (rc) return rc;
     }
+    c.gathered = false;
     const bool reduce = a.comm && !c.plan.gather;
     if (c.sp.enabled) {
         // block format for the sparse solves, in the solver's buffer
@@ -1292,12 +1336,14 @@ int plan_info(const int64_t* ii, const int64_t* jj, int64_t E, int64_t N, int32_
               int32_t* round_ptr, int32_t round_cap) {
     M3S_REQUIRE(info != nullptr && N >= 1 && E >= 0 && (E == 0 || (ii != nullptr && jj != nullptr)),
                 "gn_plan_info: bad arguments");
-    Plan plan;
+    // the op's per-thread plan objects (no call is in flight on this thread here)
+    Plan& plan = tls_plan();
     std::vector<int> iopt, jopt;
     int rc = plan_pairs(ii, jj, E, N, plan, iopt, jopt);
     if (rc) return rc;
     const int npose = (int)(N - 1);
-    SparsePlan sp;
+    SparsePlan& sp = tls_sparse_plan();
+    sp.reset();
     if (npose > 0) choose_sparse_plan(plan, npose, sp);
     info[0] = npose <= 0 ? -1 : sp.fused ? 0 : sp.hybrid ? 1 : 2;
     info[1] = (int32_t)sp.rounds.size();
@@ -1349,6 +1395,16 @@ int run(const m3s_gn_args& a) {
         rc = enqueue_accumulate(a, c);
         if (rc) return rc;
         c.acc_enqueued = true;
+        // edge-sharded: the records' all-gather needs no plan either -- the ranks exchange (and
+        // wait for the slowest rank's accumulate) while their hosts plan.  M3S_EARLY_GATHER: -1
+        // (default) with RCCL only (a host-callback exchange would block this thread until every
+        // rank's accumulate is done), 1 always (tests: the host exchange), 0 never
+        static const int early_gather = env_int("M3S_EARLY_GATHER", -1);
+        if (c.plan.gather && (early_gather > 0 || (early_gather < 0 && comm_is_async(a.comm)))) {
+            rc = comm_allgather_f64(a.comm, c.eall, (size_t)c.plan.gchunk * kEdgeBlk, c.st);
+            if (rc) return rc;
+            c.gathered = true;
+        }
     }
     if (env_int("M3S_SOLVER_DENSE", 0) == 0 || c.ref_order) {
         choose_sparse_plan(c.plan, npose, c.sp);

@@ -225,6 +225,18 @@ hipError_t launch_gn_solve(hipStream_t st, const SolveArgs& args);
 // copy `bytes` (a multiple of 4; both addresses 16-B aligned) from pinned host memory (its
 // device address) to device memory, stream-ordered, by a kernel
 hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes);
+// The accumulate's task records {edge, chunk, ix, jx} from the host's edge order (gn_driver.hip
+// build_schedule_order): edge-major (off) or 8 XCD groups interleaved round-robin, each group's
+// list chunk-major -- expanded on the device instead of written record by record into pinned
+// memory and read back over PCIe.
+struct SchedGroups {
+    int lo[8], n[8];  // group g: edges order[lo[g] .. lo[g] + n[g])
+    int big[8];       // the groups with n[g] = q + 1, ascending
+    int nbig, q;      // q = min n[g]
+    int off;          // 1: plain edge-major order (M3S_ACC_SCHED=0)
+};
+hipError_t launch_sched_expand(hipStream_t st, const int* order, const int* ii_loc, const int* jj_loc,
+                               int nchunks, const SchedGroups& G, int64_t ntask, int* rec);
 // flag[0] != 0 as an int (as_f64 = 0) or a double (as_f64 = 1) at dst (device-accessible)
 hipError_t launch_flag_export(hipStream_t st, const int* flag, void* dst, int as_f64);
 // save[0..n) = Twc[0..n) (before a call's first retraction)

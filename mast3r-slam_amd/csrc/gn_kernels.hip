@@ -612,6 +612,45 @@ hipError_t launch_twc_restore_on_flag(hipStream_t st, float* Twc, const float* s
     return hipGetLastError();
 }
 
+// record t: with full = 8 q nchunks, t < full is (k, g) = (t / 8, t % 8) -- every group still has
+// tasks -- and past it only the groups with q + 1 edges remain, in ascending order
+__global__ __launch_bounds__(256) void sched_expand_kernel(const int* __restrict__ order, const int* __restrict__ ii_loc,
+                                                           const int* __restrict__ jj_loc, int nchunks, SchedGroups G,
+                                                           int64_t ntask, int4* __restrict__ rec) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntask) return;
+    int e, c;
+    if (G.off) {
+        e = (int)(t / nchunks);
+        c = (int)(t % nchunks);
+    } else {
+        const int64_t full = 8 * (int64_t)G.q * nchunks;
+        int64_t k;
+        int g;
+        if (t < full) {
+            k = t >> 3;
+            g = (int)(t & 7);
+        } else {
+            const int64_t r = t - full;
+            k = (int64_t)G.q * nchunks + r / G.nbig;
+            g = G.big[r % G.nbig];
+        }
+        e = order[G.lo[g] + (int)(k % G.n[g])];
+        c = (int)(k / G.n[g]);
+    }
+    rec[t] = make_int4(e, c, ii_loc[e], jj_loc[e]);
+}
+
+hipError_t launch_sched_expand(hipStream_t st, const int* order, const int* ii_loc, const int* jj_loc,
+                               int nchunks, const SchedGroups& G, int64_t ntask, int* rec) {
+    if (ntask <= 0) return hipSuccess;
+    if (((uintptr_t)rec & 15) != 0) return hipErrorInvalidValue;
+    const int64_t blocks = (ntask + 255) / 256;
+    hipLaunchKernelGGL(sched_expand_kernel, dim3((unsigned)blocks), dim3(256), 0, st, order, ii_loc, jj_loc,
+                       nchunks, G, ntask, reinterpret_cast<int4*>(rec));
+    return hipGetLastError();
+}
+
 hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes) {
     if (bytes == 0) return hipSuccess;
     if ((bytes & 3) || ((uintptr_t)dst & 15) || ((uintptr_t)src_dev & 15)) return hipErrorInvalidValue;

@@ -70,6 +70,8 @@ def _worker(rank, world, port, mode, layout, cfg, exchange, out_q):
 
     if exchange == "reduce":
         os.environ["M3S_GN_GATHER"] = "0"
+    if exchange == "gather_early":  # iteration 0's all-gather enqueued before the host plans
+        os.environ["M3S_EARLY_GATHER"] = "1"
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "mast3r-slam_amd")]
@@ -112,7 +114,8 @@ def _worker(rank, world, port, mode, layout, cfg, exchange, out_q):
 @pytest.mark.parametrize("mode,layout,cfg,exchange", [
     ("rays", "contiguous", "cfg2", "gather"), ("calib", "contiguous", "cfg2", "gather"),
     ("rays", "two_way", "cfg2", "gather"), ("rays", "contiguous", "cfg4", "gather"),
-    ("calib", "contiguous", "cfg2", "reduce"), ("rays", "contiguous", "cfg4", "reduce")])
+    ("calib", "contiguous", "cfg2", "reduce"), ("rays", "contiguous", "cfg4", "reduce"),
+    ("calib", "contiguous", "cfg2", "gather_early"), ("rays", "contiguous", "cfg4", "gather_early")])
 def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cfg, exchange):
     """layout "two_way": each rank passes its directed-edge range of a two-way edge store as
     the op's two halves (m3s.dist.two_way_range) -- the owner-sharded store layout.  cfg4: the
@@ -139,7 +142,8 @@ def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cf
     assert rng0[0] == 0 and rng0[1] == rng1[0] and rng0[1] > 0 and rng1[1] > rng1[0]
     # one exchange per iteration (+ the ranks' edge ranges once per call when gathering); cfg4's
     # dataflow factorisation (bounded device waits) adds one for the ranks' OR of the timeout flag
-    assert calls0 == calls1 == ITERS + (exchange == "gather") + (1 if cfg == "cfg4" else 0)
+    gather = exchange.startswith("gather")
+    assert calls0 == calls1 == ITERS + gather + (1 if cfg == "cfg4" else 0)
     # bitwise identical poses on every rank: same all-reduced system, same deterministic solve
     assert np.array_equal(T0, T1)
 
@@ -164,7 +168,7 @@ def test_two_rank_sharded_op_matches_unsharded(backend, oracle, mode, layout, cf
     torch.cuda.synchronize()
     T_full = Twc.cpu().numpy()
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
-    if exchange == "gather":
+    if gather:
         assert np.array_equal(T0, T_full), rel(T0, T_full)  # rank-count independent
     else:
         assert rel(T0, T_full) < 1e-6, rel(T0, T_full)

@@ -116,3 +116,13 @@ def test_edge_cases(backend):
     assert p["pairs"] == 0
     with pytest.raises(RuntimeError, match="unique keyframe ids"):
         backend.gn_plan_info([1, 2, 3], [2, 3, 4], 2)
+
+
+def test_large_and_negative_keyframe_ids_rank_like_small_ones(backend):
+    """Keyframe ids far apart or negative take the sorted (not the dense-table) ranking: the same
+    plan as the same graph on ids 0 .. N-1."""
+    ii, jj, N = graph_lists("cfg3")
+    ref = backend.gn_plan_info(ii, jj, N)
+    for f in (lambda k: k * 10**9 + 7, lambda k: k - 50):
+        p = backend.gn_plan_info([f(k) for k in ii], [f(k) for k in jj], N)
+        assert p == ref
