@@ -84,7 +84,7 @@ template <int CM>
 __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
     const float* __restrict__ rays, const float* __restrict__ pts, const float* __restrict__ p_init,
     float* __restrict__ p_new, uint8_t* __restrict__ converged, int H, int W, int64_t N,
-    int64_t total, int max_iter, float lambda_init, float cost_thresh, int xcd_band) {
+    int64_t total, int max_iter, float lambda_init, float cost_thresh, int xcd_band, int skip_still) {
     // xcd_band: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, dispatch),
     // so block b runs on XCD b % 8; block b takes the logical block (b % 8) * per + b / 8 instead,
     // and each XCD walks ONE contiguous band of pixels -- its bilinear gathers stay in a band of
@@ -143,25 +143,33 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
         const float u_new = clamp_ref(cmad<CM>(det_inv, cmm<CM>(A11, b0, -A01, b1), u), 1.0f, umax);
         const float v_new = clamp_ref(cmad<CM>(det_inv, cmm<CM>(-A01, b0, A00, b1), v), 1.0f, vmax);
 
-        // :225-256 the cost at the new pixel (ray channels only)
-        const Bilin bn = make_bilin(img, W, u_new, v_new);
-        const float t0 = interp<CM>(bn, 0), t1 = interp<CM>(bn, 1), t2 = interp<CM>(bn, 2);
-        const float n2_inv = inv_f(sqrtf(cdot3<CM>(t0, t0, t1, t1, t2, t2)));
-        const float f0 = cmad<CM>(t0, n2_inv, -px), f1 = cmad<CM>(t1, n2_inv, -py),
-                    f2 = cmad<CM>(t2, n2_inv, -pz);
-        const float new_cost = cdot3<CM>(f0, f0, f1, f1, f2, f2);
-
-        if (new_cost < cost) {
-            u = u_new;
-            v = v_new;
-            lambda = (float)((double)lambda * 0.1);  // `lambda *= 0.1` is a double multiply
-            conv = new_cost < cost_thresh;
-            e0 = f0;
-            e1 = f1;
-            e2 = f2;
-            cost = new_cost;
-            if (it + 1 < max_iter) normal_terms(bn);
-        } else {
+        // :225-256 the cost at the new pixel (ray channels only).  A step that rounds to zero
+        // (u_new == u and v_new == v: most pixels once converged, 43-88 % from the third
+        // iteration on the bench pair) evaluates the SAME texels by the same operations, so its
+        // cost is exactly the current one and the step is rejected: the gather is skipped and
+        // only lambda and the flag move, bitwise as if it had been taken.
+        bool accepted = false;
+        if (!skip_still || u_new != u || v_new != v) {
+            const Bilin bn = make_bilin(img, W, u_new, v_new);
+            const float t0 = interp<CM>(bn, 0), t1 = interp<CM>(bn, 1), t2 = interp<CM>(bn, 2);
+            const float n2_inv = inv_f(sqrtf(cdot3<CM>(t0, t0, t1, t1, t2, t2)));
+            const float f0 = cmad<CM>(t0, n2_inv, -px), f1 = cmad<CM>(t1, n2_inv, -py),
+                        f2 = cmad<CM>(t2, n2_inv, -pz);
+            const float new_cost = cdot3<CM>(f0, f0, f1, f1, f2, f2);
+            if (new_cost < cost) {
+                accepted = true;
+                u = u_new;
+                v = v_new;
+                lambda = (float)((double)lambda * 0.1);  // `lambda *= 0.1` is a double multiply
+                conv = new_cost < cost_thresh;
+                e0 = f0;
+                e1 = f1;
+                e2 = f2;
+                cost = new_cost;
+                if (it + 1 < max_iter) normal_terms(bn);
+            }
+        }
+        if (!accepted) {
             lambda = (float)((double)lambda * 10.0);
             conv = cost < cost_thresh;
         }
@@ -353,12 +361,22 @@ extern "C" int m3s_iter_proj_ex(const float* rays, const float* pts, const float
         const char* e = getenv("M3S_IP_XCD");
         return e ? atoi(e) : 1;
     }();
+    // M3S_IP_SKIP: 1 = a zero step skips its trial gather (bitwise the same either way), 0 =
+    // always gathers, default: skip on launches of >= 2^19 pixels.  Measured (profiles/r05_s_ip_skip/):
+    // 8 pairs of 384x512 0.181 -> 0.171 ms (the gathers are L1/TA-bound there and 43-88 % of the
+    // steps from the third iteration on round to zero), one pair 0.046 -> 0.049 ms (3 waves per
+    // SIMD: latency-bound, and the divergent branch only costs)
+    static const int skip_env = [] {
+        const char* e = getenv("M3S_IP_SKIP");
+        return e ? atoi(e) : -1;
+    }();
+    const int skip_still = skip_env >= 0 ? skip_env : (total >= ((int64_t)1 << 19) ? 1 : 0);
     const int64_t nblk = (total + kBlock - 1) / kBlock;
     const unsigned ip_grid = (unsigned)(xcd_band ? (nblk + 7) / 8 * 8 : nblk);
 #define M3S_IP(CM)                                                                                      \
     hipLaunchKernelGGL(iter_proj_kernel<CM>, dim3(ip_grid), dim3(kBlock), 0, (hipStream_t)stream,       \
                        rays, pts, p_init, p_new, converged, (int)H, (int)W, N, total, max_iter,            \
-                       lambda_init, cost_thresh, xcd_band)
+                       lambda_init, cost_thresh, xcd_band, skip_still)
     if (contract == M3S_CONTRACT_OFF) M3S_IP(M3S_CONTRACT_OFF);
     else if (contract == M3S_CONTRACT_NVCC) M3S_IP(M3S_CONTRACT_NVCC);
     else M3S_IP(M3S_CONTRACT_NVCC_RIGHT);

@@ -5,6 +5,8 @@ each setting runs in its own child process):
   * M3S_MULTI_DCAP -- the multi plan's elimination degree cap (32 default; 16 = round 4): another
                       ordering, so equal only to the f64 solve's rounding (poses to 1e-6);
   * M3S_IP_XCD     -- iter_proj's XCD-banded block order (1, default) or pixel order (0);
+  * M3S_IP_SKIP    -- iter_proj skips the trial gather of a step that rounds to zero (1; default:
+                      on launches of >= 2^19 pixels) or always gathers (0);
   * M3S_MATCH_PLANES -- the fused matching op's plane-major fp16 D11 + refine (1, default) or the
                       interleaved copy + refine_f16_kernel (0)."""
 import json
@@ -72,5 +74,6 @@ def test_elimination_degree_cap_changes_only_rounding():
 
 def test_matching_switches_are_bitwise_noops():
     ref = _run(MATCH_CHILD, dict(M3S_IP_XCD="1", M3S_MATCH_PLANES="1"))
-    for env in (dict(M3S_IP_XCD="0", M3S_MATCH_PLANES="1"), dict(M3S_IP_XCD="1", M3S_MATCH_PLANES="0")):
+    for env in (dict(M3S_IP_XCD="0", M3S_MATCH_PLANES="1"), dict(M3S_IP_XCD="1", M3S_MATCH_PLANES="0"),
+                dict(M3S_IP_SKIP="0"), dict(M3S_IP_SKIP="1")):
         assert _run(MATCH_CHILD, env) == ref, env
