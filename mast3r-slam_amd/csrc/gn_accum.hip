@@ -872,14 +872,16 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
 // rebuilds x, y with the same two roundings -- the identical values, so the identical result.
 __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__ Xs, int64_t total,
                                                        float* __restrict__ Zs, AccParams P,
-                                                       int* __restrict__ flags) {
+                                                       int* __restrict__ flags, const float* __restrict__ K) {
+    // the intrinsics from the device K when given (the pass runs before the host has read K)
+    const float fx = K ? K[0] : P.fx, fy = K ? K[4] : P.fy, cx = K ? K[2] : P.cx, cy = K ? K[5] : P.cy;
     float* __restrict__ tu = Zs + total;
     float* __restrict__ tv = tu + P.width;
     float* __restrict__ IZn = inv_depths(Zs, P) + (int64_t)blockIdx.y * P.HW;
     const int n = blockIdx.y;  // keyframe row
     const int t0 = blockIdx.x * 256 + threadIdx.x;
-    if (n == 0 && t0 < P.width) tu[t0] = ((float)t0 - P.cx) / P.fx;
-    if (n == 0 && t0 < P.height) tv[t0] = ((float)t0 - P.cy) / P.fy;
+    if (n == 0 && t0 < P.width) tu[t0] = ((float)t0 - cx) / fx;
+    if (n == 0 && t0 < P.height) tv[t0] = ((float)t0 - cy) / fy;
     const float* __restrict__ Xn = Xs + (int64_t)n * P.HW * 3;
     float* __restrict__ Zn = Zs + (int64_t)n * P.HW;
     bool ray = true;
@@ -889,8 +891,8 @@ __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__
         IZn[k] = z > P.z_eps ? vrcp(z) : __builtin_nanf("");
         float u, v;
         pixel_of(k, P, u, v);
-        const float xr = z * ((u - P.cx) / P.fx);
-        const float yr = z * ((v - P.cy) / P.fy);
+        const float xr = z * ((u - cx) / fx);
+        const float yr = z * ((v - cy) / fy);
         ray = ray && __float_as_uint(xr) == __float_as_uint(x) && __float_as_uint(yr) == __float_as_uint(y);
     }
     if (!ray) flags[kFlagNotRay] = 1;  // benign race: every writer stores 1
@@ -1121,9 +1123,25 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
     return hipGetLastError();
 }
 
+hipError_t launch_pack_pre(hipStream_t st, const float* Xs, int64_t N, const float* Cs, const AccParams& P, int* cok,
+                           float* Zs, int* flags, const float* K) {
+    if (cok != nullptr && N > 0) {  // per keyframe: do all its confidences pass C_thresh?
+        const int bx = (int)std::max<int64_t>(1, std::min<int64_t>((P.HW + 1023) / 1024, 8192 / std::max<int64_t>(N, 1)));
+        hipLaunchKernelGGL(gn_cpass_kernel, dim3(bx, (unsigned)N), dim3(256), 0, st, Cs, P, cok, flags);
+    }
+    if (Zs) {
+        const int64_t total = N * (int64_t)P.HW;
+        const int bx = (int)std::max<int64_t>(std::min<int64_t>((P.HW + 255) / 256,
+                                                                std::max<int64_t>(8192 / std::max<int64_t>(N, 1), 2)),
+                                              (std::max(P.width, P.height) + 255) / 256);
+        hipLaunchKernelGGL(gn_depth_kernel, dim3(bx, (unsigned)N), dim3(256), 0, st, Xs, total, Zs, P, flags, K);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
                        const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P, int* cok,
-                       int4* pack, float* px, int* pcnt, float* Zs, const int* flags, bool skip_pack) {
+                       int4* pack, float* px, int* pcnt, const int* flags, bool skip_pack) {
     if (E_local > 0 && px) {
         const dim3 grid((unsigned)P.nchunks, (unsigned)E_local);
         int2* pk = reinterpret_cast<int2*>(pack);
@@ -1137,22 +1155,11 @@ hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, i
             hipLaunchKernelGGL(gn_pack_compact_kernel<GN_POINTS>, grid, dim3(kAccThreads), 0, st, Xs, Cs, ii_loc,
                                jj_loc, es, P, pk, px, pcnt, flags);
     } else if (E_local > 0) {
-        if (cok != nullptr && N > 0) {  // per keyframe: do all its confidences pass C_thresh?
-            const int bx = (int)std::max<int64_t>(1, std::min<int64_t>((P.HW + 1023) / 1024, 8192 / std::max<int64_t>(N, 1)));
-            hipLaunchKernelGGL(gn_cpass_kernel, dim3(bx, (unsigned)N), dim3(256), 0, st, Cs, P, cok, flags);
-        }
+        // (cok from the cpass of launch_pack_pre)
         const dim3 grid((unsigned)((P.HW / 4 + kAccThreads - 1) / kAccThreads), (unsigned)E_local);
         if (!skip_pack)  // (else the first iteration's accumulate builds the records)
             hipLaunchKernelGGL(gn_pack_kernel, grid, dim3(kAccThreads), 0, st, Cs, ii_loc, jj_loc, es,
                                P, cok, pack, flags);
-    }
-    if (Zs) {
-        const int64_t total = N * (int64_t)P.HW;
-        const int bx = (int)std::max<int64_t>(std::min<int64_t>((P.HW + 255) / 256,
-                                                                std::max<int64_t>(8192 / std::max<int64_t>(N, 1), 2)),
-                                              (std::max(P.width, P.height) + 255) / 256);
-        hipLaunchKernelGGL(gn_depth_kernel, dim3(bx, (unsigned)N), dim3(256), 0, st, Xs, total, Zs, P,
-                           const_cast<int*>(flags));
     }
     return hipGetLastError();
 }

@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -275,6 +276,7 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     // allocations: see Ctx::alloc_dense and upload_sparse_plan)
     L.x = take(sizeof(double) * (size_t)L.npad);
     L.flags = take(sizeof(int) * kNumFlags);
+    L.cok = take(sizeof(int) * (size_t)std::max<int64_t>(N, 1));  // per keyframe: every c > C_thresh
     L.twc_save = take(sizeof(float) * 8 * (size_t)std::max<int64_t>(N, 1));  // Twc at the call's start
     L.ii_loc = take(sizeof(int) * (size_t)E_local);
     L.jj_loc = take(sizeof(int) * (size_t)E_local);
@@ -285,7 +287,6 @@ Layout make_layout(int mode, int64_t N, int64_t HW, int64_t E_total, int64_t E_l
     L.grad_ptr = take(sizeof(int) * ((size_t)npose + 1));
     L.grad_ent = take(sizeof(int) * (size_t)std::max(E_local, E_total) * 2);
     L.ecnt = take(sizeof(int) * (size_t)E_local);  // fused edge reduce: finished chunks per edge
-    L.cok = take(sizeof(int) * (size_t)std::max<int64_t>(N, 1));  // per keyframe: every c > C_thresh
     L.sorder = take(sizeof(int) * (size_t)E_local);  // the accumulate schedule's edge order
     L.sched = take(sizeof(int) * 4 * (size_t)E_local * L.nchunks);  // {edge, chunk, ix, jx} per task
     // iteration-invariant packed stream {code, sqrt q} per directed point-edge (8 B), and the
@@ -432,7 +433,9 @@ int plan_pairs(const int64_t* hii, const int64_t* hjj, int64_t E, int64_t N, Pla
 
 double g_plan_sync_us = 0;  // M3S_PROF_HOST: build_plan's edge-list copies + stream sync
 
-int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
+// before_wait: enqueued after the edge-list copies, before the host waits for them (work that
+// needs no plan runs on the GPU while the host plans)
+int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan, const std::function<int()>& before_wait = {}) {
     const int64_t E = a.E_total;
     // sharded call: gather the edge records (M3S_GN_GATHER=0: all-reduce the assembled system)
     int grank = 0, granks = 1;
@@ -471,7 +474,16 @@ int build_plan(const m3s_gn_args& a, hipStream_t st, Plan& plan) {
     }
     if (a.mode == M3S_GN_CALIB)
         M3S_HIP_CHECK(in.download(reinterpret_cast<char*>(Kh), a.K, sizeof(float) * 9, st));
-    M3S_HIP_CHECK(hipStreamSynchronize(st));
+    if (before_wait) {
+        static thread_local hipEvent_t copied = nullptr;  // (no destructor: nothing at exit)
+        if (!copied) M3S_HIP_CHECK(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+        M3S_HIP_CHECK(hipEventRecord(copied, st));
+        int rc = before_wait();
+        if (rc) return rc;
+        M3S_HIP_CHECK(hipEventSynchronize(copied));
+    } else {
+        M3S_HIP_CHECK(hipStreamSynchronize(st));
+    }
     g_plan_sync_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count();
     // gathered position of every edge, when the ranks' ranges partition [0, E) (else: the
     // all-reduce of the assembled system, which sums whatever the ranks hold)
@@ -800,23 +812,12 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     c.L = make_layout(a.mode, a.N, a.HW, a.E_total, a.E_local);
     static const bool prof_host = env_int("M3S_PROF_HOST", 0) != 0;
     const auto s0 = std::chrono::steady_clock::now();
-    rc = build_plan(a, c.st, c.plan);
-    if (rc) return rc;
-    if (c.plan.gather)
-        M3S_HIP_CHECK(hipMallocAsync((void**)&c.eall,
-                                     sizeof(double) * kEdgeBlk * (size_t)c.plan.granks * c.plan.gchunk, c.st));
-    const auto s1 = std::chrono::steady_clock::now();
     const Layout& L = c.L;
-    const Plan& p = c.plan;
     AccParams& P = c.P;
     P.s0_inv = 1.0f / a.sigma0;
     P.s1_inv = (a.mode == M3S_GN_POINTS) ? 0.0f : 1.0f / a.sigma1;
     P.C_thresh = a.C_thresh;
     P.Q_thresh = a.Q_thresh;
-    P.fx = p.K[0];
-    P.fy = p.K[1];
-    P.cx = p.K[2];
-    P.cy = p.K[3];
     P.pb_lo = (float)a.pixel_border;
     P.pb_hi_u = (float)(a.width - 1 - a.pixel_border);
     P.pb_hi_v = (float)(a.height - 1 - a.pixel_border);
@@ -870,10 +871,6 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
         R.s1_inv = (a.mode == M3S_GN_POINTS) ? 0.0f : (float)(1.0 / (double)a.sigma1);
         R.C_thresh = a.C_thresh;
         R.Q_thresh = a.Q_thresh;
-        R.fx = p.K[0];
-        R.fy = p.K[1];
-        R.cx = p.K[2];
-        R.cy = p.K[3];
         R.z_eps = a.z_eps;
         R.width = a.width > 0 ? a.width : 1;
         R.height = a.height;
@@ -882,11 +879,46 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
         R.variant = env_int("M3S_GN_REF_VARIANT", 0);  // diagnostics
         R.contract = a.contract;
     }
-    // the workspace's plan integers (flags .. sched, one contiguous span of the layout) as an
+    // the per-call passes that need no edge lists (the keyframes' confidence pass, calib's depth
+    // arrays) and the call's device flags are enqueued right after the edge-list copies: they run
+    // while the host waits for the copies and plans (the lists upload below no longer carries
+    // the flags / cok)
+    int* dflags = c.at<int>(L.flags);
+    int* dcok = c.at<int>(L.cok);
+    auto pre_pass = [&]() -> int {
+        M3S_HIP_CHECK(launch_gn_init(c.st, dflags, P.raycheck ? 0 : 1, dcok, a.N));
+        if (c.packed)
+            M3S_HIP_CHECK(launch_pack_pre(c.st, a.Xs, a.N, a.Cs, P, !c.compact ? dcok : nullptr,
+                                          a.mode == M3S_GN_CALIB ? c.at<float>(L.zs) : nullptr, dflags,
+                                          a.mode == M3S_GN_CALIB ? a.K : nullptr));
+        return M3S_OK;
+    };
+    // M3S_PREPASS=0 (A/B): the passes after the host's stream wait instead (cfg3 +0.6 % with
+    // them before it, two interleaved pairs on one box: profiles/r05_u_prepass/)
+    static const bool prepass_early = env_int("M3S_PREPASS", 1) != 0;
+    rc = build_plan(a, c.st, c.plan, prepass_early ? pre_pass : std::function<int()>());
+    if (!rc && !prepass_early) rc = pre_pass();
+    if (rc) return rc;
+    if (c.plan.gather)
+        M3S_HIP_CHECK(hipMallocAsync((void**)&c.eall,
+                                     sizeof(double) * kEdgeBlk * (size_t)c.plan.granks * c.plan.gchunk, c.st));
+    const auto s1 = std::chrono::steady_clock::now();
+    const Plan& p = c.plan;
+    P.fx = p.K[0];
+    P.fy = p.K[1];
+    P.cx = p.K[2];
+    P.cy = p.K[3];
+    if (c.ref_order) {
+        c.R.fx = p.K[0];
+        c.R.fy = p.K[1];
+        c.R.cx = p.K[2];
+        c.R.cy = p.K[3];
+    }
+    // the workspace's plan integers (ii_loc .. sched, one contiguous span of the layout) as an
     // image in pinned memory: the edge lists / CSR lists first (what the pack reads), then the
     // accumulate's task records (built while the GPU packs)
     const size_t ntask = (size_t)a.E_local * L.nchunks;
-    const size_t lo = L.flags, hi = L.sched;
+    const size_t lo = L.ii_loc, hi = L.sched;
     const size_t nslot = c.need_slotmap ? p.slotmap.size() : 0;
     if (c.need_slotmap) {
         rc = c.alloc_dense(L.npad, (int)std::max<int64_t>(a.N - 1, 0));
@@ -894,8 +926,6 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     }
     char* h = stagings().ws.get(hi - lo + sizeof(int) * nslot);
     M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
-    std::memset(h, 0, L.ii_loc - lo);  // flags
-    if (!c.P.raycheck) reinterpret_cast<int*>(h)[kFlagNotRay] = 1;
     auto put = [&](size_t off, const std::vector<int>& v) {
         if (!v.empty()) std::memcpy(h + (off - lo), v.data(), sizeof(int) * v.size());
     };
@@ -907,7 +937,6 @@ int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     put(L.grad_ptr, p.grad_ptr);
     put(L.grad_ent, p.grad_ent);
     std::memset(h + (L.ecnt - lo), 0, sizeof(int) * (size_t)a.E_local);  // (the kernel re-zeroes them)
-    std::memset(h + (L.cok - lo), 1, sizeof(int) * (size_t)std::max<int64_t>(a.N, 1));  // gn_cpass_kernel clears
     SchedGroups G;
     build_schedule_order(p.ii_loc, p.jj_loc, (int)std::max<int64_t>(a.N, 1), reinterpret_cast<int*>(h + (L.sorder - lo)), G);
     M3S_HIP_CHECK(stagings().ws.upload(c.ws + lo, h, L.sched - lo, c.st));
@@ -949,7 +978,6 @@ int prepare_iterations(const m3s_gn_args& a, Ctx& c) {
     M3S_HIP_CHECK(launch_pack(a.mode, c.st, (int)a.E_local, a.Xs, a.N, a.Cs, c.at<int>(L.ii_loc),
                               c.at<int>(L.jj_loc), c.es, c.P, c.at<int>(L.cok), c.at<int4>(L.pack),
                               c.compact ? c.at<float>(L.packx) : nullptr, c.at<int>(L.pcnt),
-                              a.mode == M3S_GN_CALIB ? c.at<float>(L.zs) : nullptr,
                               c.at<int>(L.flags), c.first_pack));
     return M3S_OK;
 }

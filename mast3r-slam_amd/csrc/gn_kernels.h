@@ -103,7 +103,15 @@ hipError_t launch_accum(int mode, bool vec, dim3 grid, hipStream_t st, const flo
 // (live points only: records in pack, Xj copies in px, per-(edge, chunk) counts in pcnt)
 hipError_t launch_pack(int mode, hipStream_t st, int E_local, const float* Xs, int64_t N, const float* Cs,
                        const int* ii_loc, const int* jj_loc, const EdgeSrc& es, const AccParams& P, int* cok,
-                       int4* pack, float* px, int* pcnt, float* Zs, const int* flags, bool skip_pack = false);
+                       int4* pack, float* px, int* pcnt, const int* flags, bool skip_pack = false);
+// The per-call passes the pack reads that need no edge lists: the keyframes' confidence pass
+// (cpass: cok[n] = every C of keyframe n > C_thresh; cok preset to 1) and, calib, the depth /
+// inverse-depth arrays and ray tables (Zs != nullptr; K != nullptr: fx, fy, cx, cy read from
+// the device K instead of P) -- enqueued while the host still plans.
+hipError_t launch_pack_pre(hipStream_t st, const float* Xs, int64_t N, const float* Cs, const AccParams& P, int* cok,
+                           float* Zs, int* flags, const float* K);
+// The call's device flags (kNumFlags ints: 0, kFlagNotRay = not_ray) and cok[0 .. n) = 1.
+hipError_t launch_gn_init(hipStream_t st, int* flags, int not_ray, int* cok, int64_t n);
 hipError_t launch_accum_packed(int mode, dim3 grid, hipStream_t st, const float* Twc,
                                const float* Xs, const float* Zs, const int* ii_loc,
                                const int* jj_loc, const int4* pack, const AccParams& P,

@@ -651,6 +651,19 @@ hipError_t launch_sched_expand(hipStream_t st, const int* order, const int* ii_l
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void gn_init_kernel(int* __restrict__ flags, int not_ray, int* __restrict__ cok,
+                                                      int64_t n) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < kNumFlags) flags[t] = t == kFlagNotRay ? not_ray : 0;
+    if (t < n) cok[t] = 1;
+}
+
+hipError_t launch_gn_init(hipStream_t st, int* flags, int not_ray, int* cok, int64_t n) {
+    const int64_t m = std::max<int64_t>(n, kNumFlags);
+    hipLaunchKernelGGL(gn_init_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, flags, not_ray, cok, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_stage_copy(hipStream_t st, void* dst, const void* src_dev, size_t bytes) {
     if (bytes == 0) return hipSuccess;
     if ((bytes & 3) || ((uintptr_t)dst & 15) || ((uintptr_t)src_dev & 15)) return hipErrorInvalidValue;
