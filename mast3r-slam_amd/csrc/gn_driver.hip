@@ -649,6 +649,8 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
                                                   &sp.tc3, &sp.rc4, &sp.inl};
     size_t* offs[] = {&sp.i_nodes, &sp.i_fptr, &sp.i_fronts, &sp.i_tail, &sp.i_tmap, &sp.i_tg,
                       &sp.i_tc, &sp.i_rtg, &sp.i_rc, &sp.i_tc3, &sp.i_rc4, &sp.i_inl};
+    // (inl: its first ninl ints; SparsePlan::inl)
+    auto len = [&](size_t k) { return parts[k] == &sp.inl ? sp.ninl : parts[k]->size(); };
     size_t n = 0;
     for (size_t k = 0; k < parts.size(); k++) {
         if (k == 4) {
@@ -657,7 +659,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         }
         if (parts[k] == &sp.inl) n = align_up(n, 4);  // 16-B records (int4 loads)
         *offs[k] = n;
-        n += parts[k]->size();
+        n += len(k);
     }
     sp.o_int = take(sizeof(int) * std::max<size_t>(n, 1));
     M3S_HIP_CHECK(hipMallocAsync((void**)&sp.dbuf, off, st));
@@ -668,7 +670,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         int* h = reinterpret_cast<int*>(stagings().out.get(sizeof(int) * n));
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
         for (size_t k = 0; k < parts.size(); k++)
-            if (!parts[k]->empty()) std::memcpy(h + *offs[k], parts[k]->data(), sizeof(int) * parts[k]->size());
+            if (len(k) > 0) std::memcpy(h + *offs[k], parts[k]->data(), sizeof(int) * len(k));
         int* hr = h + sp.i_rounds;
         for (const SpRound& R : sp.rounds) {
             const int v[8] = {R.node_begin, R.nnodes, R.tbeg, R.nbt, R.rbeg, R.nrt, R.wbeg, R.wcount};
@@ -1167,7 +1169,9 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
             for (const SpRound& R : sp.rounds) {
                 int ncontrib = 0, maxc = 0;
                 for (int t = 0; t < R.nbt; t++) {
-                    const int k = sp.tg[3 * (R.tbeg + t) + 2] - sp.tg[3 * (R.tbeg + t) + 1];
+                    const int* T = sp.fused ? &sp.tg[3 * (R.tbeg + t)]
+                                            : &sp.inl[(size_t)kSpRec * (R.tbeg + R.rbeg + t)];
+                    const int k = T[2] - T[1];
                     ncontrib += k;
                     maxc = std::max(maxc, k);
                 }
@@ -1434,6 +1438,7 @@ int run(const m3s_gn_args& a) {
             c.gathered = true;
         }
     }
+    const auto t1b = now();
     if (env_int("M3S_SOLVER_DENSE", 0) == 0 || c.ref_order) {
         choose_sparse_plan(c.plan, npose, c.sp);
         t2 = now();
@@ -1445,8 +1450,8 @@ int run(const m3s_gn_args& a) {
         t3 = now();
     }
     if (prof_host)
-        fprintf(stderr, "gn host: setup %.0f us, plan %.0f us, upload %.0f us\n", us(t0, t1), us(t1, t2),
-                us(t2, t3));
+        fprintf(stderr, "gn host: setup %.0f us, early enqueue %.0f us, plan %.0f us, upload %.0f us\n", us(t0, t1),
+                us(t1, t1b), us(t1b, t2), us(t2, t3));
     for (int itr = 0; itr < a.max_iter; itr++) {
         if (!c.acc_enqueued) g_prof.mark(c.st);  // (iteration 0's mark preceded its early accumulate)
         rc = enqueue_system(a, c);

@@ -30,10 +30,16 @@ struct SparsePlan {
     int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
     std::vector<SpRound> rounds;
     std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
-    // multi-launch rounds (sp_round_kernel), per contribution: (v, code_r, code_s) for block
-    // targets, (v, code_r, W id, owner node | -1) for RHS targets; code = block * 2 + transposed
+    // multi-launch rounds (sp_round_kernel), per contribution past a record's kSpInline inline
+    // ones: (v, code_r, code_s) for block targets, (v, code_r, W id, owner node | -1) for RHS
+    // targets; code = block * 2 + transposed.  (tg / tc / rtg / rc: the single-workgroup solve's)
     std::vector<int> tc3, rc4;
-    std::vector<int> inl;  // multi-launch rounds: one kSpRec record per target (gn_kernels.h)
+    // multi-launch rounds: one kSpRec record per target (gn_kernels.h), the first ninl ints of
+    // inl.  The buffer is not cleared between plans: a record's inline slots past its
+    // contribution count are never read by the kernel, so they are left as they are (most
+    // targets have 1-2 of 9; writing the whole 160-B records was most of a cfg4 plan's time)
+    std::vector<int> inl;
+    size_t ninl = 0;
     // device (one stream-ordered allocation per call)
     char* dbuf = nullptr;
     size_t o_dense = 0, o_linv = 0;  // the dense core (npad_tail + 64) x npad_tail and its tile inverses
@@ -56,10 +62,11 @@ struct SparsePlan {
         SparsePlan fresh;
         for (auto v : {&SparsePlan::nodes, &SparsePlan::fptr, &SparsePlan::fronts, &SparsePlan::tg,
                        &SparsePlan::tc, &SparsePlan::rtg, &SparsePlan::rc, &SparsePlan::tail,
-                       &SparsePlan::tmap, &SparsePlan::tc3, &SparsePlan::rc4, &SparsePlan::inl}) {
+                       &SparsePlan::tmap, &SparsePlan::tc3, &SparsePlan::rc4}) {
             (this->*v).clear();
             (fresh.*v).swap(this->*v);
         }
+        fresh.inl.swap(inl);  // (kept as it is: see ninl)
         rounds.clear();
         fresh.rounds.swap(rounds);
         *this = std::move(fresh);
@@ -82,9 +89,10 @@ struct RoundPolicy {
 };
 // pairs: the unordered pose pairs of the graph's off-diagonal blocks (block id nblk0 + k for
 // pairs[k], nblk0 = npose diagonal blocks first); nblk: the graph's block count.
-// symbolic: choose the rounds and eliminate only -- no target / contribution lists (rounds,
-// nodes, fronts, tail, tmap, fused_tail and nints_back as the full plan's; nblocks, nints and the
-// lists not): what the driver needs to accept or reject a policy before building its plan.
+// symbolic: choose the rounds and eliminate only -- no block ids, target / contribution lists
+// (rounds, nodes, tail, fused_tail and nints_back as the full plan's, fronts and tmap sized but
+// not filled; nblocks, nints and the lists not): what the driver needs to accept or reject a
+// policy before building its plan.
 // Cost (cfg4, 255 poses, 1007 pairs): counting sorts instead of comparison sorts for the round's
 // targets and word-parallel fill keep the host plan well below the first accumulate it overlaps
 // once the edges are sharded over several GPUs (tools/plan_bench.cpp).
@@ -129,7 +137,7 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
             for (uint64_t w = a[k]; w; w &= w - 1) out.push_back(64 * k + __builtin_ctzll(w));
     };
     auto& bidm = S.bidm;  // upper triangle (x < y) used
-    bidm.assign((size_t)npose * npose, -1);
+    if (!symbolic) bidm.assign((size_t)npose * npose, -1);
     for (size_t k = 0; k < pairs.size(); k++) {
         const int a = pairs[k].first, b = pairs[k].second;
         for (int t = 0; t < 2; t++) {
@@ -141,7 +149,7 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
                 deg[x]++;
             }
         }
-        bidm[(size_t)a * npose + b] = npose + (int)k;
+        if (!symbolic) bidm[(size_t)a * npose + b] = npose + (int)k;
     }
     sp.nblocks = nblk;
     auto block_of = [&](int x, int y) -> int {
@@ -175,6 +183,7 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
         for (const auto& x : xs) tmp[cnt[key(x)]++] = x;
         xs.swap(tmp);
     };
+    int ntg_total = 0, nrtg_total = 0;  // multi-launch records so far (block, RHS targets)
     for (int round = 0; round < rmax && nalive > 0; round++) {
         // a remaining clique is the dense tail (eliminating it pose by pose gains nothing)
         bool clique = true;
@@ -233,7 +242,7 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
             sp.nodes.push_back(v);
             const int k0 = (int)sp.fronts.size() / 4 - kb;
             for (int r : F[q]) {
-                const int blk = block_of(r, v);
+                const int blk = symbolic ? 0 : block_of(r, v);
                 sp.fronts.push_back(r);
                 sp.fronts.push_back(blk);
                 sp.fronts.push_back(r > v ? 1 : 0);
@@ -261,80 +270,107 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
             csort(tcs, tcs2, npose, [&](const TC& x) { return fr[4 * x.kj]; });
             csort(tcs, tcs2, npose, [&](const TC& x) { return fr[4 * x.ki]; });
             csort(rcs, rcs2, npose + 1, [&](int x) { return x < 0 ? 0 : fr[4 * x] + 1; });
-            R.tbeg = (int)sp.tg.size() / 3;
             const size_t n = tcs.size();
-            size_t otc = sp.tc.size(), otc3 = sp.tc3.size(), otg = sp.tg.size();
-            sp.tc.resize(otc + 2 * n);
-            if (!pol.fused) sp.tc3.resize(otc3 + 3 * n);
-            sp.tg.resize(otg + 3 * n);  // (at most one target per contribution; trimmed below)
-            int* tc = sp.tc.data() + otc;
-            int* tc3 = sp.tc3.data() + otc3;
-            int* tg = sp.tg.data() + otg;
-            for (size_t k = 0; k < n;) {
-                const int r = fr[4 * tcs[k].ki], s = fr[4 * tcs[k].kj];
-                const int c0 = (int)(otc / 2);
-                size_t e = k;
-                for (; e < n && fr[4 * tcs[e].ki] == r && fr[4 * tcs[e].kj] == s; e++) {
-                    const int ki = tcs[e].ki, kj = tcs[e].kj;
-                    *tc++ = fr[4 * ki + 3];
-                    *tc++ = fr[4 * kj + 3];
-                    otc += 2;
-                    if (!pol.fused) {
-                        *tc3++ = chosen[fq[ki]];
-                        *tc3++ = code(ki);
-                        *tc3++ = code(kj);
+            if (pol.fused) {
+                // single-workgroup solve: targets (block, c0, c1) over (W id, W id) pairs; RHS
+                // targets (pose, c0, c1) over (W id, node slot)
+                R.tbeg = (int)sp.tg.size() / 3;
+                size_t otc = sp.tc.size(), otg = sp.tg.size();
+                sp.tc.resize(otc + 2 * n);
+                sp.tg.resize(otg + 3 * n);  // (at most one target per contribution; trimmed below)
+                int* tc = sp.tc.data() + otc;
+                int* tg = sp.tg.data() + otg;
+                for (size_t k = 0; k < n;) {
+                    const int r = fr[4 * tcs[k].ki], s = fr[4 * tcs[k].kj];
+                    const int c0 = (int)(otc / 2);
+                    size_t e = k;
+                    for (; e < n && fr[4 * tcs[e].ki] == r && fr[4 * tcs[e].kj] == s; e++) {
+                        *tc++ = fr[4 * tcs[e].ki + 3];
+                        *tc++ = fr[4 * tcs[e].kj + 3];
+                        otc += 2;
                     }
+                    *tg++ = block_of(r, s);
+                    *tg++ = c0;
+                    *tg++ = (int)(otc / 2);
+                    k = e;
                 }
-                *tg++ = block_of(r, s);
-                *tg++ = c0;
-                *tg++ = (int)(otc / 2);
-                k = e;
-            }
-            sp.tg.resize(tg - sp.tg.data());
-            R.nbt = (int)sp.tg.size() / 3 - R.tbeg;
-            R.rbeg = (int)sp.rtg.size() / 3;
-            for (size_t k = 0; k < rcs.size();) {
-                const int r = rcs[k] < 0 ? -1 : fr[4 * rcs[k]];
-                const int c0 = (int)sp.rc.size() / 2;
-                size_t e = k;
-                for (; e < rcs.size() && (rcs[e] < 0 ? -1 : fr[4 * rcs[e]]) == r; e++) {
-                    const int x = rcs[e];
-                    const int q = x < 0 ? -1 - x : fq[x], v = chosen[q], node = R.node_begin + q;
-                    const int w = x < 0 ? -1 : fr[4 * x + 3];
-                    sp.rc.push_back(w);  // (W id, node slot | pose)
-                    sp.rc.push_back(pol.fused ? q : v);
-                    if (!pol.fused) {
-                        // the owner: the node's first front entry (or its no-target entry)
-                        const bool first = x < 0 || x == 0 || fq[x - 1] != q;
-                        const int r4[4] = {v, x < 0 ? 2 * v : code(x), w, first ? node : -1};
-                        sp.rc4.insert(sp.rc4.end(), r4, r4 + 4);
+                sp.tg.resize(tg - sp.tg.data());
+                R.nbt = (int)sp.tg.size() / 3 - R.tbeg;
+                R.rbeg = (int)sp.rtg.size() / 3;
+                for (size_t k = 0; k < rcs.size();) {
+                    const int r = fr[4 * rcs[k]];
+                    const int c0 = (int)sp.rc.size() / 2;
+                    size_t e = k;
+                    for (; e < rcs.size() && fr[4 * rcs[e]] == r; e++) {
+                        sp.rc.push_back(fr[4 * rcs[e] + 3]);
+                        sp.rc.push_back(fq[rcs[e]]);
                     }
+                    sp.rtg.push_back(r);
+                    sp.rtg.push_back(c0);
+                    sp.rtg.push_back((int)sp.rc.size() / 2);
+                    k = e;
                 }
-                sp.rtg.push_back(r);
-                sp.rtg.push_back(c0);
-                sp.rtg.push_back((int)sp.rc.size() / 2);
-                k = e;
-            }
-            R.nrt = (int)sp.rtg.size() / 3 - R.rbeg;
-            if (!pol.fused) {
-                // the round's target records (block targets, then RHS targets), the first
-                // kSpInline contributions inline
-                sp.inl.reserve(sp.inl.size() + (size_t)kSpRec * (R.nbt + R.nrt));
-                auto record = [&](const int* T_, const std::vector<int>& lst, int w) {
-                    int d[kSpRec];  // (appended whole: no zero fill of the list first)
-                    d[0] = T_[0];
-                    d[1] = T_[1];
-                    d[2] = T_[2];
+                R.nrt = (int)sp.rtg.size() / 3 - R.rbeg;
+            } else {
+                // multi-launch rounds (sp_round_kernel): one kSpRec record per target, block
+                // targets then RHS targets, the first kSpInline contributions inline; only the
+                // rest go to tc3 / rc4, and a record's {c0, c1} is set so that contribution
+                // k >= kSpInline is list entry c0 + k
+                auto emit = [&](int tgt, int cnt, std::vector<int>& lst, int w, auto put) {
+                    if (sp.inl.size() < sp.ninl + kSpRec)
+                        sp.inl.resize(std::max(2 * sp.inl.size(), sp.ninl + (size_t)kSpRec * 256));
+                    int* d = &sp.inl[sp.ninl];
+                    sp.ninl += kSpRec;
+                    const int ovf = (int)(lst.size() / w);
+                    d[0] = tgt;
+                    d[1] = ovf - kSpInline;
+                    d[2] = ovf - kSpInline + cnt;
                     d[3] = 0;
-                    for (int k = 0; k < kSpInline; k++) {
-                        int* c = d + 4 + 4 * k;
-                        const bool have = T_[1] + k < T_[2];
-                        for (int f = 0; f < 4; f++) c[f] = have && f < w ? lst[(size_t)w * (T_[1] + k) + f] : 0;
+                    for (int j = 0; j < std::min(cnt, kSpInline); j++) put(j, d + 4 + 4 * j);
+                    for (int j = kSpInline; j < cnt; j++) {
+                        int c[4];
+                        put(j, c);
+                        lst.insert(lst.end(), c, c + w);
                     }
-                    sp.inl.insert(sp.inl.end(), d, d + kSpRec);
                 };
-                for (int t = 0; t < R.nbt; t++) record(&sp.tg[3 * (R.tbeg + t)], sp.tc3, 3);
-                for (int t = 0; t < R.nrt; t++) record(&sp.rtg[3 * (R.rbeg + t)], sp.rc4, 4);
+                R.tbeg = ntg_total;
+                R.nbt = 0;
+                for (size_t k = 0; k < n;) {
+                    const int r = fr[4 * tcs[k].ki], s = fr[4 * tcs[k].kj];
+                    size_t e = k;
+                    while (e < n && fr[4 * tcs[e].ki] == r && fr[4 * tcs[e].kj] == s) e++;
+                    emit(block_of(r, s), (int)(e - k), sp.tc3, 3, [&](int j, int* c) {
+                        const int ki = tcs[k + j].ki, kj = tcs[k + j].kj;
+                        c[0] = chosen[fq[ki]];
+                        c[1] = code(ki);
+                        c[2] = code(kj);
+                        c[3] = 0;
+                    });
+                    R.nbt++;
+                    k = e;
+                }
+                R.rbeg = nrtg_total;
+                R.nrt = 0;
+                for (size_t k = 0; k < rcs.size();) {
+                    const int r = rcs[k] < 0 ? -1 : fr[4 * rcs[k]];
+                    size_t e = k;
+                    while (e < rcs.size() && (rcs[e] < 0 ? -1 : fr[4 * rcs[e]]) == r) e++;
+                    emit(r, (int)(e - k), sp.rc4, 4, [&](int j, int* c) {
+                        const int x = rcs[k + j];
+                        const int q = x < 0 ? -1 - x : fq[x], v = chosen[q];
+                        // (v, code_r, W id | -1, owner node | -1): the owner is the node's first
+                        // front entry (or its no-target entry)
+                        const bool first = x < 0 || x == 0 || fq[x - 1] != q;
+                        c[0] = v;
+                        c[1] = x < 0 ? 2 * v : code(x);
+                        c[2] = x < 0 ? -1 : fr[4 * x + 3];
+                        c[3] = first ? R.node_begin + q : -1;
+                    });
+                    R.nrt++;
+                    k = e;
+                }
+                ntg_total += R.nbt;
+                nrtg_total += R.nrt;
             }
         }
         R.wcount = sp.nW - R.wbeg;
@@ -367,7 +403,7 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
     sp.zero_blk = sp.nblocks++;  // an all-zero block (zeroed with the fill blocks)
     sp.npad_tail = sp.ntail > 0 ? (int)sp_align_up((size_t)sp.ntail * 7, kCholTile) : 0;
     sp.tmap.assign((size_t)sp.ntail * sp.ntail, -1);
-    for (int i = 0; i < sp.ntail; i++)
+    for (int i = 0; i < (symbolic ? 0 : sp.ntail); i++)
         for (int j = 0; j < sp.ntail; j++) {
             const int x = sp.tail[i], y = sp.tail[j];
             int code = -1;

@@ -180,7 +180,7 @@ def test_full_size_cfg2_matches_oracle(backend, oracle):
 
 @pytest.mark.parametrize("solver", ["1", "2", "3"])
 @pytest.mark.parametrize("topo", ["cfg3", "cfg4", "chain", "star", "clique", "clique27", "clique28",
-                                  "clique4", "clique8", "clique17", "clique21"])
+                                  "clique4", "clique8", "clique17", "clique21", "hub"])
 def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, solver):
     """The block-sparse solvers against the dense blocked Cholesky (M3S_SOLVER_DENSE=1) on the
     same system: one GN step, f64 solves of the same matrix in different orders -> updates
@@ -192,8 +192,14 @@ def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, sol
     pinned pose (poses without fronts) and cliques (no independent low-degree set: dense tail
     only; 27 non-pinned poses = the largest in-register tail, 189 unknowns in 12 x 12 tiles of
     16x16; 28 = beyond it; 3 / 7 / 11 / 16 / 20 poses: tails of 2 / 4 / 6 / 8 / 10 tile rows, so
-    every instantiated tile map -- dealt to the waves by MFMA work -- is exercised)."""
-    if topo == "chain":
+    every instantiated tile map -- dealt to the waves by MFMA work -- is exercised).  "hub": 20
+    poses each linked to the same two hubs, eliminated in one round, so the hub pair's block
+    target and both hubs' RHS targets take 20 contributions -- past a round record's 9 inline
+    ones (sparse_plan.h: the rest from the overflow lists)."""
+    if topo == "hub":
+        N = 23
+        und = [(0, 1), (1, 2)] + [(h, k) for k in range(3, N) for h in (1, 2)]
+    elif topo == "chain":
         N = 24
         und = [(k - 1, k) for k in range(1, N)]
     elif topo == "star":
@@ -203,7 +209,7 @@ def test_sparse_elimination_matches_dense_solver(backend, monkeypatch, topo, sol
         N = {"clique": 12, "clique27": 28, "clique28": 29, "clique4": 4, "clique8": 8, "clique17": 17,
              "clique21": 21}[topo]
         und = [(a, b) for a in range(N) for b in range(a + 1, N)]
-    if topo in ("chain", "star") or topo.startswith("clique"):
+    if topo in ("chain", "star", "hub") or topo.startswith("clique"):
         g = synth.make_graph(dict(N=N, E=len(und)), H=24, W=32, seed=3, edges_only=und)
     else:
         g = synth.make_graph(topo, H=24, W=32, seed=6)
