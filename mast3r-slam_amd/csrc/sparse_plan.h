@@ -402,19 +402,21 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
     sp.ntail = (int)sp.tail.size();
     sp.zero_blk = sp.nblocks++;  // an all-zero block (zeroed with the fill blocks)
     sp.npad_tail = sp.ntail > 0 ? (int)sp_align_up((size_t)sp.ntail * 7, kCholTile) : 0;
+    // the core's block map: code 2 block + (row pose > column pose); the tail is ascending, so
+    // the upper triangle reads bidm row by row and the lower one mirrors it
     sp.tmap.assign((size_t)sp.ntail * sp.ntail, -1);
-    for (int i = 0; i < (symbolic ? 0 : sp.ntail); i++)
-        for (int j = 0; j < sp.ntail; j++) {
-            const int x = sp.tail[i], y = sp.tail[j];
-            int code = -1;
-            if (x == y) {
-                code = 2 * x;
-            } else {
-                const int id = bidm[(size_t)std::min(x, y) * npose + std::max(x, y)];
-                if (id >= 0) code = 2 * id + (x > y ? 1 : 0);
+    for (int i = 0; i < (symbolic ? 0 : sp.ntail); i++) {
+        const int x = sp.tail[i];
+        sp.tmap[(size_t)i * sp.ntail + i] = 2 * x;
+        const int* brow = &bidm[(size_t)x * npose];
+        for (int j = i + 1; j < sp.ntail; j++) {
+            const int id = brow[sp.tail[j]];
+            if (id >= 0) {
+                sp.tmap[(size_t)i * sp.ntail + j] = 2 * id;
+                sp.tmap[(size_t)j * sp.ntail + i] = 2 * id + 1;
             }
-            sp.tmap[(size_t)i * sp.ntail + j] = code;
         }
+    }
     sp.fused_tail = sp.ntail * 7 <= kTailMax;
     sp.fused = pol.fused && sp.fused_tail;
     sp.nints_back = sp.nodes.size() + sp.fptr.size() + sp.fronts.size() + sp.tail.size() +
