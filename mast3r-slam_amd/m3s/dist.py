@@ -41,7 +41,8 @@ def comm_size(comm) -> int:
 
 
 class RcclComm:
-    """Backend-owned RCCL communicator for the per-iteration Hessian all-reduce."""
+    """Backend-owned RCCL communicator for the op's per-iteration exchange (an all-gather of the
+    ranks' f64 per-edge records; M3S_GN_GATHER=0: the all-reduce of the assembled systems)."""
 
     def __init__(self, rank: int, world: int, group=None, device=None):
         idb = torch.zeros(128, dtype=torch.uint8)
