@@ -6,6 +6,7 @@ path sum ~10^5 fp32 terms per entry in different orders (the HIP path accumulate
 pre-adjoint Jacobian and applies the adjoint in f64), so entries agree to ~1e-6 of the
 largest entry; the solved pose updates then agree far below the 1e-5 pose tolerance.
 """
+import dataclasses
 import os
 
 import numpy as np
@@ -678,3 +679,24 @@ def test_dataflow_factor_with_cus_held_by_another_stream(backend, monkeypatch, n
     else:
         assert np.array_equal(T_h, T_ref) and np.array_equal(dx_h, dx_ref)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_degenerate_graphs_leave_poses_and_match_oracle(backend, oracle, mode):
+    """Degenerate pose graphs through the whole op (host plan, pre-passes, solve): no edges at all
+    (an all-zero system: the Cholesky fails -> dx = 0, poses unchanged, as SimplicialLLT's
+    failure path), and a graph whose only edges are self-edges and duplicates of one pair."""
+    g = synth.make_graph(dict(N=3, E=1), H=24, W=32, seed=3, edges_only=[(0, 1)])
+    empty = lambda t: t[:0].contiguous()
+    g0 = dataclasses.replace(g, ii=empty(g.ii), jj=empty(g.jj), idx=empty(g.idx), valid=empty(g.valid),
+                             Q=empty(g.Q))
+    T, dx = _run_gpu(backend, g0, mode, 3)
+    assert np.array_equal(T, g.Twc.numpy())
+    assert dx is None or not np.any(dx)
+    # duplicates of (0, 1) in both directions and a self-edge on pose 2
+    und = [(0, 1), (0, 1), (2, 2)]
+    g2 = synth.make_graph(dict(N=3, E=len(und)), H=24, W=32, seed=4, edges_only=und)
+    T2, _ = _run_gpu(backend, g2, mode, 2)
+    T_o, _, _ = _run_oracle(oracle, g2, mode, 2)
+    assert np.isfinite(T2).all()
+    assert _rel(T2, T_o) < 1e-5, _rel(T2, T_o)

@@ -1,0 +1,8 @@
+#!/bin/bash
+# degenerate-graph GN tests
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r05z
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_gn.py -k "degenerate or hub" > $O/pytest.log 2>&1 || { echo "pytest rc=$?"; tail -40 $O/pytest.log; exit 1; }
+grep -E "PASS|FAIL" $O/pytest.log | tail -10
