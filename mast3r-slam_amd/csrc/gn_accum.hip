@@ -1027,6 +1027,14 @@ __device__ __forceinline__ void accum_steps(const float* __restrict__ Xj_b, cons
 #ifndef M3S_ACC_WAVES
 #define M3S_ACC_WAVES 1
 #endif
+// the rays iteration kernel's occupancy floor (A/B builds; 1 = the compiler's choice)
+#ifndef M3S_ACC_WAVES_RAYS
+#define M3S_ACC_WAVES_RAYS M3S_ACC_WAVES
+#endif
+template <int MODE, bool FIRST>
+constexpr int acc_waves() {
+    return (MODE == GN_RAYS && !FIRST) ? M3S_ACC_WAVES_RAYS : M3S_ACC_WAVES;
+}
 // FIRST (calib, the positional stream): the first iteration of a call, building the packed
 // records from the reference's inputs on the way (RawSrc; no separate gn_pack_kernel pass).
 struct FirstSrc {
@@ -1037,7 +1045,7 @@ struct FirstSrc {
 };
 
 template <int MODE, bool COMPACT, bool RCOK = false, bool FIRST = false>
-__global__ __launch_bounds__(kAccThreads) __attribute__((amdgpu_waves_per_eu(M3S_ACC_WAVES)))
+__global__ __launch_bounds__(kAccThreads) __attribute__((amdgpu_waves_per_eu(acc_waves<MODE, FIRST>())))
 void gn_accum_packed_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Zs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, const int4* __restrict__ pack,
