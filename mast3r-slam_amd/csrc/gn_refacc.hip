@@ -5,7 +5,7 @@
 // do it (gn_kernels.cu:813-1138, 1231-1543, 455-723):
 //   * one 256-thread workgroup per directed edge, thread t owning points t, t+256, ...
 //     (GPU_1D_KERNEL_LOOP, :31-32), one serial fp32 chain per thread and Hessian entry;
-//   * the reference's per-point formulas: IEEE 1.0/x in double, logf(zj) - logf(zi), the
+//   * the reference's per-point formulas: IEEE 1.0/x in double (as the equal f32 quotient), logf(zj) - logf(zi), the
 //     compare-select Huber weight in double, sqrtf, the Jacobian pushed through
 //     apply_Sim3_adj_inv(T_i) for EVERY point (:277-297), Ji = -Jj;
 //   * the 256 partials reduced by blockReduce's tree (256 -> 128 -> 64 -> 32 -> ... -> 1,
@@ -43,13 +43,21 @@ namespace {
 __device__ __forceinline__ float huber_ref(float r, int variant = 0) {
     const float r_abs = fabsf(r);
     if (variant & kRefVarHuberMin) return fminf(1.345f * __builtin_amdgcn_rcpf(r_abs), 1.0f);
-    return (double)r_abs < 1.345 ? 1.0f : (float)(1.345 / (double)r_abs);
+    // the quotient unconditionally, then a select: the point math stays one basic block, so the
+    // scheduler can interleave the unrolled points (gn_accum_ref_kernel)
+    const double d = (double)r_abs;
+    const float q = (float)(1.345 / d);
+    return d < 1.345 ? 1.0f : q;
 }
 
-// (float)(1.0 / (double)x) -- or, diagnostic variant kRefVarRcp, the hardware v_rcp_f32
+// (float)(1.0 / (double)x) -- or, diagnostic variant kRefVarRcp, the hardware v_rcp_f32.  Computed
+// as the IEEE single-precision quotient 1.0f / x: a float quotient rounded to double and then to
+// float equals the correctly rounded float quotient (double rounding is innocuous for division
+// when the intermediate has >= 2p + 2 bits: 53 >= 2 * 24 + 2), at about half the f64 sequence's
+// cost (matching.hip inv_f, the same identity)
 __device__ __forceinline__ float inv_ref(float x, int variant) {
     if (variant & kRefVarRcp) return __builtin_amdgcn_rcpf(x);
-    return (float)(1.0 / (double)x);
+    return __fdiv_rn(1.0f, x);
 }
 
 // gn_kernels.cu:277-297: Y = X Adj(T_i)^{-1} for a row vector X; Y[3..5] += s_inv (...) and
@@ -68,34 +76,63 @@ __device__ __forceinline__ void adj_inv_ref(const Sim3f& Ti, float s_inv, const 
     Y[6] = cmad<CM>(s_inv, cdot3<CM>(Ti.t[0], Ra[0], Ti.t[1], Ra[1], Ti.t[2], Ra[2]), X[6]);
 }
 
+// points per thread evaluated together before their rows are accumulated (A/B: -DM3S_REF_UNROLL=n).
+// 1: 2, 3 and 4 measured 4-6 % slower on cfg3 (profiles/r05_af_refacc/), bitwise the same sums
+#ifndef M3S_REF_UNROLL
+#define M3S_REF_UNROLL 1
+#endif
+constexpr int kRefUnroll = M3S_REF_UNROLL;
+
 struct RefAcc {
     float D[7][7];
     float g[7];
 };
 
-// One residual row: Jj = J Adj^{-1}, then hij += (w Jx[n]) Jx[m], vj += (w e) Jj[n]
-// (gn_kernels.cu:999-1013 and the two loops after it) on the 49 + 7 distinct chains.
-template <int CM>
-__device__ __forceinline__ void accum_row_ref(RefAcc& a, const Sim3f& Ti, float s_inv, const float* J,
-                                              float w, float err) {
-    float Jj[7];
-    adj_inv_ref<CM>(Ti, s_inv, J, Jj);
+// The residual rows of one point: Jj = J Adj^{-1} (gn_kernels.cu:999-1000), the weight and the
+// error per row -- all of the point's math, none of its accumulation
+template <int MODE>
+constexpr int ref_nrows() {
+    return MODE == GN_RAYS ? 4 : 3;
+}
+template <int NR>
+struct RefRows {
+    float Jj[NR][7];
+    float w[NR];
+    float err[NR];
+};
+
+template <int CM, int NR>
+__device__ __forceinline__ void set_row(RefRows<NR>& r, int row, const Sim3f& Ti, float s_inv, const float* J,
+                                        float w, float err) {
+    adj_inv_ref<CM>(Ti, s_inv, J, r.Jj[row]);
+    r.w[row] = w;
+    r.err[row] = err;
+}
+
+// hij += (w Jx[n]) Jx[m], vj += (w e) Jj[n] (gn_kernels.cu:1001-1013 and the two loops after it)
+// on the 49 + 7 distinct chains, row after row
+template <int CM, int NR>
+__device__ __forceinline__ void accum_rows_ref(RefAcc& a, const RefRows<NR>& r) {
 #pragma unroll
-    for (int n = 0; n < 7; n++) {
-        const float wj = w * Jj[n];
+    for (int row = 0; row < NR; row++) {
+        const float w = r.w[row];
 #pragma unroll
-        for (int m = 0; m < 7; m++) a.D[n][m] = cmad<CM>(wj, Jj[m], a.D[n][m]);
+        for (int n = 0; n < 7; n++) {
+            const float wj = w * r.Jj[row][n];
+#pragma unroll
+            for (int m = 0; m < 7; m++) a.D[n][m] = cmad<CM>(wj, r.Jj[row][m], a.D[n][m]);
+        }
+        const float we = w * r.err[row];
+#pragma unroll
+        for (int n = 0; n < 7; n++) a.g[n] = cmad<CM>(we, r.Jj[row][n], a.g[n]);
     }
-    const float we = w * err;
-#pragma unroll
-    for (int n = 0; n < 7; n++) a.g[n] = cmad<CM>(we, Jj[n], a.g[n]);
 }
 
 template <int MODE, int CM>
 __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, float si_inv,
                                           const Sim3f& Tij, const float* Xi, const float* Xj,
                                           float q, float ci, float cj, bool vm, int64_t ind,
-                                          RefAcc& a) {
+                                          int variant, RefRows<ref_nrows<MODE>()>& a) {
     float Xj_Ci[3];
     act_sim3<CM>(Tij, Xj, Xj_Ci);  // actSim3 (:207-219)
     float J[7];
@@ -103,10 +140,10 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         // gn_kernels.cu:924-1089
         const float norm2_i = cdot3<CM>(Xi[0], Xi[0], Xi[1], Xi[1], Xi[2], Xi[2]);
         const float norm1_i = sqrtf(norm2_i);
-        const float norm1_i_inv = inv_ref(norm1_i, P.variant);
+        const float norm1_i_inv = inv_ref(norm1_i, variant);
         const float norm2_j = cdot3<CM>(Xj_Ci[0], Xj_Ci[0], Xj_Ci[1], Xj_Ci[1], Xj_Ci[2], Xj_Ci[2]);
         const float norm1_j = sqrtf(norm2_j);
-        const float norm1_j_inv = inv_ref(norm1_j, P.variant);
+        const float norm1_j_inv = inv_ref(norm1_j, variant);
         const float rj[3] = {norm1_j_inv * Xj_Ci[0], norm1_j_inv * Xj_Ci[1], norm1_j_inv * Xj_Ci[2]};
         // rj - ri: a two-product difference (ri = norm1_i_inv Xi enters only here)
         const float err[4] = {cmm<CM>(norm1_j_inv, Xj_Ci[0], -norm1_i_inv, Xi[0]),
@@ -115,8 +152,8 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         const bool valid = vm & (q > P.Q_thresh) & (ci > P.C_thresh) & (cj > P.C_thresh);
         const float sqrt_w_ray = valid ? P.s0_inv * sqrtf(q) : 0.0f;
         const float sqrt_w_dist = valid ? P.s1_inv * sqrtf(q) : 0.0f;
-        float w[4] = {huber_ref(sqrt_w_ray * err[0], P.variant), huber_ref(sqrt_w_ray * err[1], P.variant),
-                      huber_ref(sqrt_w_ray * err[2], P.variant), huber_ref(sqrt_w_dist * err[3], P.variant)};
+        float w[4] = {huber_ref(sqrt_w_ray * err[0], variant), huber_ref(sqrt_w_ray * err[1], variant),
+                      huber_ref(sqrt_w_ray * err[2], variant), huber_ref(sqrt_w_dist * err[3], variant)};
         const float wc_ray = sqrt_w_ray * sqrt_w_ray;
         const float wc_dist = sqrt_w_dist * sqrt_w_dist;
         w[0] *= wc_ray; w[1] *= wc_ray; w[2] *= wc_ray; w[3] *= wc_dist;
@@ -128,22 +165,26 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         const float drx_dPz = ((-Xj_Ci[0]) * Xj_Ci[2]) * norm3_j_inv;
         const float dry_dPz = ((-Xj_Ci[1]) * Xj_Ci[2]) * norm3_j_inv;
         J[0] = drx_dPx; J[1] = drx_dPy; J[2] = drx_dPz; J[3] = 0.0f; J[4] = rj[2]; J[5] = -rj[1]; J[6] = 0.0f;
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[0], err[0]);
+        set_row<CM>(a, 0, Ti, si_inv, J, w[0], err[0]);
         J[0] = drx_dPy; J[1] = dry_dPy; J[2] = dry_dPz; J[3] = -rj[2]; J[4] = 0.0f; J[5] = rj[0]; J[6] = 0.0f;
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[1], err[1]);
+        set_row<CM>(a, 1, Ti, si_inv, J, w[1], err[1]);
         J[0] = drx_dPz; J[1] = dry_dPz; J[2] = drz_dPz; J[3] = rj[1]; J[4] = -rj[0]; J[5] = 0.0f; J[6] = 0.0f;
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[2], err[2]);
+        set_row<CM>(a, 2, Ti, si_inv, J, w[2], err[2]);
         J[0] = rj[0]; J[1] = rj[1]; J[2] = rj[2]; J[3] = 0.0f; J[4] = 0.0f; J[5] = 0.0f; J[6] = norm1_j;
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[3], err[3]);
+        set_row<CM>(a, 3, Ti, si_inv, J, w[3], err[3]);
     } else if constexpr (MODE == GN_CALIB) {
         // gn_kernels.cu:1360-1495
-        const int u_target = (int)(ind % P.width);
-        const int v_target = (int)(ind / P.width);
+        // ind in [0, HW), HW < 2^31: the 32-bit quotient (the same integers as the 64-bit one)
+        const int v_target = (int)ind / P.width;
+        const int u_target = (int)ind - v_target * P.width;
         const bool valid_z = (Xj_Ci[2] > P.z_eps) && (Xi[2] > P.z_eps);
-        const float zj_inv = valid_z ? inv_ref(Xj_Ci[2], P.variant) : 0.0f;
-        float zj_log = valid_z ? logf(Xj_Ci[2]) : 0.0f;
-        float zi_log = valid_z ? logf(Xi[2]) : 0.0f;
-        if (P.variant & kRefVarLogRatio) {  // the fast path's ln2 * log2(zj / zi) before round 2
+        // evaluated unconditionally and selected (no branch in the point math)
+        const float zj_inv_all = inv_ref(Xj_Ci[2], variant);
+        const float zj_log_all = logf(Xj_Ci[2]), zi_log_all = logf(Xi[2]);
+        const float zj_inv = valid_z ? zj_inv_all : 0.0f;
+        float zj_log = valid_z ? zj_log_all : 0.0f;
+        float zi_log = valid_z ? zi_log_all : 0.0f;
+        if (variant & kRefVarLogRatio) {  // the fast path's ln2 * log2(zj / zi) before round 2
             zj_log = valid_z ? 0.69314718055994531f * __builtin_amdgcn_logf(Xj_Ci[2] * __builtin_amdgcn_rcpf(Xi[2]))
                              : 0.0f;
             zi_log = 0.0f;
@@ -159,8 +200,8 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
                            valid_v & valid_z;
         const float sqrt_w_pixel = valid ? P.s0_inv * sqrtf(q) : 0.0f;
         const float sqrt_w_depth = valid ? P.s1_inv * sqrtf(q) : 0.0f;
-        float w[3] = {huber_ref(sqrt_w_pixel * err[0], P.variant), huber_ref(sqrt_w_pixel * err[1], P.variant),
-                      huber_ref(sqrt_w_depth * err[2], P.variant)};
+        float w[3] = {huber_ref(sqrt_w_pixel * err[0], variant), huber_ref(sqrt_w_pixel * err[1], variant),
+                      huber_ref(sqrt_w_depth * err[2], variant)};
         const float wc_pixel = sqrt_w_pixel * sqrt_w_pixel;
         const float wc_depth = sqrt_w_depth * sqrt_w_depth;
         w[0] *= wc_pixel; w[1] *= wc_pixel; w[2] *= wc_depth;
@@ -168,28 +209,28 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
         J[0] = fx * zj_inv; J[1] = 0.0f; J[2] = ((-fx) * x_div_z) * zj_inv;
         J[3] = ((-fx) * x_div_z) * y_div_z; J[4] = fx * cmad<CM>(x_div_z, x_div_z, 1.0f);
         J[5] = (-fx) * y_div_z; J[6] = 0.0f;
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[0], err[0]);
+        set_row<CM>(a, 0, Ti, si_inv, J, w[0], err[0]);
         J[0] = 0.0f; J[1] = fy * zj_inv; J[2] = ((-fy) * y_div_z) * zj_inv;
         J[3] = (-fy) * cmad<CM>(y_div_z, y_div_z, 1.0f); J[4] = (fy * x_div_z) * y_div_z;
         J[5] = fy * x_div_z; J[6] = 0.0f;
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[1], err[1]);
+        set_row<CM>(a, 1, Ti, si_inv, J, w[1], err[1]);
         J[0] = 0.0f; J[1] = 0.0f; J[2] = zj_inv; J[3] = y_div_z; J[4] = -x_div_z; J[5] = 0.0f; J[6] = 1.0f;
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[2], err[2]);
+        set_row<CM>(a, 2, Ti, si_inv, J, w[2], err[2]);
     } else {
         // point_align_kernel, gn_kernels.cu:564-674
         const float err[3] = {Xj_Ci[0] - Xi[0], Xj_Ci[1] - Xi[1], Xj_Ci[2] - Xi[2]};
         const bool valid = vm & (q > P.Q_thresh) & (ci > P.C_thresh) & (cj > P.C_thresh);
         const float sqrt_w_point = valid ? P.s0_inv * sqrtf(q) : 0.0f;
-        float w[3] = {huber_ref(sqrt_w_point * err[0], P.variant), huber_ref(sqrt_w_point * err[1], P.variant),
-                      huber_ref(sqrt_w_point * err[2], P.variant)};
+        float w[3] = {huber_ref(sqrt_w_point * err[0], variant), huber_ref(sqrt_w_point * err[1], variant),
+                      huber_ref(sqrt_w_point * err[2], variant)};
         const float wc = sqrt_w_point * sqrt_w_point;
         w[0] *= wc; w[1] *= wc; w[2] *= wc;
         J[0] = 1.0f; J[1] = 0.0f; J[2] = 0.0f; J[3] = 0.0f; J[4] = Xj_Ci[2]; J[5] = -Xj_Ci[1]; J[6] = Xj_Ci[0];
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[0], err[0]);
+        set_row<CM>(a, 0, Ti, si_inv, J, w[0], err[0]);
         J[0] = 0.0f; J[1] = 1.0f; J[2] = 0.0f; J[3] = -Xj_Ci[2]; J[4] = 0.0f; J[5] = Xj_Ci[0]; J[6] = Xj_Ci[1];
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[1], err[1]);
+        set_row<CM>(a, 1, Ti, si_inv, J, w[1], err[1]);
         J[0] = 0.0f; J[1] = 0.0f; J[2] = 1.0f; J[3] = Xj_Ci[1]; J[4] = -Xj_Ci[0]; J[5] = 0.0f; J[6] = Xj_Ci[2];
-        accum_row_ref<CM>(a, Ti, si_inv, J, w[2], err[2]);
+        set_row<CM>(a, 2, Ti, si_inv, J, w[2], err[2]);
     }
 }
 
@@ -197,7 +238,9 @@ __device__ __forceinline__ void point_ref(const RefParams& P, const Sim3f& Ti, f
 
 // One workgroup per local directed edge; out[e * kRefStride + 0..48] = D (row-major),
 // out[.. + 49..55] = g, the blockReduce'd f32 sums.
-template <int MODE, int CM>
+// VAR: the diagnostic formula variants (RefParams::variant) are read at run time; the parity
+// build (VAR = false) has none, so its point math carries no uniform branches between the points
+template <int MODE, int CM, bool VAR>
 __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
     const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
     const int* __restrict__ ii_loc, const int* __restrict__ jj_loc, EdgeSrc es, RefParams P,
@@ -230,13 +273,31 @@ __global__ __launch_bounds__(kAccThreads) void gn_accum_ref_kernel(
         for (int m = 0; m < 7; m++) a.D[n][m] = 0.0f;
         a.g[n] = 0.0f;
     }
-    for (int64_t k = tid; k < HW; k += kAccThreads) {
-        const bool vm = valid[k] != 0;
-        int64_t ind = vm ? idx[k] : 0;
-        if ((uint64_t)ind >= (uint64_t)HW) ind = HW - 1;  // the reference reads out of bounds
-        const float Xi[3] = {Xi_b[ind * 3], Xi_b[ind * 3 + 1], Xi_b[ind * 3 + 2]};
-        const float Xj[3] = {Xj_b[k * 3], Xj_b[k * 3 + 1], Xj_b[k * 3 + 2]};
-        point_ref<MODE, CM>(P, Ti, si_inv, Tij, Xi, Xj, Q[k], Ci_b[ind], Cj_b[k], vm, ind, a);
+    // The thread's points k, k + 256, ... in order, U at a time: the U points' math first (one
+    // basic block, no branch: the diagnostic variants are compiled out, the selects evaluate
+    // both sides), then their rows accumulated in point order, so every chain sums the same
+    // terms in the same order whatever U.
+    constexpr int U = kRefUnroll;
+    constexpr int NR = ref_nrows<MODE>();
+    for (int64_t k0 = tid; k0 < HW; k0 += U * kAccThreads) {
+        RefRows<NR> rows[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            // a point past the end is evaluated on the last point's inputs and not accumulated
+            const int64_t k = min(k0 + (int64_t)u * kAccThreads, HW - 1);
+            const bool vm = valid[k] != 0;
+            const int64_t id = idx[k];  // loaded beside valid[k], not after it
+            int64_t ind = vm ? id : 0;
+            if ((uint64_t)ind >= (uint64_t)HW) ind = HW - 1;  // the reference reads out of bounds
+            const float Xi[3] = {Xi_b[ind * 3], Xi_b[ind * 3 + 1], Xi_b[ind * 3 + 2]};
+            const float Xj[3] = {Xj_b[k * 3], Xj_b[k * 3 + 1], Xj_b[k * 3 + 2]};
+            point_ref<MODE, CM>(P, Ti, si_inv, Tij, Xi, Xj, Q[k], Ci_b[ind], Cj_b[k], vm, ind, VAR ? P.variant : 0,
+                                rows[u]);
+        }
+        accum_rows_ref<CM>(a, rows[0]);
+#pragma unroll
+        for (int u = 1; u < U; u++)
+            if (k0 + (int64_t)u * kAccThreads < HW) accum_rows_ref<CM>(a, rows[u]);
     }
 
     // blockReduce (gn_kernels.cu:36-55) of all 56 chains at once: level o adds s[t + o] into
@@ -315,9 +376,15 @@ hipError_t launch_accum_ref(int mode, int E_local, hipStream_t st, const float* 
                             const float* Cs, const int* ii_loc, const int* jj_loc, const EdgeSrc& es,
                             const RefParams& P, float* out, const int* flags) {
     if (E_local <= 0) return hipSuccess;
-#define M3S_REF(MODE, CM)                                                                              \
-    hipLaunchKernelGGL((gn_accum_ref_kernel<MODE, CM>), dim3(E_local), dim3(kAccThreads), 0, st, Twc, Xs, \
-                       Cs, ii_loc, jj_loc, es, P, out, flags)
+#define M3S_REF(MODE, CM)                                                                                   \
+    do {                                                                                                    \
+        if (P.variant)                                                                                      \
+            hipLaunchKernelGGL((gn_accum_ref_kernel<MODE, CM, true>), dim3(E_local), dim3(kAccThreads), 0, st, \
+                               Twc, Xs, Cs, ii_loc, jj_loc, es, P, out, flags);                             \
+        else                                                                                                \
+            hipLaunchKernelGGL((gn_accum_ref_kernel<MODE, CM, false>), dim3(E_local), dim3(kAccThreads), 0, st, \
+                               Twc, Xs, Cs, ii_loc, jj_loc, es, P, out, flags);                             \
+    } while (0)
 #define M3S_REF_MODES(CM)                     \
     if (mode == GN_RAYS) M3S_REF(GN_RAYS, CM); \
     else if (mode == GN_CALIB) M3S_REF(GN_CALIB, CM); \
