@@ -20,6 +20,7 @@
 #include "edge_reduce.h"
 #include "gn_kernels.h"
 #include "sim3.h"
+#include "wave_reduce.h"
 
 // Scheduling of the 4 points of a lane's step (AccStage::compute): 0 (default; what every
 // measurement so far ran -- the old default of 1 sat below its first use and never applied) lets
@@ -364,30 +365,6 @@ __device__ __forceinline__ int pack_code(int ind, bool ok, const AccParams& P) {
         c = (int)(q << 16) | (ind - (int)q * P.width);
     }
     return ok ? c : (int)((unsigned)c | 0x80000000u);
-}
-
-// Half exchanges of two registers (gfx950 v_permlane32_swap / v_permlane16_swap): afterwards
-// a + b holds, in the first half (row pair) of the lanes, a's partial sums and in the second
-// b's -- a reduce-scatter step that costs one swap + one add for two values.
-__device__ __forceinline__ float halfsum32(float a, float b) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float halfsum16(float a, float b) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-// sum over the 16 lanes of each row (every lane of the row gets it): DPP row rotations
-template <int N>
-__device__ __forceinline__ float row_ror(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x120 + N, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float row_sum16(float v) {
-    v += row_ror<8>(v);
-    v += row_ror<4>(v);
-    v += row_ror<2>(v);
-    v += row_ror<1>(v);
-    return v;
 }
 
 // Deterministic workgroup reduction of the 35 sums, one 36-float partial per (edge, chunk).

@@ -5,12 +5,12 @@
 // whitened Jacobian A [4HW | 3HW, 7] and residual b with ~30 torch kernels, forms
 // H = A^T A, g = -A^T b, synchronises on cost.item(), factors H with
 // torch.linalg.cholesky and retracts with lietorch.  Here an iteration is two launches:
-//   track_accum_kernel  a few points per thread: residual and Jacobian (point_to_ray_dist |
+//   track_accum_kernel  one point per thread: residual and Jacobian (point_to_ray_dist |
 //                       project_calib, act_Sim3; geometry.py:17-104), the huber-robustified
 //                       sqrt-information (tracker.py:156-163), and the 28 + 7 unique entries
-//                       of H, g plus the cost, reduced per workgroup (wave butterfly, fixed
+//                       of H, g plus the cost, reduced per workgroup (reduce-scatter, fixed
 //                       order) -> one 36-float partial per workgroup
-//   track_step_kernel   one wave: f64 sum of the partials in a fixed order, 7x7 Cholesky
+//   track_step_kernel   f64 sums of the partials in a fixed order (1008 threads), 7x7 Cholesky
 //                       solve (tracker.py:164-169, in f64), T_CkCf <- Exp(tau) T_CkCf
 //                       (lietorch retr), check_convergence (nonlinear_optimizer.py:5-25) ->
 //                       a device flag that turns the remaining iterations into no-ops
@@ -31,12 +31,13 @@
 #include "../../include/m3s_backend.h"
 #include "m3s_common.h"
 #include "sim3.h"
+#include "wave_reduce.h"
 
 namespace m3s {
 namespace {
 
 constexpr int kTrkThreads = 256;
-constexpr int kTrkPPT = 4;  // points per thread
+constexpr int kTrkPPT = 1;  // points per thread (4 measured 2x slower: 192 workgroups, 4 dependent trips)
 constexpr int kTrkNacc = 36;  // H upper triangle 28, g 7, sum of b^2
 constexpr int kTrkMaxBlocks = 4096;
 
@@ -56,6 +57,10 @@ struct TrkParams {
     float delta_norm;
     int max_iters;
 };
+
+// the partials are value-major, [kTrkNacc][ldp] with the row stride padded to 4 blocks, so the
+// step kernel reads each value's blocks as float4 runs
+__host__ __device__ inline int track_ldp(int nblk) { return (nblk + 3) & ~3; }
 
 int track_blocks(int64_t HW) {
     const int64_t per = (int64_t)kTrkThreads * kTrkPPT;
@@ -149,7 +154,10 @@ __global__ __launch_bounds__(kTrkThreads) void track_accum_kernel(
     const uint8_t* __restrict__ valid, const float* __restrict__ meas,
     const uint8_t* __restrict__ vmeas, const float* __restrict__ K, const TrackState* __restrict__ st,
     TrkParams P, float* __restrict__ partials) {
-    if (st->done) return;
+    // the done flag is loaded with the pose and checked only after the point's loads and math, so
+    // a live iteration does not wait one memory round trip for the flag before its loads (a
+    // finished one computes its one point per thread and drops it)
+    const bool done = st->done != 0;
     __shared__ float red[kTrkThreads / 64][kTrkNacc];
     float T[8];
 #pragma unroll
@@ -220,21 +228,24 @@ __global__ __launch_bounds__(kTrkThreads) void track_accum_kernel(
             trk_row(acc, J, trk_robust(si_z, r2, P.k), r2);
         }
     }
-    // workgroup reduction in a fixed order: wave butterfly, then the 4 waves in order
+    if (done) return;
+    // workgroup reduction in a fixed order: per wave a reduce-scatter (wave_reduce.h), then the
+    // 4 waves in order; the partial goes to column blockIdx.x of the value-major [36][ldp] table
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    static_assert(kTrkNacc == 36, "wave_sum36 is laid out for 36 values");
+    float x[9];
+    wave_sum36(acc, x);
+    if ((lane & 15) == 0) {
+        const int r = lane >> 4;
 #pragma unroll
-    for (int q = 0; q < kTrkNacc; q++) {
-        float s = acc[q];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (lane == 0) red[wave][q] = s;
+        for (int j = 0; j < 9; j++) red[wave][j + 9 * r] = x[j];
     }
     __syncthreads();
     if (threadIdx.x < kTrkNacc) {
         float s = red[0][threadIdx.x];
 #pragma unroll
         for (int w = 1; w < kTrkThreads / 64; w++) s += red[w][threadIdx.x];
-        partials[(int64_t)blockIdx.x * kTrkNacc + threadIdx.x] = s;
+        partials[(int64_t)threadIdx.x * track_ldp(gridDim.x) + blockIdx.x] = s;
     }
 }
 
@@ -258,26 +269,57 @@ __global__ __launch_bounds__(64) void track_init_kernel(const float* __restrict_
     info[0] = info[1] = info[2] = info[3] = 0;
 }
 
-__global__ __launch_bounds__(64) void track_step_kernel(const float* __restrict__ partials, int nblk,
-                                                        TrackState* __restrict__ st, TrkParams P,
-                                                        int* __restrict__ info,
-                                                        double* __restrict__ cost_out) {
-    if (st->done) return;
+// the f64 sum of one value's partials runs as kTrkChains chains of consecutive blocks (one
+// thread each, all its loads issued together: one memory round trip for up to 896 blocks), then
+// the chains in order: a fixed order, so deterministic
+constexpr int kTrkStepThreads = 1024;
+constexpr int kTrkChains = 28;   // 36 x 28 = 1008 of the 1024 threads
+constexpr int kTrkChainVec = 8;  // float4 loads in flight per chain and batch
+
+__global__ __launch_bounds__(kTrkStepThreads) void track_step_kernel(const float* __restrict__ partials, int nblk,
+                                                                 TrackState* __restrict__ st, TrkParams P,
+                                                                 int* __restrict__ info,
+                                                                 double* __restrict__ cost_out) {
+    // the flag, the pose and the old cost are loaded together with the partials (one round trip)
+    const bool done = st->done != 0;
+    float T[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) T[q] = st->T[q];
+    const double old_cost = st->old_cost;
+    const int iters = st->iters, converged0 = st->converged;
     __shared__ double S[kTrkNacc];
+    __shared__ double C[kTrkNacc][kTrkChains];
     const int tid = threadIdx.x;
-    if (tid < kTrkNacc) {
-        // the blocks' partials in block order (deterministic), 16 loads in flight per batch: one
-        // dependent L2 round trip per block made this ~46 us of every tracker iteration
+    if (tid < kTrkNacc * kTrkChains) {
+        // chain c of value q: blocks [b0, b1), b0 a multiple of 4 (16-B aligned float4 runs; a run
+        // may read up to 3 floats past b1 but never past the row's padded end)
+        const int q = tid / kTrkChains, c = tid - q * kTrkChains;
+        const int per = ((nblk + kTrkChains - 1) / kTrkChains + 3) & ~3;
+        const int b0 = min(c * per, nblk), b1 = min(b0 + per, nblk);
+        const float* __restrict__ row = partials + (int64_t)q * track_ldp(nblk);
         double s = 0.0;
-        int b = 0;
-        for (; b + 16 <= nblk; b += 16) {
-            float v[16];
+        for (int b = b0; b < b1; b += 4 * kTrkChainVec) {
+            float4 v[kTrkChainVec];
 #pragma unroll
-            for (int u = 0; u < 16; u++) v[u] = partials[(int64_t)(b + u) * kTrkNacc + tid];
+            for (int u = 0; u < kTrkChainVec; u++)
+                v[u] = b + 4 * u < b1 ? *reinterpret_cast<const float4*>(row + b + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-            for (int u = 0; u < 16; u++) s += (double)v[u];
+            for (int u = 0; u < kTrkChainVec; u++) {
+                const int bb = b + 4 * u;
+                if (bb < b1) s += (double)v[u].x;
+                if (bb + 1 < b1) s += (double)v[u].y;
+                if (bb + 2 < b1) s += (double)v[u].z;
+                if (bb + 3 < b1) s += (double)v[u].w;
+            }
         }
-        for (; b < nblk; b++) s += (double)partials[(int64_t)b * kTrkNacc + tid];
+        C[q][c] = s;
+    }
+    if (done) return;  // uniform: every thread read the same flag
+    __syncthreads();
+    if (tid < kTrkNacc) {
+        double s = C[tid][0];
+#pragma unroll
+        for (int c = 1; c < kTrkChains; c++) s += C[tid][c];
         S[tid] = s;
     }
     __syncthreads();
@@ -296,22 +338,24 @@ __global__ __launch_bounds__(64) void track_step_kernel(const float* __restrict_
     const double cost = 0.5 * S[35];
     // L L^T = H (tracker.py:168); a pivot that is not > 0 (incl. NaN) fails like torch
     bool bad = false;
+    double rinv[7];
     for (int p = 0; p < 7; p++) {
         double d = L[p][p];
         for (int q = 0; q < p; q++) d -= L[p][q] * L[p][q];
         if (!(d > 0.0)) bad = true;
         const double lpp = sqrt(d);
         L[p][p] = lpp;
+        rinv[p] = 1.0 / lpp;  // one division per pivot; the column and both solves multiply
         for (int i = p + 1; i < 7; i++) {
             double a = L[i][p];
             for (int q = 0; q < p; q++) a -= L[i][q] * L[p][q];
-            L[i][p] = a / lpp;
+            L[i][p] = a * rinv[p];
         }
     }
     if (bad) {
         st->failed = 1;
         st->done = 1;
-        info[0] = st->iters;
+        info[0] = iters;
         info[2] = 1;
         cost_out[0] = cost;
         return;
@@ -321,12 +365,12 @@ __global__ __launch_bounds__(64) void track_step_kernel(const float* __restrict_
     for (int i = 0; i < 7; i++) {
         double a = g[i];
         for (int q = 0; q < i; q++) a -= L[i][q] * y[q];
-        y[i] = a / L[i][i];
+        y[i] = a * rinv[i];
     }
     for (int i = 6; i >= 0; i--) {
         double a = y[i];
         for (int q = i + 1; q < 7; q++) a -= L[q][i] * xs[q];
-        xs[i] = a / L[i][i];
+        xs[i] = a * rinv[i];
     }
     float tau[7];
     float nrm2 = 0.0f;
@@ -335,21 +379,21 @@ __global__ __launch_bounds__(64) void track_step_kernel(const float* __restrict_
         nrm2 = fmaf(tau[i], tau[i], nrm2);
     }
     // T_CkCf = T_CkCf.retr(tau) = Exp(tau) * T_CkCf (tracker.py:195, 247)
-    float T[8];
-    for (int q = 0; q < 8; q++) T[q] = st->T[q];
     retr_sim3(tau, T);
     for (int q = 0; q < 8; q++) st->T[q] = T[q];
     // check_convergence (nonlinear_optimizer.py:5-25); inf old cost -> NaN -> not converged
-    const double rel_dec = fabs((st->old_cost - cost) / st->old_cost);
+    const double rel_dec = fabs((old_cost - cost) / old_cost);
     const float delta = sqrtf(nrm2);
     const bool conv = rel_dec < P.rel_error || delta < P.delta_norm;
+    const int it1 = iters + 1;
+    const int converged = conv ? 1 : converged0;
     st->old_cost = cost;
     st->cost = cost;
-    st->iters += 1;
-    if (conv) st->converged = 1;
-    if (conv || st->iters >= P.max_iters) st->done = 1;
-    info[0] = st->iters;
-    info[1] = st->converged;
+    st->iters = it1;
+    st->converged = converged;
+    if (conv || it1 >= P.max_iters) st->done = 1;
+    info[0] = it1;
+    info[1] = converged;
     info[2] = 0;
     cost_out[0] = cost;
 }
@@ -398,7 +442,7 @@ using namespace m3s;
 
 extern "C" size_t m3s_track_workspace_bytes(int64_t HW) {
     if (HW < 1) return 0;
-    return align_up(sizeof(TrackState), 256) + sizeof(float) * kTrkNacc * (size_t)track_blocks(HW);
+    return align_up(sizeof(TrackState), 256) + sizeof(float) * kTrkNacc * (size_t)track_ldp(track_blocks(HW));
 }
 
 extern "C" int m3s_track_sim3(const m3s_track_args* args) {
@@ -452,7 +496,7 @@ extern "C" int m3s_track_sim3(const m3s_track_args* args) {
                                a.Xf, a.Xk, a.Qk, a.valid, a.meas_k, a.valid_meas, a.K, state, P,
                                partials);
         M3S_LAUNCH_CHECK();
-        hipLaunchKernelGGL(track_step_kernel, dim3(1), dim3(64), 0, st, partials, nblk, state, P,
+        hipLaunchKernelGGL(track_step_kernel, dim3(1), dim3(kTrkStepThreads), 0, st, partials, nblk, state, P,
                            a.info, a.cost);
         M3S_LAUNCH_CHECK();
         if ((it + 1) % every == 0 && it + 1 < a.max_iters) {

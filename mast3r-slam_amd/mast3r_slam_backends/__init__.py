@@ -554,8 +554,9 @@ def track_sim3(mode, Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma0, sigma1, huber_k, m
     dev = _on_device(**tens)
     out_f = torch.empty((1, 8), dtype=torch.float32, device=dev)
     out_r = torch.empty((1, 8), dtype=torch.float32, device=dev)
-    info = torch.zeros((4,), dtype=torch.int32, device=dev)
-    cost = torch.zeros((1,), dtype=torch.float64, device=dev)
+    # info (4 int32) and cost (1 f64) share one buffer: one fill, one device-to-host read
+    res = torch.zeros((3,), dtype=torch.float64, device=dev)
+    info, cost = res[:2].view(torch.int32), res[2:]
     ws_bytes = lib.m3s_track_workspace_bytes(HW)
     ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
     a = TrackArgs()
@@ -581,11 +582,12 @@ def track_sim3(mode, Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma0, sigma1, huber_k, m
         a.stream = torch.cuda.current_stream(dev).cuda_stream
         rc = lib.m3s_track_sim3(ctypes.byref(a))
     _raise(rc, "track_sim3")
-    it, _, failed, _ = info.tolist()
+    h = res.cpu()
+    it, _, failed, _ = h[:2].view(torch.int32).tolist()
     if failed:
         raise CholeskyError("track_sim3: normal equations not positive definite "
                             f"(iteration {it + 1})")
-    return out_f, out_r, it, float(cost.item())
+    return out_f, out_r, it, float(h[2])
 
 
 # ---------------------------------------------------------------------------------
