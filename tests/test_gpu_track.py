@@ -89,6 +89,22 @@ def test_track_full_size_with_convergence_test(backend, mode, seed):
     assert _rel(Tf, To) <= 1e-5 and _rel(Tr, Tro) <= 1e-5, (_rel(Tf, To), _rel(Tr, Tro))
 
 
+@pytest.mark.parametrize("hw", [(37, 53), (1152, 1024)])
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_track_ragged_and_large_frames(backend, mode, hw):
+    """The reduction's edge cases: a point count that is not a multiple of the 256-point
+    workgroup (the last one partly empty; 8 partials, fewer than the step's 28 chains), and
+    1.18 M points -- more workgroups than the 4096 cap, so threads take 2 points and each of the
+    step's chains sums several batches of partials.  3 fixed iterations vs the oracle."""
+    p = TO.make_tracking_pair(hw, seed=31, mode=mode, noise=0.003)
+    cfg = dict(CFG, rel_error=0.0, delta_norm=0.0)
+    Tf, Tr, it, cost = _gpu(backend, p, mode, hw, cfg, max_iters=3)
+    To, Tro, ito, costo = _oracle(p, mode, hw, cfg, max_iters=3)
+    assert it == ito == 3
+    assert _rel(Tf, To) <= 1e-5 and _rel(Tr, Tro) <= 1e-5, (_rel(Tf, To), _rel(Tr, Tro))
+    assert abs(cost - costo) <= 1e-4 * abs(costo)
+
+
 @pytest.mark.parametrize("mode", ["rays", "calib"])
 def test_track_converges_like_oracle(backend, mode):
     hw = (96, 128)
