@@ -168,12 +168,11 @@ __device__ __forceinline__ void apply_rel(const RelXf& T, V x0, V x1, V x2, V& X
     X2 = vfma(vsplat(T.m[6], x0), x0, vfma(vsplat(T.m[7], x0), x1, vfma(vsplat(T.m[8], x0), x2, vsplat(T.t[2], x0))));
 }
 
-// One (pair of) point-edge(s): residuals, robust weights, raw rows -> acc.
+// One (pair of) point-edge(s) from its transformed point X = T_ij Xj: residuals, robust
+// weights, raw rows -> acc.
 template <int MODE, typename V>
-__device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T, const AccParams& P,
-                                           V* __restrict__ acc) {
-    V X0, X1, X2;
-    apply_rel(T, p.xj0, p.xj1, p.xj2, X0, X1, X2);
+__device__ __forceinline__ void point_body_x(const PointsIn<V>& p, V X0, V X1, V X2, const AccParams& P,
+                                             V* __restrict__ acc) {
     auto valid = p.valid;
     const V zero = vsplat(0.0f, X0);
     const V sq = p.sq;
@@ -318,6 +317,14 @@ __device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T,
     }
 }
 
+template <int MODE, typename V>
+__device__ __forceinline__ void point_body(const PointsIn<V>& p, const RelXf& T, const AccParams& P,
+                                           V* __restrict__ acc) {
+    V X0, X1, X2;
+    apply_rel(T, p.xj0, p.xj1, p.xj2, X0, X1, X2);
+    point_body_x<MODE, V>(p, X0, X1, X2, P, acc);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -397,6 +404,12 @@ __device__ __forceinline__ void block_partial(const float* accs, float* __restri
     }
 }
 
+
+// The ray-constrained calib stream's transform factored per pixel row (AccStage::compute; A/B
+// builds: -DM3S_RC_FACTOR=0 keeps s M x + t on the rebuilt point, bitwise the positional stream)
+#ifndef M3S_RC_FACTOR
+#define M3S_RC_FACTOR 1
+#endif
 
 // One pipeline stage of the packed accumulate: the records, Xj and the gathered matched points
 // of 4 consecutive points of one lane.
@@ -484,7 +497,23 @@ struct AccStage {
         const int* codes = cd;
         const int* sqb = sb;
         float xj[3 * NP];
-        if constexpr (RC) {  // x = z * ((u - cx) / fx), y = z * ((v - cy) / fy): constrain_points_to_ray
+        // RC_FACTOR: the ray-constrained point is z (tu, tv, 1), so T_ij Xj = z (tu M_0 + B_v) + t
+        // with B_v = tv M_1 + M_2 shared by the lane's NP points (one pixel row): 6 FMAs per point
+        // and 3 per step instead of 2 multiplies + 9 FMAs per point (other roundings than the
+        // positional stream's s M x + t)
+        constexpr bool kFactor = RC && M == GN_CALIB && M3S_RC_FACTOR;
+        float Xr[3 * NP];
+        if constexpr (kFactor) {
+            const float tv = xv[2 * NP];
+            const float B0 = fmaf(T.m[1], tv, T.m[2]), B1 = fmaf(T.m[4], tv, T.m[5]), B2 = fmaf(T.m[7], tv, T.m[8]);
+#pragma unroll
+            for (int s = 0; s < NP; s++) {
+                const float z = xv[s], tu = xv[NP + s];
+                Xr[3 * s] = fmaf(z, fmaf(T.m[0], tu, B0), T.t[0]);
+                Xr[3 * s + 1] = fmaf(z, fmaf(T.m[3], tu, B1), T.t[1]);
+                Xr[3 * s + 2] = fmaf(z, fmaf(T.m[6], tu, B2), T.t[2]);
+            }
+        } else if constexpr (RC) {  // x = z * ((u - cx) / fx), y = z * ((v - cy) / fy): constrain_points_to_ray
 #pragma unroll
             for (int s = 0; s < NP; s++) {
                 xj[3 * s] = xv[s] * xv[NP + s];
@@ -509,12 +538,16 @@ struct AccStage {
                 p.xi1 = g[s][1];
             }
             p.xi2 = g[s][2];
-            p.xj0 = xj[3 * s];
-            p.xj1 = xj[3 * s + 1];
-            p.xj2 = xj[3 * s + 2];
             p.valid = codes[s] >= 0;
             p.sq = __int_as_float(sqb[s]);
-            point_body<M, float>(p, T, P, acc);
+            if constexpr (kFactor) {
+                point_body_x<M, float>(p, Xr[3 * s], Xr[3 * s + 1], Xr[3 * s + 2], P, acc);
+            } else {
+                p.xj0 = xj[3 * s];
+                p.xj1 = xj[3 * s + 1];
+                p.xj2 = xj[3 * s + 2];
+                point_body<M, float>(p, T, P, acc);
+            }
 #if M3S_ACC_SCHED_BARRIER == 1
             __builtin_amdgcn_sched_barrier(0);  // one point's temporaries live at a time
 #elif M3S_ACC_SCHED_BARRIER == 2
@@ -846,7 +879,8 @@ __global__ __launch_bounds__(kAccThreads) void gn_pack_compact_kernel(
 // every point IS its pixel's ray times its depth, bit for bit, i.e. what solve_GN_calib's
 // constrain_points_to_ray (global_opt.py:172, geometry.py:37-42/107-123: z * ((u - cx) / fx))
 // produces.  If so (flag kFlagNotRay stays 0) the accumulate reads Xj as its 4-B depth and
-// rebuilds x, y with the same two roundings -- the identical values, so the identical result.
+// applies T_ij to z (tu, tv, 1) factored per pixel row (M3S_RC_FACTOR; with it off, x and y are
+// rebuilt with the same two roundings and the result is bitwise the positional stream's).
 __global__ __launch_bounds__(256) void gn_depth_kernel(const float* __restrict__ Xs, int64_t total,
                                                        float* __restrict__ Zs, AccParams P,
                                                        int* __restrict__ flags, const float* __restrict__ K) {

@@ -256,8 +256,14 @@ def test_packed_stream_gives_identical_system(backend, monkeypatch, mode):
     H0, b0 = build_system_gpu(g, mode, LOCAL)
     monkeypatch.setenv("M3S_GN_PACK", "2")
     monkeypatch.setenv("M3S_GN_COMPACT", "0")  # the positional stream: same points, same order
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "0")  # (calib: Xj read whole, not rebuilt from its depth)
     H2, b2 = build_system_gpu(g, mode, LOCAL)
     assert np.array_equal(H0, H2) and np.array_equal(b0, b2)
+    if mode == "calib":  # the ray-constrained stream: the same terms up to the transform's rounding
+        monkeypatch.setenv("M3S_GN_RAYCHECK", "1")
+        H4, b4 = build_system_gpu(g, mode, LOCAL)
+        assert np.abs(H4 - H0).max() <= 1e-5 * np.abs(H0).max()
+        assert np.abs(b4 - b0).max() <= 1e-5 * np.abs(b0).max()
     # the compacted stream (M3S_GN_COMPACT=1): dead points dropped, so only the summation
     # grouping moves
     monkeypatch.setenv("M3S_GN_COMPACT", "1")
@@ -289,6 +295,7 @@ def test_confidence_pass_skips_only_passing_keyframes(backend, monkeypatch, mode
     H0, b0 = build_system_gpu(g, mode, Lc)
     monkeypatch.setenv("M3S_GN_PACK", "2")
     monkeypatch.setenv("M3S_GN_COMPACT", "0")
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "0")  # positional Xj: bitwise the direct path's terms
     H2, b2 = build_system_gpu(g, mode, Lc)
     assert np.array_equal(H0, H2, equal_nan=True) and np.array_equal(b0, b2, equal_nan=True)
 
@@ -395,27 +402,45 @@ def test_full_size_cfg3_calib_step_closer_to_exactly_summed_system(backend, orac
     assert np.array_equal(T_gpu, T_r), _rel(T_gpu, T_r)
 
 
+def _ray_path_taken(backend, g, iters, monkeypatch):
+    """Run once more with the device flags read back: did the packed calib accumulate take the
+    ray-constrained stream (Xj read as its depth)?"""
+    import ctypes
+
+    monkeypatch.setenv("M3S_GN_DEBUG_FLAGS", "2")
+    _run_gpu(backend, g, "calib", iters)
+    monkeypatch.delenv("M3S_GN_DEBUG_FLAGS")
+    dbg = (ctypes.c_int * 4)()
+    backend.lib.m3s_gn_debug_flags(dbg)
+    return bool(dbg[3])
+
+
 @pytest.mark.parametrize("iters", [3, 6])
-def test_ray_constrained_calib_path_is_identical(backend, oracle, monkeypatch, iters):
+def test_ray_constrained_calib_path(backend, oracle, monkeypatch, iters):
     """solve_GN_calib hands the op ray-constrained points (global_opt.py:172); the packed calib
-    accumulate then reads Xj as its depth and rebuilds x, y with the same roundings
-    (gn_depth_kernel checks every point bit for bit).  The result must be bitwise the same as
-    with the check disabled, and the path must not be taken for unconstrained points."""
+    accumulate then reads Xj as its depth (gn_depth_kernel checks every point bit for bit) and
+    applies T_ij to z (tu, tv, 1) factored per pixel row (M3S_RC_FACTOR), other roundings than
+    the positional stream's s M x + t: both within 1e-5 of the oracle and of each other to float
+    rounding.  The path must not be taken for unconstrained points (then the result is bitwise
+    the positional stream's)."""
     from m3s.geometry import constrain_points_to_ray
 
     g = synth.make_graph("cfg2", H=96, W=128, mode="calib")
     g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
     monkeypatch.setenv("M3S_GN_RAYCHECK", "1")
     T_rc, _ = _run_gpu(backend, g, "calib", iters)
+    assert _ray_path_taken(backend, g, iters, monkeypatch)
     monkeypatch.setenv("M3S_GN_RAYCHECK", "0")
     T_gen, _ = _run_gpu(backend, g, "calib", iters)
+    assert not _ray_path_taken(backend, g, iters, monkeypatch)
     monkeypatch.setenv("M3S_GN_RAYCHECK", "1")
-    assert np.array_equal(T_rc, T_gen)
     T_o, _, _ = _run_oracle(oracle, g, "calib", iters)
-    assert np.abs(T_rc - T_o).max() / np.abs(T_o).max() < 1e-5
+    assert _rel(T_rc, T_o) < 1e-5 and _rel(T_gen, T_o) < 1e-5, (_rel(T_rc, T_o), _rel(T_gen, T_o))
+    assert _rel(T_rc, T_gen) < 2e-6, _rel(T_rc, T_gen)
     # one point off its ray: the check must fall back (result == generic path on those inputs)
     g.Xs[5, 77, 0] = torch.nextafter(g.Xs[5, 77, 0], torch.tensor(1e9))
     T_fb, _ = _run_gpu(backend, g, "calib", iters)
+    assert not _ray_path_taken(backend, g, iters, monkeypatch)
     monkeypatch.setenv("M3S_GN_RAYCHECK", "0")
     T_fb_gen, _ = _run_gpu(backend, g, "calib", iters)
     assert np.array_equal(T_fb, T_fb_gen)
@@ -424,21 +449,25 @@ def test_ray_constrained_calib_path_is_identical(backend, oracle, monkeypatch, i
 @pytest.mark.parametrize("W", [100, 102, 126])
 def test_pixel_coded_calib_records_at_odd_widths(backend, oracle, monkeypatch, W):
     """The packed calib records carry the match as its pixel (v << 16 | u, decoded with a 24-bit
-    multiply-add): at widths that are not powers of two, with W % 4 == 0 (the ray-constrained
-    path) and W % 4 == 2 (positional Xj), the packed call is bitwise the unpacked one (which
-    decodes flat indices by division) and within 1e-5 of the oracle."""
+    multiply-add): at widths that are not powers of two, the packed call on positional Xj is
+    bitwise the unpacked one (which decodes flat indices by division), and with W % 4 == 0 the
+    ray-constrained stream (its own transform roundings) is within 1e-5 of the oracle too."""
     from m3s.geometry import constrain_points_to_ray
 
     g = synth.make_graph("cfg2", H=48, W=W, mode="calib")
     g.Xs = constrain_points_to_ray((g.H, g.W), g.Xs, g.K).contiguous()
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "0")
     monkeypatch.setenv("M3S_GN_PACK", "2")
     T_p, _ = _run_gpu(backend, g, "calib", 3)
+    monkeypatch.setenv("M3S_GN_RAYCHECK", "1")
+    T_rc, _ = _run_gpu(backend, g, "calib", 3)
     monkeypatch.setenv("M3S_GN_PACK", "0")
     T_u, _ = _run_gpu(backend, g, "calib", 3)
     monkeypatch.setenv("M3S_GN_PACK", "1")
     assert np.array_equal(T_p, T_u)
     T_o, _, _ = _run_oracle(oracle, g, "calib", 3)
     assert np.abs(T_p - T_o).max() / np.abs(T_o).max() < 1e-5
+    assert np.abs(T_rc - T_o).max() / np.abs(T_o).max() < 1e-5
 
 
 def _cfg3_calib_graph():
