@@ -615,13 +615,29 @@ RoundPolicy multi_policy() {
     return {false, env_int("M3S_MULTI_DCAP", 32), env_int("M3S_MULTI_RMIN", 2),
             env_int("M3S_MULTI_RMAX", 64), 0, 0, env_int("M3S_MULTI_MMD", 0) != 0};
 }
-// hybrid: multi-launch rounds in minimum-degree order down to a core that fits the in-register
-// factorisation of gn_solve (which then also back-substitutes and retracts)
+// hybrid: multi-launch rounds in minimum-degree order down to a dense core, then gn_solve
+// back-substitutes and retracts.  The core is factored by the dataflow launch (M3S_HYB_CORE=1,
+// default) -- then it is not bound by gn_solve's in-register factorisation (kTailPoseMax poses)
+// and M3S_HYB_TAILCAP may move the rounds' stop point up to kHybDfTailMax poses -- or in
+// registers (M3S_HYB_CORE=0, or the cooperative rounds launch: <= kTailPoseMax poses).
+// Default stop point with the dataflow core: 36 poses (252 unknowns: still 4 tile columns), where
+// a round must remove >= kmin poses to continue -- cfg3: 5 rounds and a 34-pose core instead of 8
+// rounds and 26 poses, solve 0.1205 -> 0.1148 ms per iteration (two interleaved same-box rounds;
+// caps 30 and 40 with kmin 6 -- 7 rounds / 28 poses, 4 rounds / 39 poses in 5 tiles -- were slower:
+// profiles/r05_ap_hyb_tailcap/).
+constexpr int kHybDfTailMax = 64;
+constexpr int kHybDfTailDefault = 36;
+bool hyb_core_df() { return env_int("M3S_HYB_CORE", 1) != 0 && env_int("M3S_SOLVE_COOP", 0) == 0; }
 RoundPolicy hybrid_policy() {
+    const bool df = hyb_core_df();
     return {false, env_int("M3S_HYB_DCAP", 64), env_int("M3S_HYB_RMIN", 1),
             env_int("M3S_HYB_RMAX", 64),
-            std::min(kTailPoseMax, env_int("M3S_HYB_TAILCAP", kTailPoseMax)),
+            std::min(df ? kHybDfTailMax : kTailPoseMax, env_int("M3S_HYB_TAILCAP", df ? kHybDfTailDefault : kTailPoseMax)),
             env_int("M3S_HYB_KMIN", 4), env_int("M3S_HYB_MMD", 1) != 0};
+}
+// the hybrid plan's core fits its factorisation
+bool hyb_core_fits(const SparsePlan& p) {
+    return hyb_core_df() ? p.ntail <= kHybDfTailMax : p.fused_tail;
 }
 
 int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
@@ -1333,7 +1349,7 @@ void choose_sparse_plan(const Plan& plan, int npose, SparsePlan& sp) {
         static thread_local SparsePlan probe;
         build_sparse_plan(plan.pairs, plan.nblk, npose, hybrid_policy(), probe, true);
         if ((int)probe.rounds.size() > max_fused_rounds) {
-            const bool hyb = probe.fused_tail && npose <= solve_max_poses() &&
+            const bool hyb = hyb_core_fits(probe) && npose <= solve_max_poses() &&
                              solve_lds_bytes((int)probe.nints_back) <= (size_t)kSolveMaxLds;
             build_sparse_plan(plan.pairs, plan.nblk, npose, hyb ? hybrid_policy() : multi_policy(), sp);
             sp.hybrid = hyb;
@@ -1355,7 +1371,7 @@ void choose_sparse_plan(const Plan& plan, int npose, SparsePlan& sp) {
         bool hyb = false;
         if (choice == 3 || (choice == 0 && hybrid_on)) {
             build_sparse_plan(plan.pairs, plan.nblk, npose, hybrid_policy(), sp);
-            hyb = sp.fused_tail && npose <= solve_max_poses() &&
+            hyb = hyb_core_fits(sp) && npose <= solve_max_poses() &&
                   solve_lds_bytes((int)sp.nints_back) <= (size_t)kSolveMaxLds;
         }
         if (!hyb) build_sparse_plan(plan.pairs, plan.nblk, npose, multi_policy(), sp);

@@ -64,10 +64,12 @@ def simulate(ii, jj, N, info, dcap):
 def test_bench_graphs_plans(backend):
     ii, jj, N = graph_lists("cfg3")
     p = backend.gn_plan_info(ii, jj, N)
-    # cfg3 (127 free poses, 252 pairs): minimum-degree rounds down to a 26-pose core that the
-    # hybrid solve factors
+    # cfg3 (127 free poses, 252 pairs): minimum-degree rounds until the rest fits 4 tile columns
+    # of the dataflow core (<= 36 poses) and a round would remove fewer than 4 poses: 5 rounds, a
+    # 34-pose core (late round 5)
     assert (p["solver"], p["rounds"], p["core_poses"], p["core_unknowns_padded"], p["pairs"]) == \
-        ("hybrid", 8, 26, 192, 252)
+        ("hybrid", 5, 34, 256, 252)
+    assert p["core_fits"]
     simulate(ii, jj, N, p, 64)
     ii, jj, N = graph_lists("cfg4")
     p = backend.gn_plan_info(ii, jj, N)
@@ -77,6 +79,20 @@ def test_bench_graphs_plans(backend):
         ("multi", 4, 125, 896, 1007)
     assert p["core_fits"]
     simulate(ii, jj, N, p, 32)
+
+
+def test_hybrid_core_cap_switches(backend, monkeypatch):
+    ii, jj, N = graph_lists("cfg3")
+    # the in-register core's bound (27 poses): 8 rounds down to 26 poses, the plan before late
+    # round 5 -- also what the in-register core factorisation (M3S_HYB_CORE=0) gets by default
+    monkeypatch.setenv("M3S_HYB_TAILCAP", "27")
+    p = backend.gn_plan_info(ii, jj, N)
+    assert (p["solver"], p["rounds"], p["core_poses"], p["core_unknowns_padded"]) == ("hybrid", 8, 26, 192)
+    simulate(ii, jj, N, p, 64)
+    monkeypatch.delenv("M3S_HYB_TAILCAP")
+    monkeypatch.setenv("M3S_HYB_CORE", "0")
+    p = backend.gn_plan_info(ii, jj, N)
+    assert (p["solver"], p["rounds"], p["core_poses"]) == ("hybrid", 8, 26)
 
 
 def test_degree_cap_switch(backend, monkeypatch):
