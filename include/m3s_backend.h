@@ -340,6 +340,12 @@ typedef struct m3s_track_args {
 
 size_t m3s_track_workspace_bytes(int64_t HW);
 int m3s_track_sim3(const m3s_track_args* args);
+/* The last m3s_track_sim3 call's result on this host thread, on the host: info4 = {iterations,
+ * converged, cholesky failed, 0}, *cost (the same values as the call's device `info` / `cost`).
+ * Free of a device round trip when the call returned on a host check that saw its done flag
+ * (converged before max_iters); otherwise it synchronises the call's stream once.  That call's
+ * workspace must still be allocated.  Extension (the reference's tracker reads them with .item()). */
+int m3s_track_last_result(int32_t* info4, double* cost);
 
 /* ---------------- edge construction after matching ---------------- */
 

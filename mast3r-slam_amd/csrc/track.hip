@@ -14,7 +14,8 @@
 //                       solve (tracker.py:164-169, in f64), T_CkCf <- Exp(tau) T_CkCf
 //                       (lietorch retr), check_convergence (nonlinear_optimizer.py:5-25) ->
 //                       a device flag that turns the remaining iterations into no-ops
-// The host reads the flag every `check_every` iterations (one sync each).  Deterministic:
+// The host reads the flag every `check_every` iterations (one sync each) and returns once it is
+// set: each live step writes the outputs itself (no final launch behind the host's check).  Deterministic:
 // the same inputs give bitwise identical poses.
 //
 // Arithmetic follows the torch expressions (f32, python-float scalars rounded to f32 where
@@ -279,12 +280,17 @@ constexpr int kTrkChainVec = 8;  // float4 loads in flight per chain and batch
 __global__ __launch_bounds__(kTrkStepThreads) void track_step_kernel(const float* __restrict__ partials, int nblk,
                                                                  TrackState* __restrict__ st, TrkParams P,
                                                                  int* __restrict__ info,
-                                                                 double* __restrict__ cost_out) {
+                                                                 double* __restrict__ cost_out,
+                                                                 const float* __restrict__ T_WCk,
+                                                                 float* __restrict__ T_WCf_out,
+                                                                 float* __restrict__ T_CkCf_out) {
     // the flag, the pose and the old cost are loaded together with the partials (one round trip)
     const bool done = st->done != 0;
-    float T[8];
+    float T[8], Tk[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) T[q] = st->T[q];
+#pragma unroll
+    for (int q = 0; q < 8; q++) Tk[q] = T_WCk[q];
     const double old_cost = st->old_cost;
     const int iters = st->iters, converged0 = st->converged;
     __shared__ double S[kTrkNacc];
@@ -352,12 +358,24 @@ __global__ __launch_bounds__(kTrkStepThreads) void track_step_kernel(const float
             L[i][p] = a * rinv[p];
         }
     }
+    // every live step also writes the op's outputs, T_WCf = T_WCk * T_CkCf (tracker.py:212,
+    // 264): the host returns as soon as it sees the done flag, with no final launch after it
+    auto write_out = [&]() {
+        float O[8];
+        sim3_mul(Tk, T, O);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            T_WCf_out[q] = O[q];
+            T_CkCf_out[q] = T[q];
+        }
+    };
     if (bad) {
         st->failed = 1;
         st->done = 1;
         info[0] = iters;
         info[2] = 1;
         cost_out[0] = cost;
+        write_out();
         return;
     }
     // tau = H^-1 g (cholesky_solve, tracker.py:169)
@@ -396,6 +414,7 @@ __global__ __launch_bounds__(kTrkStepThreads) void track_step_kernel(const float
     info[1] = converged;
     info[2] = 0;
     cost_out[0] = cost;
+    write_out();
 }
 
 __global__ __launch_bounds__(64) void track_final_kernel(const float* __restrict__ T_WCk,
@@ -420,6 +439,11 @@ __global__ __launch_bounds__(64) void track_final_kernel(const float* __restrict
 // exit-time destructor, m3s_common.h).
 struct TrkFlags {
     TrackState* h = nullptr;
+    // the last call on this thread: its workspace state, its stream, and whether h already holds
+    // its final state (the call returned on a host check that saw the done flag)
+    const TrackState* dev = nullptr;
+    hipStream_t stream = nullptr;
+    bool fresh = false;
     static void release(void* p) {
         TrkFlags* f = static_cast<TrkFlags*>(p);
         if (f->h) (void)hipHostFree(f->h);
@@ -483,6 +507,9 @@ extern "C" int m3s_track_sim3(const m3s_track_args* args) {
 
     if (!trk_flags().h)
         M3S_HIP_CHECK(hipHostMalloc((void**)&trk_flags().h, sizeof(TrackState), hipHostMallocDefault));
+    trk_flags().dev = state;
+    trk_flags().stream = st;
+    trk_flags().fresh = false;
     hipLaunchKernelGGL(track_init_kernel, dim3(1), dim3(64), 0, st, a.T_WCf, a.T_WCk, state, a.info);
     M3S_LAUNCH_CHECK();
     const int every = a.check_every > 0 ? a.check_every : 4;
@@ -497,17 +524,45 @@ extern "C" int m3s_track_sim3(const m3s_track_args* args) {
                                partials);
         M3S_LAUNCH_CHECK();
         hipLaunchKernelGGL(track_step_kernel, dim3(1), dim3(kTrkStepThreads), 0, st, partials, nblk, state, P,
-                           a.info, a.cost);
+                           a.info, a.cost, a.T_WCk, a.T_WCf_out, a.T_CkCf_out);
         M3S_LAUNCH_CHECK();
         if ((it + 1) % every == 0 && it + 1 < a.max_iters) {
             M3S_HIP_CHECK(hipMemcpyAsync(trk_flags().h, state, sizeof(TrackState),
                                          hipMemcpyDeviceToHost, st));
             M3S_HIP_CHECK(hipStreamSynchronize(st));
-            if (trk_flags().h->done) break;
+            if (trk_flags().h->done) {
+                trk_flags().fresh = true;  // nothing is enqueued after this state
+                break;
+            }
         }
     }
-    hipLaunchKernelGGL(track_final_kernel, dim3(1), dim3(64), 0, st, a.T_WCk, state, a.T_WCf_out,
-                       a.T_CkCf_out);
-    M3S_LAUNCH_CHECK();
+    // the outputs were written by the last live step; with no iteration at all, from the start
+    if (a.max_iters == 0) {
+        hipLaunchKernelGGL(track_final_kernel, dim3(1), dim3(64), 0, st, a.T_WCk, state, a.T_WCf_out,
+                           a.T_CkCf_out);
+        M3S_LAUNCH_CHECK();
+    }
+    return M3S_OK;
+}
+
+// The last m3s_track_sim3 call's result on this host thread, to the host: {iterations, converged,
+// cholesky failed, 0} and the cost.  When that call already synchronised on its done flag (the
+// usual tracking case: converged before max_iters, seen at a host check) this reads the pinned copy
+// without another device round trip; otherwise it copies the state on the call's stream (one
+// synchronisation).  The workspace of that call must still be alive.
+extern "C" int m3s_track_last_result(int32_t* info4, double* cost) {
+    M3S_REQUIRE(info4 != nullptr && cost != nullptr, "track_last_result: null pointer");
+    TrkFlags& f = trk_flags();
+    M3S_REQUIRE(f.dev != nullptr && f.h != nullptr, "track_last_result: no track_sim3 call on this thread");
+    if (!f.fresh) {
+        M3S_HIP_CHECK(hipMemcpyAsync(f.h, f.dev, sizeof(TrackState), hipMemcpyDeviceToHost, f.stream));
+        M3S_HIP_CHECK(hipStreamSynchronize(f.stream));
+        f.fresh = true;
+    }
+    info4[0] = f.h->iters;
+    info4[1] = f.h->converged;
+    info4[2] = f.h->failed;
+    info4[3] = 0;
+    cost[0] = f.h->cost;
     return M3S_OK;
 }

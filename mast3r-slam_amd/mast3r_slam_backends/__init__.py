@@ -510,6 +510,7 @@ class TrackArgs(ctypes.Structure):
 lib.m3s_track_sim3.argtypes = [ctypes.POINTER(TrackArgs)]
 lib.m3s_track_workspace_bytes.restype = ctypes.c_size_t
 lib.m3s_track_workspace_bytes.argtypes = [_c_int64]
+lib.m3s_track_last_result.argtypes = [_vp, _vp]
 
 
 class CholeskyError(RuntimeError):
@@ -554,8 +555,9 @@ def track_sim3(mode, Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma0, sigma1, huber_k, m
     dev = _on_device(**tens)
     out_f = torch.empty((1, 8), dtype=torch.float32, device=dev)
     out_r = torch.empty((1, 8), dtype=torch.float32, device=dev)
-    # info (4 int32) and cost (1 f64) share one buffer: one fill, one device-to-host read
-    res = torch.zeros((3,), dtype=torch.float64, device=dev)
+    # the device-side info (4 int32) and cost (1 f64), one buffer (the result is read on the host
+    # through m3s_track_last_result below)
+    res = torch.empty((3,), dtype=torch.float64, device=dev)
     info, cost = res[:2].view(torch.int32), res[2:]
     ws_bytes = lib.m3s_track_workspace_bytes(HW)
     ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
@@ -582,12 +584,17 @@ def track_sim3(mode, Xf, Xk, T_WCf, T_WCk, Qk, valid, sigma0, sigma1, huber_k, m
         a.stream = torch.cuda.current_stream(dev).cuda_stream
         rc = lib.m3s_track_sim3(ctypes.byref(a))
     _raise(rc, "track_sim3")
-    h = res.cpu()
-    it, _, failed, _ = h[:2].view(torch.int32).tolist()
+    # the result from the call's pinned state copy (no second device round trip when the call
+    # already saw its done flag); `info` / `cost` on the device hold the same values
+    hinfo = (ctypes.c_int32 * 4)()
+    hcost = ctypes.c_double()
+    _raise(lib.m3s_track_last_result(ctypes.cast(hinfo, _vp), ctypes.cast(ctypes.pointer(hcost), _vp)),
+           "track_last_result")
+    it, failed = int(hinfo[0]), int(hinfo[2])
     if failed:
         raise CholeskyError("track_sim3: normal equations not positive definite "
                             f"(iteration {it + 1})")
-    return out_f, out_r, it, float(h[2])
+    return out_f, out_r, it, float(hcost.value)
 
 
 # ---------------------------------------------------------------------------------

@@ -115,6 +115,14 @@ def test_track_converges_like_oracle(backend, mode):
     assert _rel(Tf, To) <= 1e-5, _rel(Tf, To)
 
 
+def test_track_zero_iterations_returns_the_start(backend):
+    """max_iters = 0: no step runs, the outputs come from the start pose (T_WCk (T_WCk^-1 T_WCf))."""
+    p = TO.make_tracking_pair((24, 32), seed=5, noise=0.003)
+    Tf, Tr, it, _ = _gpu(backend, p, "rays", (24, 32), max_iters=0)
+    assert it == 0
+    np.testing.assert_allclose(Tf, np.asarray(p["T_WCf"], np.float64).reshape(8), rtol=0, atol=1e-5)
+
+
 def test_track_noise_free_recovers_truth(backend):
     hw = (48, 64)
     p = TO.make_tracking_pair(hw, seed=8, mode="rays")
