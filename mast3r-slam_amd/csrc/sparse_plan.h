@@ -223,6 +223,11 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
             chosen.resize(k);
         }
         if ((int)chosen.size() < rmin && (int)chosen.size() != nalive) break;
+        // multi (no tail cap): a round of fewer than kmin poses that leaves the dense core's tile
+        // count unchanged only adds a forward and a back launch
+        if (!pol.fused && tailcap == 0 && kmin > 0 && (int)chosen.size() < kmin &&
+            (7 * nalive + kCholTile - 1) / kCholTile == (7 * (nalive - (int)chosen.size()) + kCholTile - 1) / kCholTile)
+            break;
         // once the rest fits the in-register dense tail, a round must eliminate enough poses
         // to beat the per-pose cost of the tail steps
         if (nalive <= tailcap && (int)chosen.size() < kmin) break;
