@@ -613,7 +613,7 @@ RoundPolicy fused_policy() {
 // 24 0.292, 64 0.301: profiles/r05_b_dcap*.json)
 RoundPolicy multi_policy() {
     return {false, env_int("M3S_MULTI_DCAP", 32), env_int("M3S_MULTI_RMIN", 2),
-            env_int("M3S_MULTI_RMAX", 64), 0, env_int("M3S_MULTI_KMIN", 0), env_int("M3S_MULTI_MMD", 0) != 0};
+            env_int("M3S_MULTI_RMAX", 64), 0, env_int("M3S_MULTI_KMIN", 4), env_int("M3S_MULTI_MMD", 0) != 0};
 }
 // hybrid: multi-launch rounds in minimum-degree order down to a dense core, then gn_solve
 // back-substitutes and retracts.  The core is factored by the dataflow launch (M3S_HYB_CORE=1,

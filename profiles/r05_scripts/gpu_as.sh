@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r05as
 mkdir -p $O
 export TMPDIR=/tmp
-for rep in 1 2 3; do
+for rep in 1 2; do
 for km in 0 4; do
 M3S_MULTI_KMIN=$km timeout -k 10 300 python bench.py --config cfg4 --no-cpu-baseline --no-matching --steps 5 --warmup 2 > $O/km${km}_$rep.json 2> $O/km${km}_$rep.err || { echo "bench rc=$?"; tail -5 $O/km${km}_$rep.err; exit 1; }
 python -c "import json; d=json.load(open('$O/km${km}_$rep.json')); p=d['phase_ms_per_iter']; print('kmin $km', round(d['value']), round(d['ms_per_step'],3), 'solve', round(p['solve'],4), 'acc', round(p['accumulate'],4))"

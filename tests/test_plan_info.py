@@ -73,10 +73,11 @@ def test_bench_graphs_plans(backend):
     simulate(ii, jj, N, p, 64)
     ii, jj, N = graph_lists("cfg4")
     p = backend.gn_plan_info(ii, jj, N)
-    # cfg4 (255 free poses, 1007 pairs): degree cap 32, 4 rounds, a 125-pose core (875
-    # unknowns -> 14 tiles of 64) for chol_df
+    # cfg4 (255 free poses, 1007 pairs): degree cap 32, 3 rounds -- a 4th of 2 poses would leave
+    # the core's 14 tiles of 64 unchanged (M3S_MULTI_KMIN) --, a 127-pose core (889 unknowns) for
+    # chol_df
     assert (p["solver"], p["rounds"], p["core_poses"], p["core_unknowns_padded"], p["pairs"]) == \
-        ("multi", 4, 125, 896, 1007)
+        ("multi", 3, 127, 896, 1007)
     assert p["core_fits"]
     simulate(ii, jj, N, p, 32)
 
@@ -93,6 +94,14 @@ def test_hybrid_core_cap_switches(backend, monkeypatch):
     monkeypatch.setenv("M3S_HYB_CORE", "0")
     p = backend.gn_plan_info(ii, jj, N)
     assert (p["solver"], p["rounds"], p["core_poses"]) == ("hybrid", 8, 26)
+
+
+def test_multi_tile_stop_switch(backend, monkeypatch):
+    ii, jj, N = graph_lists("cfg4")
+    monkeypatch.setenv("M3S_MULTI_KMIN", "0")  # every round the degree cap admits
+    p = backend.gn_plan_info(ii, jj, N)
+    assert (p["solver"], p["rounds"], p["core_poses"], p["core_unknowns_padded"]) == ("multi", 4, 125, 896)
+    simulate(ii, jj, N, p, 32)
 
 
 def test_degree_cap_switch(backend, monkeypatch):
