@@ -195,6 +195,7 @@ def main():
             "solve": ph[2] / n_ph,
             "retract": ph[3] / n_ph,
         },
+        "solve_path": _solve_path(r["solve_stats"], iters, r["solve_ms"]),
         "roofline": {
             "kernel": f"gn_accum_packed_kernel<{mode}>" if packed else f"gn_accum_kernel<{mode}>",
             "bound": "hbm",
@@ -210,6 +211,7 @@ def main():
             "ref_formulation_bytes_per_launch": ref_bytes_launch,
             "ref_formulation_equiv_GBps": ref_bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None,
             "launches_per_step": n_it / args.steps,
+            "launch_ms_spread": launch_spread(r["launch_ms"]),
             "first_accumulate_with_pack_ms": first_ms,
         },
         "cpu_baseline": None,
@@ -220,6 +222,7 @@ def main():
         out["accuracy"] = accuracy(g, mode, Twc0, Twc, cpu_baseline.last_poses,
                                    cpu_baseline.exact_poses, cpu_baseline.full_poses, iters,
                                    cpu_baseline.last_step, cpu_baseline.exact_step)
+        out["accuracy"]["timed_kernel_parity"] = timed_kernel_parity(g, mode, Twc0, cpu_baseline.refs)
         if os.environ.get("M3S_BENCH_REF_ORDER", "1") != "0":
             out["accuracy"]["reference_order_mode"] = reference_order_block(g, mode, Twc0, args, iters)
         if mode == "calib" and os.environ.get("M3S_BENCH_STRESS", "1") != "0":
@@ -300,12 +303,19 @@ def time_config(cfg, iters_arg, steps, warmup, world, rank, rehearse, dev, comm)
     prof = (ctypes.c_double * 4)()
     nprof = ctypes.c_int(0)
     mb.lib.m3s_prof_end(prof, ctypes.byref(nprof))
+    launch_ms = []
+    if acc_events:  # the iteration kernel launch by launch (its spread within this run)
+        buf = (ctypes.c_double * 4096)()
+        n_l = mb.lib.m3s_prof_launch_ms(buf, 4096)
+        launch_ms = [buf[k] for k in range(min(n_l, 4096))]
     mb.lib.m3s_prof_begin()
     step()
     torch.cuda.synchronize()
     ph = (ctypes.c_double * 4)()
     nph = ctypes.c_int(0)
     mb.lib.m3s_prof_end(ph, ctypes.byref(nph))
+    sbuf = (ctypes.c_double * 256)()
+    solve_ms = [sbuf[k] for k in range(min(mb.lib.m3s_prof_solve_ms(sbuf, 256), 256))]
     # which accumulate path the op took (its device flags, read back by one more untimed call)
     os.environ["M3S_GN_DEBUG_FLAGS"] = "2"
     step()
@@ -314,13 +324,37 @@ def time_config(cfg, iters_arg, steps, warmup, world, rank, rehearse, dev, comm)
     mb.gn_check()  # a timed-out factorisation is reported by the next call or here (deferred)
     dbg = (ctypes.c_int * 4)()
     mb.lib.m3s_gn_debug_flags(dbg)
+    solve_stats = mb.gn_debug_flags()  # (that call's lagged-factor PCG solves)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return dict(g=g, mode=mode, iters=iters, E_und=E_und, lo=lo, hi=hi, Twc0=Twc0, Twc=Twc,
                 elapsed=elapsed, prof=prof, nprof=nprof, ph=ph, nph=nph, ray_path=bool(dbg[3]),
-                acc_events=acc_events, step=step)
+                acc_events=acc_events, step=step, launch_ms=launch_ms, solve_stats=solve_stats,
+                solve_ms=solve_ms)
+
+
+def _solve_path(st, iters, solve_ms):
+    """How a call solved its iterations: the direct block-sparse factorisation (iterations 0-1,
+    and any fallback) and the lagged-factor PCG (gn_pcg.hip) from iteration 2 on; the solve phase
+    per iteration (events of the untimed phase step) before and from iteration 2."""
+    runs = st["pcg_runs"]
+    head, tail = solve_ms[:2], solve_ms[2:iters]
+    return {"pcg_planned": st["pcg_planned"], "direct_iterations": iters - runs + st["pcg_fallbacks"],
+            "pcg_iterations": runs - st["pcg_fallbacks"], "pcg_fallbacks": st["pcg_fallbacks"],
+            "cg_steps_per_pcg_solve": (st["pcg_steps"] / runs) if runs else None,
+            "solve_ms_iterations_0_1": (sum(head) / len(head)) if head else None,
+            "solve_ms_iterations_2_on": (sum(tail) / len(tail)) if tail else None}
+
+
+def launch_spread(ms):
+    """min / median / max (and count) of per-launch kernel ms: a run's own spread, against which
+    a same-box A/B gain must be read"""
+    if not ms:
+        return None
+    s = sorted(ms)
+    return {"min": s[0], "median": s[len(s) // 2], "max": s[-1], "launches": len(s)}
 
 
 def config_block(cfg, args, world, rank, rehearse, dev, comm):
@@ -358,7 +392,11 @@ def config_block(cfg, args, world, rank, rehearse, dev, comm):
             "solve": r["ph"][2] / nph,
             "retract": r["ph"][3] / nph,
         },
+        "solve_path": _solve_path(r["solve_stats"], r["iters"], r["solve_ms"]),
         "accumulate_GBps": bytes_launch / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None,
+        # the iteration kernel's per-launch events over the timed steps (interleaved with the
+        # other phases of every call): quote cfg4 gains only beyond this spread
+        "accumulate_launch_ms_spread": launch_spread(r["launch_ms"]),
         "accumulate_bytes_per_point_edge": bpe,
     }
 
@@ -441,19 +479,28 @@ def stress_block(dev):
     finally:
         mb.set_gn_order(prev)
     c = lambda t: t.cpu().numpy()
-    P = O.make_params("calib", L["sigma_pixel"], L["sigma_depth"], L["C_conf"], L["Q_conf"], K=c(g.K), height=g.H,
-                      width=g.W, pixel_border=L["pixel_border"], z_eps=L["depth_eps"], max_iter=1, delta_thresh=0.0)
+
+    def params(n):
+        return O.make_params("calib", L["sigma_pixel"], L["sigma_depth"], L["C_conf"], L["Q_conf"], K=c(g.K),
+                             height=g.H, width=g.W, pixel_border=L["pixel_border"], z_eps=L["depth_eps"],
+                             max_iter=n, delta_thresh=0.0)
+
     arrs = [c(t) for t in (g.Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q)]
-    T_o = O.gauss_newton(P, *arrs)[0].astype(np.float64)
-    with O.exact_sums():
-        T_x = O.gauss_newton(P, *arrs)[0].astype(np.float64)
+    refs = {}
+    for n in (1, 3):
+        T_on = O.gauss_newton(params(n), *arrs)[0].astype(np.float64)
+        with O.exact_sums():
+            refs[n] = (T_on, O.gauss_newton(params(n), *arrs)[0].astype(np.float64))
+    T_o, T_x = refs[1]
     rel = lambda a, b: float(np.abs(a - b).max() / np.abs(b).max())
     return {
         "graph": "cfg3 topology, 512x384, start 10 deg / 25 cm / 0.1 log-scale, 10 % outlier matches, 1 iteration",
+        "path": "unpacked gn_accum_kernel (max_iter < 3); the timed packed kernel: timed_kernel",
         "fast_vs_oracle": rel(T_fast, T_o),
         "fast_vs_exact": rel(T_fast, T_x),
         "reference_order_vs_oracle": rel(T_ref, T_o),
         "sigma_oracle_vs_exact": rel(T_o, T_x),
+        "timed_kernel": timed_kernel_parity(g, "calib", g.Twc, refs),
     }
 
 
@@ -612,6 +659,70 @@ def tracking_bench(dev, reps=20):
     return res
 
 
+def _op_call(g, mode, Twc, n, env=None, order=None):
+    """One op call of ``n`` iterations on ``Twc`` (in place) with temporary environment switches
+    (read by the op per call) and/or summation order; returns (dx, debug flags of that call:
+    [done, fail, packed stream, ray-constrained packed accumulate])."""
+    import mast3r_slam_backends as mb
+
+    env = dict(env or {}, M3S_GN_DEBUG_FLAGS="2")
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    prev = mb.set_gn_order(order) if order else None
+    try:
+        if mode == "calib":
+            (dx,) = mb.gauss_newton_calib(Twc, g.Xs, g.Cs, g.K, g.ii, g.jj, g.idx, g.valid, g.Q, g.H, g.W,
+                                          LOCAL["pixel_border"], LOCAL["depth_eps"], LOCAL["sigma_pixel"],
+                                          LOCAL["sigma_depth"], LOCAL["C_conf"], LOCAL["Q_conf"], n, 0.0)
+        else:
+            (dx,) = mb.gauss_newton_rays(Twc, g.Xs, g.Cs, g.ii, g.jj, g.idx, g.valid, g.Q, LOCAL["sigma_ray"],
+                                         LOCAL["sigma_dist"], LOCAL["C_conf"], LOCAL["Q_conf"], n, 0.0)
+        torch.cuda.synchronize()
+    finally:
+        if order:
+            mb.set_gn_order(prev)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    mb.gn_check()
+    dbg = (ctypes.c_int * 4)()
+    mb.lib.m3s_gn_debug_flags(dbg)
+    return dx, list(dbg)
+
+
+def timed_kernel_parity(g, mode, Twc0, refs):
+    """Mid-convergence parity of the kernel the bench TIMES: a call of
+    fewer than 3 iterations normally skips the packed stream (gn_driver.hip setup), so the
+    1-iteration comparison is rerun with M3S_GN_PACK=2 -- the packed (calib: ray-constrained)
+    accumulate the timed 10-iteration call runs -- and a 3-iteration call (packed by default)
+    is added.  ``refs[n]`` = (oracle poses, exactly summed poses) after n iterations; sigma = the
+    oracle's own distance from the exact sums (the reference order's fp32 rounding noise)."""
+    import numpy as np
+
+    rel = lambda a, b: float(np.abs(a - b).max() / np.abs(b).max())
+    out = {"path": f"gn_accum_packed_kernel<{mode}{', raycheck' if mode == 'calib' else ''}> "
+                   "(M3S_GN_PACK=2 at 1 iteration; the default from 3)"}
+    for n, (To, Tx) in sorted(refs.items()):
+        To, Tx = np.asarray(To, np.float64), np.asarray(Tx, np.float64)
+        T = Twc0.clone()
+        _, dbg = _op_call(g, mode, T, n, env={"M3S_GN_PACK": "2"})
+        Tf = T.cpu().numpy().astype(np.float64)
+        T = Twc0.clone()
+        _op_call(g, mode, T, n, order="reference")
+        Tr = T.cpu().numpy().astype(np.float64)
+        out[f"{n}iter"] = {
+            "took_packed_stream": bool(dbg[2]),
+            "took_ray_constrained_accumulate": bool(dbg[3]),
+            "fast_vs_oracle": rel(Tf, To),
+            "fast_vs_exact": rel(Tf, Tx),
+            "reference_order_vs_oracle": rel(Tr, To),
+            "sigma_oracle_vs_exact": rel(To, Tx),
+        }
+    return out
+
+
 def accuracy(g, mode, Twc0, Twc_final, T_oracle_1, T_exact_1, T_oracle_full, iters, dx_oracle_1=None,
              dx_exact_1=None):
     """'ATE-RMSE vs ref' (BASELINE.json metric): the GPU op's poses after ONE iteration and the
@@ -654,6 +765,10 @@ def accuracy(g, mode, Twc0, Twc_final, T_oracle_1, T_exact_1, T_oracle_full, ite
                  "reference_order_step_max_rel_err_vs_exact_sum_1iter": rel(np.asarray(dx_oracle_1, np.float64), dxx)}
     return {
         **steps,
+        # (the *_1iter fields above and below run the call as the reference's callers would:
+        # ONE iteration, which takes the unpacked accumulate; timed_kernel_parity prices the
+        # packed kernel the timed calls run)
+        "one_iteration_path": "unpacked gn_accum_kernel (max_iter < 3)",
         f"pose_max_rel_err_vs_oracle_{iters}iter_timed_call": rel(fin, Tf),
         f"ate_rmse_vs_oracle_{iters}iter_m": ate_f,
         "pose_max_rel_err_vs_oracle_1iter": rel(T1, To),
@@ -730,7 +845,11 @@ def cpu_baseline(g, mode, E_und, iters):
     cpu_baseline.last_step = dx_o
     with O.exact_sums():  # precision reference: the same float terms summed in double
         cpu_baseline.exact_poses, cpu_baseline.exact_step, _ = O.gauss_newton(P1, *arrs)
+        T3x, _, _ = O.gauss_newton(params(3), *arrs)
     cpu_baseline.full_poses, _, _ = O.gauss_newton(params(iters), *arrs)
+    T3o, _, _ = O.gauss_newton(params(3), *arrs)
+    # oracle / exactly summed poses after 1 and 3 iterations (timed_kernel_parity)
+    cpu_baseline.refs = {1: (T_o, cpu_baseline.exact_poses), 3: (T3o, T3x)}
     return {
         "value": E_und * 1 / dt,
         "unit": "keyframe-pair GN iters/s",

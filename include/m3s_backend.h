@@ -125,6 +125,9 @@ int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D1
  * flags at the end (one extra synchronisation); out4 = {early exit, pivot failure, packed stream,
  * ray-constrained calib accumulate (Xj read as its depth)} of the last such call. */
 void m3s_gn_debug_flags(int* out4);
+/* The same call's lagged-factor PCG: out4 = {PCG solves, their CG steps in all,
+ * PCG solves that fell back to the direct factorisation, 1 if the call planned PCG iterations}. */
+void m3s_gn_pcg_stats(int* out4);
 
 /* Deferred error report.  A GN call whose solver has bounded device-side waits (the dataflow
  * factorisation) exports its timeout flag without a host wait.  A call whose wait timed out
@@ -280,6 +283,13 @@ int m3s_prof_begin(void);
  * packed records (a calib call's first accumulate, M3S_GN_PACK_FIRST), out[3] = 0. */
 int m3s_prof_begin_accum(void);
 int m3s_prof_end(double* out /* [4] */, int* n_iter);
+/* After an m3s_prof_begin_accum() .. m3s_prof_end() session: the iteration kernel's per-launch
+ * ms (out[0 .. min(n, cap) - 1]); returns n, the number of launches recorded (bench.py reports
+ * their min / median / max: the accumulate's spread within one run). */
+int m3s_prof_launch_ms(double* out, int cap);
+/* After an m3s_prof_begin() .. m3s_prof_end() session: each recorded iteration's solve ms
+ * (out[0 .. min(n, cap) - 1], call after call); returns n. */
+int m3s_prof_solve_ms(double* out, int cap);
 
 /* ---------------- frame tracking (single-pair Sim3 GN) ---------------- */
 
@@ -344,7 +354,10 @@ int m3s_track_sim3(const m3s_track_args* args);
  * converged, cholesky failed, 0}, *cost (the same values as the call's device `info` / `cost`).
  * Free of a device round trip when the call returned on a host check that saw its done flag
  * (converged before max_iters); otherwise it synchronises the call's stream once.  That call's
- * workspace must still be allocated.  Extension (the reference's tracker reads them with .item()). */
+ * workspace must still be allocated at the first read after the call, which drops the reference
+ * to it: later reads (same thread, no new call) return the same host copy without touching device
+ * memory.  Per host thread: another thread's calls are not seen.  Extension (the reference's
+ * tracker reads them with .item()). */
 int m3s_track_last_result(int32_t* info4, double* cost);
 
 /* ---------------- edge construction after matching ---------------- */

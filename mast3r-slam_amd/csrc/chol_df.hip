@@ -5,8 +5,8 @@
 // panel (potrf, trsm, update: 48 for cfg4's 141-pose core), ~5 us of dispatch each, and its
 // potrf ran the rank-8 trailing updates and the inverse on VALU from LDS (~30 us per tile).
 // Here every lower tile (i, j) of the (npad + 64) x npad bordered matrix (the border row tile
-// nt carries the RHS, so the forward substitution rides along) is owned by one workgroup of a
-// single launch (a plain launch of a grid the occupancy query keeps co-resident), processed left-looking:
+// nt carries the RHS, so the forward substitution rides along) is a task of a single launch
+// (a plain launch, grid sized by the occupancy query; tasks claimed dynamically), processed left-looking:
 //   acc = A_ij;  for k < j: wait L_ik, L_jk final -> acc -= L_ik L_jk^T  (f64 MFMA)
 //   i == j: potrf of acc in LDS (8-column panels, per-lane 8x8 factor + row solve, MFMA rank-8
 //           trailing updates) and L_jj^-1 by doubling (8x8 blocks from the panel step, MFMA for
@@ -73,6 +73,8 @@ struct DfArgs {
     // consumer sees x, and no flag poll + second load after it
     unsigned long long* xg;
     int xgran;  // x hand-off by granules (M3S_DF_XGRAN, default 1) or by ready words (0)
+    int* tick;  // [2]: the task ticket counter and the exit counter (zero between launches)
+    int dyn;    // tasks claimed dynamically (M3S_DF_DYN, default 1) or dealt statically (0)
 };
 
 // workgroup barrier ordering LDS only (__syncthreads also waits for every outstanding global
@@ -1002,8 +1004,8 @@ __device__ __forceinline__ double wait_x(const DfArgs& a, int k) {
 // per two tile columns on the back-substitution chain (a hand-off -- write-through store, flag,
 // spin, coherent load -- is ~3 us: 16 of them were 54 us of cfg4's factorisation, r04_r).
 // Thread (c, g): column c, rows 16g .. 16g+15 of each tile; the 4 row-group partials are summed
-// in fixed order (deterministic).  Every wait targets a task earlier in some co-resident
-// workgroup's list: no deadlock.
+// in fixed order (deterministic).  Every wait targets a task of a smaller ticket (claimed by a
+// running workgroup): no deadlock.
 __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
     const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
     const int nt = a.nt;
@@ -1143,7 +1145,7 @@ __device__ void back_pair(const DfArgs& a, int jh, int jl, double* S) {
 }
 
 __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
-    if (a.flags[kFlagDone]) return;  // written by earlier launches: all workgroups agree
+    if (solve_skipped(a.flags)) return;  // written by earlier launches: all workgroups agree
     __shared__ __attribute__((aligned(16))) double X[T * LD];
     __shared__ __attribute__((aligned(16))) double Y[T * LD];
     __shared__ __attribute__((aligned(16))) double Z[T * LD];
@@ -1164,7 +1166,44 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
         if (ct && tid == 0) ct[4 * nt + 4 * j + slot] = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
     };
-    if (blockIdx.x == 0) {
+    // Tasks are dealt dynamically: a workgroup claims ticket after ticket from
+    // one counter and leaves once the tickets are spent.  Ticket 0 is the diagonal chain, ticket
+    // 1 + t helper task t in the column-major order below, then the back-substitution pairs.
+    // Every wait targets the output of a smaller ticket (or a chain step those tickets already
+    // passed), and a ticket is only ever held by a RUNNING workgroup -- so the factorisation makes
+    // progress with any number of its workgroups resident: a grid that starts partly late (CUs held
+    // by another stream's kernels) only runs slower, never deadlocks or times out, and every task
+    // computes the same values whichever workgroup runs it (bitwise the unhindered result).
+    // The last workgroup to leave re-zeroes the counters for the next launch (stream order).
+    __shared__ int s_ticket;
+    const int ntasks = a.ntiles + (a.x != nullptr ? (nt + 1) / 2 : 0);
+    int nclaim = 0;
+    auto claim = [&]() {
+        int t;
+        if (a.dyn) {
+            if (tid == 0) s_ticket = __hip_atomic_fetch_add(a.tick, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            t = s_ticket;
+            __syncthreads();  // (s_ticket is rewritten by the next claim)
+        } else {  // M3S_DF_DYN=0 (A/B): the former static deal -- workgroup 0 the chain, b >= 1 tasks b-1 + k (G-1)
+            t = blockIdx.x == 0 ? 0 : (int)blockIdx.x + nclaim * ((int)gridDim.x - 1);
+        }
+        nclaim++;
+        return t;
+    };
+    // the last workgroup out re-zeroes the ticket and exit counters (the next launch on this
+    // stream starts after this one has completed, so it sees them zeroed)
+    auto leave = [&]() {
+        if (a.dyn && tid == 0 &&
+            __hip_atomic_fetch_add(a.tick + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+            __hip_atomic_store(a.tick, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.tick + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    // (the chain and the task loop are separate regions, as with the static deal: wrapped in one
+    // claim loop, the chain's registers and the tasks' stayed live together -- 143 VGPRs spilled)
+    int ticket = claim();
+    if (ticket == 0) {
         // ---- the diagonal chain
         for (int j = 0; j < nt; j++) {
             d4 accd[4];
@@ -1234,10 +1273,12 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
         }
         publish(a, (nt - 1) * nt + (nt - 1));
         cstamp(nt - 1, 3);
+        leave();
         return;
     }
-    const int ntasks = a.ntiles + (a.x != nullptr ? (nt + 1) / 2 : 0);
-    for (int t = blockIdx.x - 1; t < ntasks; t += gridDim.x - 1) {
+    for (;; ticket = claim()) {
+        if (ticket > ntasks) break;
+        const int t = ticket - 1;
         if (t >= a.ntiles) {
             const int jh = nt - 1 - 2 * (t - a.ntiles);
             back_pair(a, jh, jh - 1, X);
@@ -1306,15 +1347,19 @@ __global__ __launch_bounds__(NT) void chol_df_kernel(DfArgs a) {
             stamp(a, t, 3);
         }
     }
+    leave();
 }
 
 }  // namespace
 
-// ready words (tiles, H_j, x_j), then the x granules (16 B per entry, 16-B aligned)
-static size_t chol_words_bytes(int npad) {
+// ready words (tiles, H_j, x_j), the ticket and exit counters, then the x granules (16 B per
+// entry, 16-B aligned)
+// (the two counters on a 128-B line of their own, away from the polled ready words)
+static size_t chol_nwords(int npad) {
     const int nt = npad / T;
-    return ((sizeof(int) * ((size_t)(nt + 1) * (size_t)nt + 2 * (size_t)nt)) + 15) / 16 * 16;
+    return ((size_t)(nt + 1) * (size_t)nt + 2 * (size_t)nt + 31) / 32 * 32;
 }
+static size_t chol_words_bytes(int npad) { return sizeof(int) * (chol_nwords(npad) + 32); }
 size_t chol_ready_bytes(int npad) { return chol_words_bytes(npad) + 16 * (size_t)npad; }
 
 hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Linv, int* ready,
@@ -1348,6 +1393,7 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
     a.epoch = epoch;
     a.x = x;
     a.xg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ready) + chol_words_bytes(npad));
+    a.tick = ready + chol_nwords(npad);
     if (g) a.g = *g;
     // M3S_TEST_FORCE_TIMEOUT=1 (tests only): every ready wait gives up at once, to exercise the
     // timeout -> M3S_ERR_TIMEOUT path without a real hang
@@ -1360,13 +1406,18 @@ hipError_t launch_chol_dataflow(hipStream_t st, int npad, double* Hd, double* Li
         return e ? atoi(e) : 1;
     }();
     a.xgran = xgran;
-    const int grid = 1 + a.ntiles < maxg ? 1 + a.ntiles : maxg;  // workgroup 0 = the diagonal chain
+    static const int dyn = [] {
+        const char* e = getenv("M3S_DF_DYN");
+        return e ? atoi(e) : 1;
+    }();
+    a.dyn = dyn;
+    const int grid = 1 + a.ntiles < maxg ? 1 + a.ntiles : maxg;  // ticket 0 = the diagonal chain
     // A plain launch of a grid the occupancy query admits (one workgroup per CU here: 131 KB of
-    // LDS) gives the same residency as a cooperative one (MI355X_MICROARCH.md, "Residency and
-    // cooperative launch") without its per-launch host cost and without the ROCm 7.2 exit-time
-    // fault of a process that made a cooperative launch (profiles/r03_exit_fault).  Should the
-    // device ever not hold the whole grid (another kernel occupying CUs), the bounded ready waits
-    // fail the solve with M3S_ERR_TIMEOUT instead of hanging.  M3S_CHOL_COOP=1: cooperative.
+    // LDS) without the per-launch host cost of a cooperative one and without the ROCm 7.2
+    // exit-time fault of a process that made a cooperative launch (profiles/r03_exit_fault).  The
+    // dynamic task claim needs no co-residency: should the device not hold the whole grid
+    // (another stream's kernels occupying CUs), the late workgroups only claim later tickets; the
+    // bounded waits remain a hang guard (M3S_ERR_TIMEOUT).  M3S_CHOL_COOP=1: cooperative.
     static const bool coop = [] {
         const char* e = getenv("M3S_CHOL_COOP");
         return e && atoi(e) != 0;

@@ -75,9 +75,12 @@ struct Prof {
     }
 };
 Prof g_prof;
+std::vector<double> g_prof_launch_ms;  // the last accumulate-only session: the iteration kernel's per-launch ms
+std::vector<double> g_prof_solve_ms;   // the last phase session: each iteration's solve ms
 }  // namespace
 
 int g_dbg_flags[4] = {0, 0, 0, 0};  // done, fail, packed, ray-constrained accumulate (last call)
+int g_dbg_pcg[4] = {0, 0, 0, 0};    // PCG solves, their CG steps, fallbacks, PCG planned (last call)
 
 void set_error(const char* fmt, ...) {
     char buf[1024];
@@ -209,6 +212,48 @@ Stagings& stagings() {
         register_host_resource(t_stagings, &Stagings::release);
     }
     return *t_stagings;
+}
+
+// The PCG's side stream (gn_pcg.hip): M's refresh (sp_inverse_kernel) runs there, beside the
+// next iteration's accumulate on the call's stream; per host thread and device (the events must
+// not be shared by concurrent calls), released by m3s_shutdown.
+struct PcgSide {
+    static constexpr int kMaxDev = 64;
+    hipStream_t ss[kMaxDev] = {};
+    hipEvent_t e1[kMaxDev] = {}, e2[kMaxDev] = {};
+    static void release(void* p) {
+        PcgSide* s = static_cast<PcgSide*>(p);
+        for (int d = 0; d < kMaxDev; d++) {
+            if (s->e1[d]) (void)hipEventDestroy(s->e1[d]);
+            if (s->e2[d]) (void)hipEventDestroy(s->e2[d]);
+            if (s->ss[d]) (void)hipStreamDestroy(s->ss[d]);
+            s->e1[d] = s->e2[d] = nullptr;
+            s->ss[d] = nullptr;
+        }
+    }
+};
+thread_local PcgSide* t_pcg_side = nullptr;
+// this thread's side stream and its two events for the current device (created on first use)
+int pcg_side(hipStream_t& ss, hipEvent_t& e1, hipEvent_t& e2) {
+    if (!t_pcg_side) {
+        t_pcg_side = new PcgSide;
+        register_host_resource(t_pcg_side, &PcgSide::release);
+    }
+    int dev = 0;
+    M3S_HIP_CHECK(hipGetDevice(&dev));
+    M3S_REQUIRE(dev >= 0 && dev < PcgSide::kMaxDev, "gauss_newton: device %d out of range", dev);
+    PcgSide& p = *t_pcg_side;
+    if (!p.ss[dev]) {
+        M3S_HIP_CHECK(hipStreamCreateWithFlags(&p.ss[dev], hipStreamNonBlocking));
+        // (device-scope only: a default event's system-scope release / acquire writes back and
+        // invalidates the caches on the call's stream at every record -- idle GPU, Prof above)
+        M3S_HIP_CHECK(hipEventCreateWithFlags(&p.e1[dev], hipEventDisableTiming | hipEventDisableSystemFence));
+        M3S_HIP_CHECK(hipEventCreateWithFlags(&p.e2[dev], hipEventDisableTiming | hipEventDisableSystemFence));
+    }
+    ss = p.ss[dev];
+    e1 = p.e1[dev];
+    e2 = p.e2[dev];
+    return M3S_OK;
 }
 
 // Points per accumulate task (edge x chunk).  16384 (round 3): the chunks amortise the task
@@ -627,6 +672,9 @@ RoundPolicy multi_policy() {
 // profiles/r05_ap_hyb_tailcap/).
 constexpr int kHybDfTailMax = 64;
 constexpr int kHybDfTailDefault = 36;
+// read by the planner per call and carried with the plan (SparsePlan::core_df), so that
+// enqueue_solve factors the core the way the plan was sized for (a per-call read
+// beside a per-process one could hand a 28-64-pose core to the in-register factorisation)
 bool hyb_core_df() { return env_int("M3S_HYB_CORE", 1) != 0 && env_int("M3S_SOLVE_COOP", 0) == 0; }
 RoundPolicy hybrid_policy() {
     const bool df = hyb_core_df();
@@ -658,13 +706,17 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         sp.o_linv = take(chol_linv_bytes(sp.npad_tail));
     }
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
+    if (sp.pcg) {
+        sp.o_pcgx = take(sizeof(double) * (size_t)npose * 7 * sp.pcg_ldx);
+        sp.o_gran = take(16 * 2 * (size_t)sp.pcg_nv);
+    }
     // the plan integers in one array (layout: SparsePlan), the rounds BEFORE tmap: a launch that
     // only back-substitutes stages [nodes fptr fronts tail rounds] and not the core map
     std::vector<const std::vector<int>*> parts = {&sp.nodes, &sp.fptr, &sp.fronts, &sp.tail,
                                                   &sp.tmap, &sp.tg, &sp.tc, &sp.rtg, &sp.rc,
-                                                  &sp.tc3, &sp.rc4, &sp.inl};
+                                                  &sp.tc3, &sp.rc4, &sp.inl, &sp.apt, &sp.adj};
     size_t* offs[] = {&sp.i_nodes, &sp.i_fptr, &sp.i_fronts, &sp.i_tail, &sp.i_tmap, &sp.i_tg,
-                      &sp.i_tc, &sp.i_rtg, &sp.i_rc, &sp.i_tc3, &sp.i_rc4, &sp.i_inl};
+                      &sp.i_tc, &sp.i_rtg, &sp.i_rc, &sp.i_tc3, &sp.i_rc4, &sp.i_inl, &sp.i_apt, &sp.i_adj};
     // (inl: its first ninl ints; SparsePlan::inl)
     auto len = [&](size_t k) { return parts[k] == &sp.inl ? sp.ninl : parts[k]->size(); };
     size_t n = 0;
@@ -674,6 +726,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
             n += 8 * sp.rounds.size();
         }
         if (parts[k] == &sp.inl) n = align_up(n, 4);  // 16-B records (int4 loads)
+        if (parts[k] == &sp.adj) n = align_up(n, 2);  // int2 entries
         *offs[k] = n;
         n += len(k);
     }
@@ -682,6 +735,8 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     if (sp.npad_tail > 0)  // the dataflow factor's ready words start below every epoch
         M3S_HIP_CHECK(hipMemsetAsync(chol_ready_ptr(sp.dptr<double>(sp.o_linv), sp.npad_tail), 0,
                                      chol_ready_bytes(sp.npad_tail), st));
+    if (sp.pcg)  // the exchange's tags start below every launch's
+        M3S_HIP_CHECK(hipMemsetAsync(sp.dbuf + sp.o_gran, 0, 16 * 2 * (size_t)sp.pcg_nv, st));
     if (n > 0) {
         int* h = reinterpret_cast<int*>(stagings().out.get(sizeof(int) * n));
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
@@ -787,6 +842,10 @@ struct Ctx {
     }
     const double* eblk_all() const { return eall ? eall : at<double>(L.edgeblk); }
     int chol_epoch = 0;  // dataflow factorisations enqueued in this call (chol_df.hip ready words)
+    int pcg_launches = 0;  // PCG launches enqueued in this call (their exchange tags)
+    // an M refresh enqueued on the side stream that the call's stream has not waited for yet
+    bool inv_pending = false;
+    hipEvent_t inv_done = nullptr;
     bool may_timeout = false;  // a solver with bounded device-side waits ran (kFlagTimeout)
     template <typename T>
     T* at(size_t off) const { return reinterpret_cast<T*>(ws + off); }
@@ -811,6 +870,9 @@ struct Ctx {
     Ctx& operator=(const Ctx&) = delete;
     // every return path of a call releases its per-call buffers (stream-ordered)
     ~Ctx() {
+        // (an error path may leave an M refresh in flight on the side stream: it reads the plan
+        // buffer, so the call's stream waits for it before the buffer is released)
+        if (inv_pending && inv_done) (void)hipStreamWaitEvent(st, inv_done, 0);
         if (sp.dbuf) (void)hipFreeAsync(sp.dbuf, st);
         sp.dbuf = nullptr;
         if (dyn) (void)hipFreeAsync(dyn, st);
@@ -1256,12 +1318,14 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
             M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_inl), R.tbeg + R.rbeg, R.nbt, R.nrt,
                                           sp.iptr(sp.i_tc3), sp.iptr(sp.i_rc4), A, b, Ls, W, y, flags));
     }
-    // M3S_HYB_CORE=1 (default): the hybrid's dense core (<= 27 poses) is factored and solved by
-    // the dataflow launch (chol_df.hip: batch-cyclic tile factor, ~100 ns per column on the
-    // pivot chain, back-substitution in the same launch) instead of gn_solve's in-register pose
-    // steps (~330-430 ns per column); gn_solve then only back-substitutes through the rounds
-    // and retracts.  0: the in-register core.
-    static const bool core_df = env_int("M3S_HYB_CORE", 1) != 0;
+    // M3S_HYB_CORE=1 (default): the hybrid's dense core (<= kHybDfTailMax = 64 poses, 36 by
+    // default) is factored and solved by the dataflow launch (chol_df.hip: batch-cyclic tile
+    // factor, ~100 ns per column on the pivot chain, back-substitution in the same launch)
+    // instead of gn_solve's in-register pose steps (~330-430 ns per column); gn_solve then only
+    // back-substitutes through the rounds and retracts.  0 (or the cooperative rounds launch):
+    // the in-register core, <= 27 poses.  The planner read the switch (hyb_core_df) and sized the
+    // core for it: the plan carries the choice.
+    const bool core_df = sp.core_df;
     if (sp.hybrid && core_df && !coop && sp.ntail > 0) {
         c.may_timeout = true;  // chol_df's bounded waits
         M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
@@ -1281,6 +1345,8 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
         return M3S_OK;
     }
     if (sp.hybrid) {
+        M3S_REQUIRE(sp.fused_tail, "gauss_newton: a %d-pose hybrid core exceeds the in-register factorisation",
+                    sp.ntail);
         // the <= 27-pose core in registers, the back-substitution through the rounds and the
         // retraction: one single-workgroup launch (gn_solve.hip) reading the plan prefix; the
         // core is first laid out densely by a many-workgroup fill (one CU gathering it block by
@@ -1306,6 +1372,141 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     for (auto it = sp.rounds.rbegin(); it != sp.rounds.rend(); ++it)
         M3S_HIP_CHECK(launch_sp_back(c.st, it->nnodes, sp.iptr(sp.i_nodes), sp.iptr(sp.i_fptr),
                                      sp.iptr(sp.i_fronts), it->node_begin, Ls, W, y, x, flags));
+    return M3S_OK;
+}
+
+// ---- the lagged-factor PCG (gn_pcg.hip) ----
+// M3S_GN_PCG (default 1): from iteration M3S_PCG_FROM (default 2) on, the step is solved by CG
+// preconditioned with the inverse of iteration (M3S_PCG_FROM - 1)'s system, which that
+// iteration's direct factorisation provides (sp_inverse_kernel); the direct solve stays enqueued
+// behind every PCG launch as its fallback and returns at once when the PCG converged.  Plans whose
+// factor the inverse reads: elimination rounds by sp_round_kernel and a chol_df core (the hybrid
+// with M3S_HYB_CORE=1, the multi plan); not the single-workgroup solve, the reference-order mode,
+// the all-rounds launch or the dense solver.
+int pcg_from() {
+    static const int v = std::max(1, env_int("M3S_PCG_FROM", 2));
+    return v;
+}
+void choose_pcg(const m3s_gn_args& a, const Ctx& c, const Plan& plan, int npose, SparsePlan& sp) {
+    sp.pcg = false;
+    const int n = 7 * npose;
+    if (env_int("M3S_GN_PCG", 1) == 0 || c.ref_order || !sp.enabled || sp.fused || (sp.hybrid && !sp.core_df) ||
+        env_int("M3S_SOLVE_COOP", 0) != 0 || a.max_iter <= pcg_from() || n > kPcgMaxN || n < 7)
+        return;
+    // rows of M per workgroup: a power of two (4 .. 32), the smallest giving <= M3S_PCG_WG
+    // workgroups (default 64) -- or the largest whose f32 rows fit the LDS beside the vector and
+    // the product's lists; never more than 240 workgroups (all resident at once, at most one per CU)
+    const int wg_cap = std::max(1, env_int("M3S_PCG_WG", 64));
+    const int nadj = npose + 2 * (int)plan.pairs.size();
+    int R = 4;
+    while (R < 32 && (n + R - 1) / R > wg_cap && pcg_lds_bytes(n, 2 * R, nadj) <= (size_t)kPcgMaxLds) R *= 2;
+    if ((n + R - 1) / R > 240 || pcg_lds_bytes(n, R, nadj) > (size_t)kPcgMaxLds) return;
+    sp.pcg = true;
+    sp.pcg_R = R;
+    sp.pcg_nwg = (n + R - 1) / R;
+    sp.pcg_ldx = (int)align_up((size_t)n, kCholTile);
+    sp.pcg_nv = pcg_nv(n);
+    // the matrix-vector product's lists: per pose its diagonal block, then its pair blocks
+    sp.apt.assign((size_t)npose + 1, 0);
+    for (const auto& pr : plan.pairs) {
+        sp.apt[pr.first + 1]++;
+        sp.apt[pr.second + 1]++;
+    }
+    for (int v = 0; v < npose; v++) sp.apt[v + 1] += sp.apt[v] + 1;
+    sp.adj.assign(2 * (size_t)sp.apt[npose], 0);
+    std::vector<int> fill(sp.apt.begin(), sp.apt.end() - 1);
+    for (int v = 0; v < npose; v++) {
+        sp.adj[2 * (size_t)fill[v]] = v;  // (the diagonal block's slot is the pose)
+        sp.adj[2 * (size_t)fill[v] + 1] = v;
+        fill[v]++;
+    }
+    for (size_t k = 0; k < plan.pairs.size(); k++) {
+        const int x = plan.pairs[k].first, y = plan.pairs[k].second, slot = npose + (int)k;
+        sp.adj[2 * (size_t)fill[x]] = slot;
+        sp.adj[2 * (size_t)fill[x]++ + 1] = y;
+        sp.adj[2 * (size_t)fill[y]] = slot;
+        sp.adj[2 * (size_t)fill[y]++ + 1] = x;
+    }
+}
+
+int enqueue_inverse(const m3s_gn_args& a, Ctx& c) {
+    const SparsePlan& sp = c.sp;
+    InvArgs v{};
+    v.n = 7 * (int)(a.N - 1);
+    v.ldx = sp.pcg_ldx;
+    v.nrounds = (int)sp.rounds.size();
+    v.ntail = sp.ntail;
+    v.npad = sp.npad_tail;
+    v.rounds = sp.iptr(sp.i_rounds);
+    v.nodes = sp.iptr(sp.i_nodes);
+    v.fptr = sp.iptr(sp.i_fptr);
+    v.fronts = sp.iptr(sp.i_fronts);
+    v.inl = sp.iptr(sp.i_inl);
+    v.rc4 = sp.iptr(sp.i_rc4);
+    v.tail = sp.iptr(sp.i_tail);
+    v.Lstore = sp.dptr<double>(sp.o_L);
+    v.W = sp.dptr<double>(sp.o_W);
+    v.Hd = sp.dptr<double>(sp.o_dense);
+    v.Linv = sp.dptr<double>(sp.o_linv);
+    v.X = sp.dptr<double>(sp.o_pcgx);
+    v.flags = c.at<int>(c.L.flags);
+    // M3S_PCG_SIDE (default 1): on the side stream, beside the next iteration's accumulate (it
+    // reads the factor and the flags, writes X only; the next PCG launch waits for it); 0: on
+    // the call's stream
+    static const bool side = env_int("M3S_PCG_SIDE", 1) != 0;
+    if (!side) {
+        M3S_HIP_CHECK(launch_sp_inverse(c.st, v));
+        return M3S_OK;
+    }
+    hipStream_t ss;
+    hipEvent_t e1, e2;
+    int rc = pcg_side(ss, e1, e2);
+    if (rc) return rc;
+    M3S_HIP_CHECK(hipEventRecord(e1, c.st));
+    M3S_HIP_CHECK(hipStreamWaitEvent(ss, e1, 0));
+    M3S_HIP_CHECK(launch_sp_inverse(ss, v));
+    M3S_HIP_CHECK(hipEventRecord(e2, ss));
+    c.inv_pending = true;
+    c.inv_done = e2;
+    return M3S_OK;
+}
+
+int enqueue_pcg(const m3s_gn_args& a, Ctx& c) {
+    const SparsePlan& sp = c.sp;
+    PcgArgs g{};
+    g.b = sp.dptr<double>(sp.o_sys);
+    g.A = g.b + sp.bpad;
+    g.adj_ptr = sp.iptr(sp.i_apt);
+    g.adj = reinterpret_cast<const int2*>(sp.iptr(sp.i_adj));
+    g.npose = (int)(a.N - 1);
+    g.nadj = (int)(sp.adj.size() / 2);
+    g.napt4 = pcg_napt4(g.npose);
+    g.X = sp.dptr<double>(sp.o_pcgx);
+    g.ldx = sp.pcg_ldx;
+    g.n = 7 * (int)(a.N - 1);
+    g.nv = sp.pcg_nv;
+    g.R = sp.pcg_R;
+    g.nwg = sp.pcg_nwg;
+    g.gran = reinterpret_cast<unsigned long long*>(sp.dbuf + sp.o_gran);
+    // tags: unique within the call (the granules are zeroed per call), kmax + 1 exchanges a launch
+    static const int kmax = std::max(1, std::min(200, env_int("M3S_PCG_KMAX", 30)));
+    static const double tol = [] {
+        const char* e = getenv("M3S_PCG_TOL");
+        return e ? atof(e) : 1e-6;
+    }();
+    g.kmax = kmax;
+    g.tol2 = tol * tol;
+    g.tag0 = 1u + (unsigned)c.pcg_launches * (unsigned)(kmax + 2);
+    c.pcg_launches++;
+    const char* ft = getenv("M3S_TEST_FORCE_TIMEOUT");
+    g.spin_limit = (ft && atoi(ft) != 0) ? 0 : (1 << 22);
+    g.Twc = a.Twc;
+    g.dx = a.dx;
+    g.N = (int)a.N;
+    g.delta_thresh = a.delta_thresh;
+    g.contract = a.contract;
+    g.flags = c.at<int>(c.L.flags);
+    M3S_HIP_CHECK(launch_pcg(c.st, g));
     return M3S_OK;
 }
 
@@ -1377,6 +1578,7 @@ void choose_sparse_plan(const Plan& plan, int npose, SparsePlan& sp) {
         if (!hyb) build_sparse_plan(plan.pairs, plan.nblk, npose, multi_policy(), sp);
         sp.hybrid = hyb;
     }
+    sp.core_df = hyb_core_df();
 }
 
 // m3s_gn_plan_info (include/m3s_backend.h): the plan choose_sparse_plan makes, from host lists
@@ -1457,6 +1659,7 @@ int run(const m3s_gn_args& a) {
     const auto t1b = now();
     if (env_int("M3S_SOLVER_DENSE", 0) == 0 || c.ref_order) {
         choose_sparse_plan(c.plan, npose, c.sp);
+        choose_pcg(a, c, c.plan, npose, c.sp);
         t2 = now();
         M3S_REQUIRE(c.sp.npad_tail <= kMaxNpad,
                     "gauss_newton: the dense core of the elimination (%d unknowns) exceeds the "
@@ -1475,12 +1678,27 @@ int run(const m3s_gn_args& a) {
         g_prof.mark(c.st);
         // the poses the call started from, so that a timed-out call can restore them (below)
         if (itr == 0) M3S_HIP_CHECK(launch_twc_save(c.st, a.Twc, c.at<float>(L.twc_save), (int)(8 * a.N)));
+        if (c.sp.pcg && itr >= pcg_from()) {  // the direct solve below is its fallback
+            if (c.inv_pending) {  // M's refresh (side stream) must be complete
+                M3S_HIP_CHECK(hipStreamWaitEvent(c.st, c.inv_done, 0));
+                c.inv_pending = false;
+            }
+            rc = enqueue_pcg(a, c);
+            if (rc) return rc;
+        }
         rc = enqueue_solve(a, c);
         if (rc) return rc;
         g_prof.mark(c.st);
         if (!c.sp.fused && !c.sp.hybrid)  // gn_solve retracts inside its launch
             M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
                                          a.delta_thresh, flags, a.contract));
+        // M for the next PCG iteration from this iteration's factor: the first direct solve
+        // before the PCG iterations, then after every PCG that fell back to the direct solve
+        // (sp_inverse_kernel returns at once when this iteration's PCG converged: M stays)
+        if (c.sp.pcg && itr >= pcg_from() - 1 && itr + 1 < a.max_iter) {
+            rc = enqueue_inverse(a, c);
+            if (rc) return rc;
+        }
         g_prof.mark(c.st);
     }
     // (the per-call solver buffers are released by ~Ctx on this and every error path)
@@ -1535,9 +1753,14 @@ int run(const m3s_gn_args& a) {
         g_dbg_flags[1] = hf[kFlagFail];
         g_dbg_flags[2] = c.packed ? 1 : 0;
         g_dbg_flags[3] = (c.packed && c.P.raycheck && hf[kFlagNotRay] == 0) ? 1 : 0;
+        g_dbg_pcg[0] = hf[kFlagPcgRuns];
+        g_dbg_pcg[1] = hf[kFlagPcgSteps];
+        g_dbg_pcg[2] = hf[kFlagPcgFall];
+        g_dbg_pcg[3] = c.sp.pcg ? 1 : 0;
         if (dbg != 2)
-            fprintf(stderr, "gn flags: done %d fail %d not_ray %d timeout %d packed %d\n", hf[kFlagDone],
-                    hf[kFlagFail], hf[kFlagNotRay], hf[kFlagTimeout], (int)c.packed);
+            fprintf(stderr, "gn flags: done %d fail %d not_ray %d timeout %d packed %d pcg runs %d steps %d fallbacks %d\n",
+                    hf[kFlagDone], hf[kFlagFail], hf[kFlagNotRay], hf[kFlagTimeout], (int)c.packed,
+                    hf[kFlagPcgRuns], hf[kFlagPcgSteps], hf[kFlagPcgFall]);
     }
     return M3S_OK;
 }
@@ -1560,6 +1783,10 @@ extern "C" int m3s_gn_check(void* stream) {
 
 extern "C" void m3s_gn_debug_flags(int* out4) {
     for (int k = 0; k < 4; k++) out4[k] = m3s::g_dbg_flags[k];
+}
+
+extern "C" void m3s_gn_pcg_stats(int* out4) {
+    for (int k = 0; k < 4; k++) out4[k] = m3s::g_dbg_pcg[k];
 }
 
 extern "C" const char* m3s_version(void) { return "m3s 0.1.0 gfx950"; }
@@ -1805,6 +2032,7 @@ extern "C" int m3s_prof_end(double* out, int* n_iter) {
         // launches that built the records themselves (a call's first, M3S_GN_PACK_FIRST) and
         // their count
         g_prof.accum_only = false;
+        g_prof_launch_ms.clear();
         for (size_t k = 0; k + 2 <= g_prof.marks.size(); k += 2) {
             float ms = 0.f;
             M3S_HIP_CHECK(hipEventSynchronize(g_prof.marks[k + 1]));
@@ -1815,6 +2043,7 @@ extern "C" int m3s_prof_end(double* out, int* n_iter) {
             } else {
                 acc[0] += ms;
                 n++;
+                g_prof_launch_ms.push_back(ms);
             }
         }
         for (int q = 0; q < 4; q++) out[q] = acc[q];
@@ -1824,6 +2053,7 @@ extern "C" int m3s_prof_end(double* out, int* n_iter) {
         return M3S_OK;
     }
     const size_t per = 6;  // t0 [a0 a1] t1 t2 t3 (a0/a1 bracket the accumulate kernel)
+    g_prof_solve_ms.clear();
     for (size_t k = 0; k + per <= g_prof.marks.size(); k += per) {
         hipEvent_t* m = &g_prof.marks[k];
         float ms[5];
@@ -1835,6 +2065,7 @@ extern "C" int m3s_prof_end(double* out, int* n_iter) {
         acc[1] += ms[0] + ms[2];
         acc[2] += ms[3];
         acc[3] += ms[4];
+        g_prof_solve_ms.push_back(ms[3]);
         n++;
     }
     for (int q = 0; q < 4; q++) out[q] = acc[q];
@@ -1842,4 +2073,21 @@ extern "C" int m3s_prof_end(double* out, int* n_iter) {
     for (hipEvent_t e : g_prof.marks) g_prof.pool.push_back(e);
     g_prof.marks.clear();
     return M3S_OK;
+}
+
+// the per-launch durations (ms) of the iteration kernel from the last m3s_prof_begin_accum ..
+// m3s_prof_end session (bench.py: the spread of the accumulate over the timed steps); returns the
+// number of launches recorded, copies at most cap of them
+extern "C" int m3s_prof_launch_ms(double* out, int cap) {
+    const int n = (int)g_prof_launch_ms.size();
+    for (int k = 0; k < n && k < cap; k++) out[k] = g_prof_launch_ms[k];
+    return n;
+}
+
+// each iteration's solve ms from the last m3s_prof_begin .. m3s_prof_end session (bench.py: the
+// direct iterations apart from the PCG ones); returns the count, copies at most cap
+extern "C" int m3s_prof_solve_ms(double* out, int cap) {
+    const int n = (int)g_prof_solve_ms.size();
+    for (int k = 0; k < n && k < cap; k++) out[k] = g_prof_solve_ms[k];
+    return n;
 }

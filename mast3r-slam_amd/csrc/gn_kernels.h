@@ -25,7 +25,20 @@ constexpr int kFlagTimeout = 3; // sticky for the call: a bounded device-side wa
                                 // ready word, grid barrier); the driver returns M3S_ERR_TIMEOUT
 constexpr int kFlagBarCount = 4;  // grid barrier of the all-rounds launch: arrivals
 constexpr int kFlagBarGen = 5;    // ... and its generation
+// The lagged-factor PCG (gn_pcg.hip) of an iteration that converged has retracted the poses
+// itself; the direct solve's launches enqueued behind it (its fallback) then return at once
+// (solve_skipped).  Set or cleared by every PCG launch; never set in iterations without one.
+constexpr int kFlagSkipSolve = 6;
+constexpr int kFlagPcgRuns = 7;   // diagnostics (M3S_GN_DEBUG_FLAGS): PCG solves of the call
+constexpr int kFlagPcgSteps = 8;  // ... their CG steps in all
+constexpr int kFlagPcgFall = 9;   // ... and how many fell back to the direct solve
+constexpr int kFlagPcgAbort = 10; // a PCG launch's workgroup gave up on a gather (= that launch's tag)
 constexpr int kNumFlags = 16;
+// the direct solve's launches of this iteration have nothing to do: the call converged (early
+// exit) or the iteration's PCG converged and retracted
+__device__ __forceinline__ bool solve_skipped(const int* flags) {
+    return (flags[kFlagDone] | flags[kFlagSkipSolve]) != 0;
+}
 
 // Where the per-point-edge inputs (idx, valid, Q) of local directed edge e live: edges
 // e < E_a in the first arrays (row e), the others in the second arrays (row e - E_a).  One
@@ -185,6 +198,41 @@ hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, cons
                           double* xd, double* x, int* flags, int epoch);
 hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                             int npose, int n, int npad, double* Hd, const int* flags);
+// The lagged-factor PCG (gn_pcg.hip).  X = A^-1 from the last direct solve's factor (the
+// elimination rounds and the chol_df core), row-major [n][ldx], ldx = n rounded up to 64.
+struct InvArgs {
+    int n, ldx, nrounds, ntail, npad;
+    const int *rounds, *nodes, *fptr, *fronts, *inl, *rc4, *tail;
+    const double *Lstore, *W, *Hd, *Linv;
+    double* X;
+    const int* flags;
+};
+hipError_t launch_sp_inverse(hipStream_t st, const InvArgs& a);
+constexpr int kPcgMaxN = 2048;               // unknowns the PCG takes (8 vector entries per thread)
+constexpr int kPcgMaxLds = 160 * 1024 - 1024;  // dynamic LDS of one PCG workgroup
+struct PcgArgs {
+    const double *b, *A;           // the block-format system (gn_assemble_kernel)
+    const int* adj_ptr;            // per pose: its blocks (the diagonal first) ...
+    const int2* adj;               // ... as (block, other pose); both staged in LDS
+    int npose, nadj, napt4;        // poses, list entries, adj_ptr's LDS ints (pcg_napt4)
+    const double* X;               // M = X (sp_inverse_kernel), row-major, ld ldx
+    int64_t ldx;
+    int n, nv, R, nwg;             // unknowns, vector stride (pcg_nv), rows of M per workgroup, workgroups
+    unsigned long long* gran;      // 2 x nv x 16 B: the z exchange's data-tagged granules (zeroed per call)
+    unsigned tag0;                 // this launch's first tag (unique within the call)
+    double tol2;                   // converged when r'z <= tol2 * r0'z0
+    int kmax, spin_limit;
+    float* Twc;
+    float* dx;
+    int N;
+    float delta_thresh;
+    int contract;
+    int* flags;
+};
+int pcg_nv(int n);
+int pcg_napt4(int npose);
+size_t pcg_lds_bytes(int n, int R, int nadj);
+hipError_t launch_pcg(hipStream_t st, const PcgArgs& a);
 // Fused single-workgroup solve (gn_solve.hip)
 constexpr int kSolveThreads = 256;
 #ifndef M3S_SOLVE_ROUND_THREADS

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void gn_fill_dense_kernel(const double* __rest
                                                             int nblk, int npose, int n, int npad,
                                                             double* __restrict__ Hd,
                                                             const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     const int64_t total = (int64_t)(npad + kCholTile) * npad;
     for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
          id += (int64_t)gridDim.x * blockDim.x) {
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kPotrfThreads) void chol_potrf_kernel(double* __res
                                                                    int npad, int k,
                                                                    double* __restrict__ Linv,
                                                                    int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     __shared__ double A[T][LDP];
     __shared__ double Li[T][LDP];
     __shared__ double Tm[T][LDP];
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(kGemmThreads) void chol_trsm_kernel(double* __restr
                                                                  int k,
                                                                  const double* __restrict__ Linv,
                                                                  const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     __shared__ __attribute__((aligned(16))) double Xs_[T][LD2];
     __shared__ __attribute__((aligned(16))) double Li[T][LD2];
     const int tid = threadIdx.x;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(kGemmThreads) void chol_trsm_kernel(double* __restr
 __global__ __launch_bounds__(kGemmThreads) void chol_update_kernel(double* __restrict__ Hd,
                                                                    int npad, int nt, int k,
                                                                    const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     __shared__ __attribute__((aligned(16))) double Li[T][LD2];
     __shared__ __attribute__((aligned(16))) double Lj[T][LD2];
     int rem = blockIdx.x;  // -> (i, j): j = k+1.., i = j..nt
@@ -450,7 +450,7 @@ constexpr int kMaxNpadBack = 8192;
 __global__ __launch_bounds__(kBackThreads) void chol_backsolve_kernel(
     const double* __restrict__ Hd, int npad, const double* __restrict__ Linv,
     double* __restrict__ x, const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     __shared__ double y[kMaxNpadBack];
     __shared__ double Li[T][T + 1];
     __shared__ double part[16][T];
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256) void gn_retract_kernel(float* __restrict__ Twc
                                                          float* __restrict__ dx, int N,
                                                          float delta_thresh,
                                                          int* __restrict__ flags, int contract) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     const int tid = threadIdx.x;
     const bool fail = flags[kFlagFail] != 0;
     double nrm = 0.0;

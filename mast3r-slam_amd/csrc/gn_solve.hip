@@ -529,7 +529,7 @@ __global__ __launch_bounds__(NT) void gn_solve_kernel(SolveArgs a) {
         sEntry = wall_clock64();
         sEntryCyc = __builtin_amdgcn_s_memtime();  // shader clock: the effective frequency
     }
-    if (a.flags[kFlagDone]) return;
+    if (solve_skipped(a.flags)) return;
     extern __shared__ double smem[];
     __shared__ double sRed[NW];
     __shared__ int sFail;

@@ -60,7 +60,7 @@ __device__ __forceinline__ void stA(double* p, double v) {
 template <bool COH>
 __device__ __forceinline__ void sp_round_target(
     const int* __restrict__ rec, bool blk, const int* __restrict__ tc3, const int* __restrict__ rc4,
-    const int* __restrict__ done, double* __restrict__ A, double* __restrict__ b,
+    const int* skipf /* the call's flags (solve_skipped), or null */, double* __restrict__ A, double* __restrict__ b,
     double* __restrict__ Lstore, double* __restrict__ W, double* __restrict__ y, int* __restrict__ flags,
     double (*sR)[7 * kLd], double (*sS)[7 * kLd]) {
     const int lane = threadIdx.x;
@@ -68,7 +68,7 @@ __device__ __forceinline__ void sp_round_target(
     // the record header, this group's inline contribution and (per launch) the flag: one round trip
     const int4 hd = *reinterpret_cast<const int4*>(rec);
     const int4 mine = *reinterpret_cast<const int4*>(rec + 4 + 4 * (g < kSpInline ? g : 0));
-    if (done && *done) return;
+    if (skipf && solve_skipped(skipf)) return;
     const int tgt = hd.x, c0 = hd.y, c1 = hd.z;
     // this lane's output: entry (er, ec) of the block, or row er of the RHS
     const int nact = tgt < 0 ? 0 : (blk ? 49 : 7);
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64) void sp_round_kernel(
     __shared__ double sR[kGroups][7 * kLd];  // rows of W_rv, per contribution of the batch
     __shared__ double sS[kGroups][7 * kLd];  // block target: rows of W_sv; RHS target: y_v
     sp_round_target<false>(inl + (int64_t)(ibeg + blockIdx.x) * kSpRec, (int)blockIdx.x < nbt, tc3, rc4,
-                           flags + kFlagDone, A, b, Lstore, W, y, flags, sR, sS);
+                           flags, A, b, Lstore, W, y, flags, sR, sS);
 }
 
 // x_v = L_v^-T (y_v - sum_r W_rv^T x_r), one workgroup per pose of the round; 7-lane group g
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64) void sp_back_kernel(
     int node_begin, const double* __restrict__ Lstore, const double* __restrict__ W,
     const double* __restrict__ y, double* __restrict__ x, const int* __restrict__ flags) {
     __shared__ double part[kGroups][kLd];
-    const int done = flags[kFlagDone];
+    const int done = solve_skipped(flags);
     const int q = node_begin + blockIdx.x, lane = threadIdx.x;
     const int v = nodes[q], f0 = fptr[q], f1 = fptr[q + 1];
     if (done) return;
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void sp_tail_fill_kernel(const double* __restr
                                                            int ntail, int npad,
                                                            double* __restrict__ Hd,
                                                            const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     sp_tail_fill<false>(A, b, tmap, tail, ntail, npad, Hd);
 }
 
@@ -298,7 +298,7 @@ __device__ __forceinline__ void grid_barrier(int* __restrict__ flags, unsigned n
 __global__ __launch_bounds__(64) void sp_rounds_coop_kernel(SpCoopArgs a) {
     __shared__ double sR[kGroups][7 * kLd];
     __shared__ double sS[kGroups][7 * kLd];
-    if (a.flags[kFlagDone]) return;
+    if (solve_skipped(a.flags)) return;
     for (int rd = 0; rd < a.nrounds; rd++) {
         const int* R = a.rounds + 8 * rd;  // node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount
         const int tbeg = R[2], nbt = R[3], rbeg = R[4], nrt = R[5];
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void sp_tail_scatter_kernel(const double* __re
                                                               const int* __restrict__ tail,
                                                               int ntail, double* __restrict__ x,
                                                               const int* __restrict__ flags) {
-    if (flags[kFlagDone]) return;
+    if (solve_skipped(flags)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < ntail * 7) x[(int64_t)tail[i / 7] * 7 + i % 7] = xd[i];
 }

@@ -27,6 +27,12 @@ struct SparsePlan {
     bool fused = false;       // the whole solve in one gn_solve launch (else multi-launch)
     bool fused_tail = false;  // the dense tail fits the in-register factorisation of gn_solve
     bool hybrid = false;      // multi-launch rounds, then gn_solve's core + back-substitution
+    bool core_df = true;      // hybrid: the core by chol_df (else in registers); the planner's choice
+    // PCG iterations (gn_pcg.hip; set by the driver): M's rows per workgroup, workgroups, X's
+    // leading dimension, the vector stride; device: X (n x ldx f64) and the exchange granules
+    bool pcg = false;
+    int pcg_R = 0, pcg_nwg = 0, pcg_ldx = 0, pcg_nv = 0;
+    size_t o_pcgx = 0, o_gran = 0;
     int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
     std::vector<SpRound> rounds;
     std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
@@ -40,6 +46,9 @@ struct SparsePlan {
     // targets have 1-2 of 9; writing the whole 160-B records was most of a cfg4 plan's time)
     std::vector<int> inl;
     size_t ninl = 0;
+    // the PCG's matrix-vector product (gn_pcg.hip): per pose its blocks, the diagonal first, as
+    // (block, other pose) pairs; built by the driver when the call runs PCG iterations
+    std::vector<int> apt, adj;
     // device (one stream-ordered allocation per call)
     char* dbuf = nullptr;
     size_t o_dense = 0, o_linv = 0;  // the dense core (npad_tail + 64) x npad_tail and its tile inverses
@@ -51,7 +60,8 @@ struct SparsePlan {
     // [tg tc rtg rc] (nints: the whole plan of the single-workgroup solve) [tc3 rc4] (multi-launch
     // rounds only)
     size_t i_nodes = 0, i_fptr = 0, i_fronts = 0, i_tg = 0, i_tc = 0, i_rtg = 0, i_rc = 0,
-           i_tail = 0, i_tmap = 0, i_rounds = 0, i_tc3 = 0, i_rc4 = 0, i_inl = 0, nints = 0, nints_back = 0;
+           i_tail = 0, i_tmap = 0, i_rounds = 0, i_tc3 = 0, i_rc4 = 0, i_inl = 0, i_apt = 0, i_adj = 0,
+           nints = 0, nints_back = 0;
     template <typename T>
     T* dptr(size_t off) const { return reinterpret_cast<T*>(dbuf + off); }
     const int* iptr(size_t i) const { return reinterpret_cast<const int*>(dbuf + o_int) + i; }
@@ -62,7 +72,8 @@ struct SparsePlan {
         SparsePlan fresh;
         for (auto v : {&SparsePlan::nodes, &SparsePlan::fptr, &SparsePlan::fronts, &SparsePlan::tg,
                        &SparsePlan::tc, &SparsePlan::rtg, &SparsePlan::rc, &SparsePlan::tail,
-                       &SparsePlan::tmap, &SparsePlan::tc3, &SparsePlan::rc4}) {
+                       &SparsePlan::tmap, &SparsePlan::tc3, &SparsePlan::rc4, &SparsePlan::apt,
+                       &SparsePlan::adj}) {
             (this->*v).clear();
             (fresh.*v).swap(this->*v);
         }
@@ -224,9 +235,11 @@ inline void build_sparse_plan(const std::vector<std::pair<int, int>>& pairs, int
         }
         if ((int)chosen.size() < rmin && (int)chosen.size() != nalive) break;
         // multi (no tail cap): a round of fewer than kmin poses that leaves the dense core's tile
-        // count unchanged only adds a forward and a back launch
+        // count unchanged only adds a forward and a back launch -- unless the core it would leave
+        // exceeds the dense solve limit (later rounds may still bring it under)
         if (!pol.fused && tailcap == 0 && kmin > 0 && (int)chosen.size() < kmin &&
-            (7 * nalive + kCholTile - 1) / kCholTile == (7 * (nalive - (int)chosen.size()) + kCholTile - 1) / kCholTile)
+            (7 * nalive + kCholTile - 1) / kCholTile == (7 * (nalive - (int)chosen.size()) + kCholTile - 1) / kCholTile &&
+            (int)sp_align_up((size_t)nalive * 7, kCholTile) <= kMaxNpad)
             break;
         // once the rest fits the in-register dense tail, a round must eliminate enough poses
         // to beat the per-pose cost of the tail steps

@@ -549,16 +549,20 @@ extern "C" int m3s_track_sim3(const m3s_track_args* args) {
 // cholesky failed, 0} and the cost.  When that call already synchronised on its done flag (the
 // usual tracking case: converged before max_iters, seen at a host check) this reads the pinned copy
 // without another device round trip; otherwise it copies the state on the call's stream (one
-// synchronisation).  The workspace of that call must still be alive.
+// synchronisation).  The workspace of that call must still be alive at the FIRST read after the
+// call; that read drops the reference to the workspace, so later reads return the
+// same host copy and never touch device memory the caller may have freed since.
 extern "C" int m3s_track_last_result(int32_t* info4, double* cost) {
     M3S_REQUIRE(info4 != nullptr && cost != nullptr, "track_last_result: null pointer");
     TrkFlags& f = trk_flags();
-    M3S_REQUIRE(f.dev != nullptr && f.h != nullptr, "track_last_result: no track_sim3 call on this thread");
+    M3S_REQUIRE(f.h != nullptr && (f.dev != nullptr || f.fresh), "track_last_result: no track_sim3 call on this thread");
     if (!f.fresh) {
         M3S_HIP_CHECK(hipMemcpyAsync(f.h, f.dev, sizeof(TrackState), hipMemcpyDeviceToHost, f.stream));
         M3S_HIP_CHECK(hipStreamSynchronize(f.stream));
         f.fresh = true;
     }
+    f.dev = nullptr;  // read: the host copy is final
+    f.stream = nullptr;
     info4[0] = f.h->iters;
     info4[1] = f.h->converged;
     info4[2] = f.h->failed;

@@ -19,6 +19,7 @@ import os
 import torch
 
 __all__ = [
+    "gn_debug_flags",
     "iter_proj",
     "refine_matches",
     "gauss_newton_points",
@@ -672,6 +673,18 @@ def gn_check(device=None):
     Synchronises the current stream of `device` (default: the current device)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     _raise(lib.m3s_gn_check(_stream(dev)), "gauss_newton")
+
+
+def gn_debug_flags() -> dict:
+    """Diagnostics of the last Gauss-Newton call made with env M3S_GN_DEBUG_FLAGS set (that call
+    reads its device flags back): the accumulate path it took and its lagged-factor PCG solves
+    (include/m3s_backend.h m3s_gn_debug_flags / m3s_gn_pcg_stats)."""
+    f = (ctypes.c_int * 4)()
+    lib.m3s_gn_debug_flags(f)
+    q = (ctypes.c_int * 4)()
+    lib.m3s_gn_pcg_stats(q)
+    return {"done": f[0], "fail": f[1], "packed": bool(f[2]), "ray_constrained": bool(f[3]),
+            "pcg_planned": bool(q[3]), "pcg_runs": q[0], "pcg_steps": q[1], "pcg_fallbacks": q[2]}
 
 
 def version() -> str:

@@ -621,17 +621,37 @@ def test_fused_edge_reduce_is_bitwise_the_separate_launch(backend, monkeypatch, 
     assert np.array_equal(T_f, T_s) and np.array_equal(dx_f, dx_s)
 
 
-@pytest.mark.parametrize("dense", [True, False])
-def test_factorisation_timeout_is_an_error_not_a_singular_system(backend, monkeypatch, dense):
-    """A bounded device-side wait of the dataflow factorisation that gives up (forced here with
-    the test hook M3S_TEST_FORCE_TIMEOUT: every ready wait times out at once) raises
-    RuntimeError (M3S_ERR_TIMEOUT) instead of passing for a singular system (dx = 0, early exit);
-    the GPU drains normally and the next call without the hook is correct again."""
+def _solver_graph(monkeypatch, solver):
+    """The graph and solver switches of the factorisation-robustness tests: the dense solver or
+    the multi plan on a cfg4-topology graph, or the DEFAULT solver on a cfg3-topology graph (the
+    hybrid plan, its core factored by chol_df)."""
+    if solver == "hybrid":
+        g = synth.make_graph("cfg3", H=24, W=32, seed=6)
+        p = backend_plan(g)
+        assert p["solver"] == "hybrid" and p["core_poses"] > 0, p
+        return g
     g = synth.make_graph("cfg4", H=24, W=32, seed=6)
-    if dense:
+    if solver == "dense":
         monkeypatch.setenv("M3S_SOLVER_DENSE", "1")
     else:
         monkeypatch.setenv("M3S_SOLVER", "2")
+    return g
+
+
+def backend_plan(g):
+    import mast3r_slam_backends as mb
+
+    return mb.gn_plan_info(g.ii.tolist(), g.jj.tolist(), g.Twc.shape[0])
+
+
+@pytest.mark.parametrize("solver", ["dense", "multi", "hybrid"])
+def test_factorisation_timeout_is_an_error_not_a_singular_system(backend, monkeypatch, solver):
+    """A bounded device-side wait of the dataflow factorisation that gives up (forced here with
+    the test hook M3S_TEST_FORCE_TIMEOUT: every ready wait times out at once) raises
+    RuntimeError (M3S_ERR_TIMEOUT) instead of passing for a singular system (dx = 0, early exit);
+    the GPU drains normally and the next call without the hook is correct again.
+    Also the default solver on a cfg3-sized graph (hybrid, chol_df core)."""
+    g = _solver_graph(monkeypatch, solver)
     monkeypatch.setenv("M3S_CHOL_DF", "1")
     T_ok, dx_ok = _run_gpu(backend, g, "rays", 2)
     backend.gn_check()  # nothing pending
@@ -680,34 +700,28 @@ def test_factorisation_timeout_sync_report(backend, monkeypatch):
     assert "RAISED" in r.stdout and "timed out" in r.stdout, (r.stdout, r.stderr[-2000:])
 
 
+@pytest.mark.parametrize("solver", ["multi", "hybrid"])
 @pytest.mark.parametrize("nblocks", [128, 256])
-def test_dataflow_factor_with_cus_held_by_another_stream(backend, monkeypatch, nblocks):
-    """chol_df is a plain launch whose spin waits assume its whole grid is resident (the
-    occupancy query sizes it for an idle GPU).  SURVEY.md §8(b): the tracker and the backend
-    launch on the same GPU concurrently.  Here workgroups on a second stream hold 64 KiB of LDS on
-    about half / all of the CUs for 30 ms -- chol_df's 131-KiB workgroups do not fit beside them,
-    so part (or all) of its grid starts late while the resident part waits.  The op must either
-    finish with bitwise the poses of an unhindered run or raise M3S_ERR_TIMEOUT with the poses
-    restored -- never return other poses."""
+def test_dataflow_factor_with_cus_held_by_another_stream(backend, monkeypatch, nblocks, solver):
+    """the tracker and the backend launch on the same GPU concurrently.  Here
+    workgroups on a second stream hold 64 KiB of LDS on about half / all of the CUs for 30 ms --
+    chol_df's 131-KiB workgroups do not fit beside them, so part (or all) of its grid starts late.
+    chol_df's workgroups claim their tasks dynamically (round 6), so the resident part only ever
+    waits on tasks running workgroups hold: the op finishes with BITWISE the poses of an unhindered
+    run -- no timeout branch.  The multi plan (cfg4 topology) and the default
+    hybrid plan (cfg3 topology, chol_df core)."""
     from mast3r_slam_backends import variants
 
-    g = synth.make_graph("cfg4", H=24, W=32, seed=6)
-    monkeypatch.setenv("M3S_SOLVER", "2")
+    g = _solver_graph(monkeypatch, solver)
     monkeypatch.setenv("M3S_CHOL_DF", "1")
     T_ref, dx_ref = _run_gpu(backend, g, "rays", 3)
     backend.gn_check()
     side = torch.cuda.Stream()
     variants.hold_cus(nblocks, 64 * 1024, 30000, side)
-    T_h, dx_h = _run_gpu(backend, g, "rays", 3)  # (the error, if any, is deferred)
-    try:
-        backend.gn_check()
-    except RuntimeError as e:
-        assert "timed out" in str(e), e
-        assert np.array_equal(T_h, g.Twc.numpy())
-        print("timed out (poses restored)")
-    else:
-        assert np.array_equal(T_h, T_ref) and np.array_equal(dx_h, dx_ref)
+    T_h, dx_h = _run_gpu(backend, g, "rays", 3)
+    backend.gn_check()  # no deferred timeout
     torch.cuda.synchronize()
+    assert np.array_equal(T_h, T_ref) and np.array_equal(dx_h, dx_ref)
 
 
 @pytest.mark.parametrize("mode", ["rays", "calib"])

@@ -130,6 +130,27 @@ def test_random_graphs_plan_invariants(backend, seed):
     simulate(ii, jj, len(used), p, cap)
 
 
+@pytest.mark.parametrize("N,extra,seed", [(1250, 3, 0), (1400, 4, 1), (1800, 2, 2)])
+def test_large_graphs_core_fits_when_the_untrimmed_plan_fits(backend, monkeypatch, N, extra, seed):
+    """The multi plan's tile-aware stop (M3S_MULTI_KMIN) must never leave a core above the dense
+    solve limit (8192 unknowns) where the plan without the stop fits: large random
+    loop-closure graphs, both plans replayed."""
+    rng = np.random.default_rng(seed)
+    und = [(k - 1, k) for k in range(1, N)]
+    for _ in range(extra * N):
+        a, b = rng.integers(0, N, 2)
+        if a != b:
+            und.append((int(a), int(b)))
+    ii = [a for a, b in und] + [b for a, b in und]
+    jj = [b for a, b in und] + [a for a, b in und]
+    p = backend.gn_plan_info(ii, jj, N)
+    simulate(ii, jj, N, p, 32 if p["solver"] == "multi" else 64)
+    monkeypatch.setenv("M3S_MULTI_KMIN", "0")
+    p0 = backend.gn_plan_info(ii, jj, N)
+    if p0["core_fits"]:
+        assert p["core_fits"], (p["core_unknowns_padded"], p0["core_unknowns_padded"])
+
+
 def test_edge_cases(backend):
     p = backend.gn_plan_info([], [], 1)
     assert p["solver"] is None and p["order"] == []

@@ -72,6 +72,10 @@ int main(int argc, char** argv) {
         a.spin_limit = 1 << 22;
         a.trace = dtr;
         a.x = dX;
+        a.xg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.ready) + chol_words_bytes(npad));
+        a.xgran = 1;
+        a.tick = a.ready + chol_nwords(npad);
+        a.dyn = getenv("M3S_DF_DYN") ? atoi(getenv("M3S_DF_DYN")) : 1;
         int per = 0, ncu = 0;
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)chol_df_kernel, NT, 0));
         CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
