@@ -708,6 +708,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
     if (sp.pcg) {
         sp.o_pcgx = take(sizeof(double) * (size_t)npose * 7 * sp.pcg_ldx);
+        sp.o_pcgxt = take(sizeof(float) * (size_t)npose * 7 * sp.pcg_ldt);
         sp.o_gran = take(16 * 2 * (size_t)sp.pcg_nv);
     }
     // the plan integers in one array (layout: SparsePlan), the rounds BEFORE tmap: a launch that
@@ -1376,7 +1377,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
 }
 
 // ---- the lagged-factor PCG (gn_pcg.hip) ----
-// M3S_GN_PCG (default 1): from iteration M3S_PCG_FROM (default 2) on, the step is solved by CG
+// From iteration M3S_PCG_FROM (default 2) on, the step may be solved by CG
 // preconditioned with the inverse of iteration (M3S_PCG_FROM - 1)'s system, which that
 // iteration's direct factorisation provides (sp_inverse_kernel); the direct solve stays enqueued
 // behind every PCG launch as its fallback and returns at once when the PCG converged.  Plans whose
@@ -1387,24 +1388,43 @@ int pcg_from() {
     static const int v = std::max(1, env_int("M3S_PCG_FROM", 2));
     return v;
 }
+// M3S_GN_PCG: 0 off; 1 (default) when the direct solve's dense core has >= M3S_PCG_MIN_TILES (8)
+// tile columns -- its factorisation chain (~14 us per column on one CU) is then what the
+// iteration waits for; with fewer, the chain is short and the direct launches behind the PCG
+// (its fallback: each costs ~5 us even when it returns at once, rocprofv3 trace) eat the gain
+// (cfg3: 4 tile columns) -- 2 always.
 void choose_pcg(const m3s_gn_args& a, const Ctx& c, const Plan& plan, int npose, SparsePlan& sp) {
     sp.pcg = false;
     const int n = 7 * npose;
-    if (env_int("M3S_GN_PCG", 1) == 0 || c.ref_order || !sp.enabled || sp.fused || (sp.hybrid && !sp.core_df) ||
-        env_int("M3S_SOLVE_COOP", 0) != 0 || a.max_iter <= pcg_from() || n > kPcgMaxN || n < 7)
+    const int mode = env_int("M3S_GN_PCG", 1);
+    const int min_tiles = env_int("M3S_PCG_MIN_TILES", 8);
+    if (mode == 0 || (mode == 1 && sp.npad_tail / kCholTile < min_tiles) || c.ref_order || !sp.enabled ||
+        sp.fused || (sp.hybrid && !sp.core_df) || env_int("M3S_SOLVE_COOP", 0) != 0 || a.max_iter <= pcg_from() ||
+        n > kPcgMaxN || n < 7)
         return;
-    // rows of M per workgroup: a power of two (4 .. 32), the smallest giving <= M3S_PCG_WG
+    // rows of M per workgroup: 12 or 24, the smaller one giving <= M3S_PCG_WG
     // workgroups (default 64) -- or the largest whose f32 rows fit the LDS beside the vector and
     // the product's lists; never more than 240 workgroups (all resident at once, at most one per CU)
     const int wg_cap = std::max(1, env_int("M3S_PCG_WG", 64));
-    const int nadj = npose + 2 * (int)plan.pairs.size();
-    int R = 4;
-    while (R < 32 && (n + R - 1) / R > wg_cap && pcg_lds_bytes(n, 2 * R, nadj) <= (size_t)kPcgMaxLds) R *= 2;
-    if ((n + R - 1) / R > 240 || pcg_lds_bytes(n, R, nadj) > (size_t)kPcgMaxLds) return;
+    // the most (row, block) items of a workgroup's rows: R rows span <= R / 7 + 2 poses
+    std::vector<int> deg((size_t)npose, 1);
+    for (const auto& pr : plan.pairs) {
+        deg[pr.first]++;
+        deg[pr.second]++;
+    }
+    const int maxdeg = npose > 0 ? *std::max_element(deg.begin(), deg.end()) : 1;
+    auto items = [&](int R) { return 7 * maxdeg * (R / 7 + 2); };
+    // (R = threads / 64 or threads / 32: a row's threads stay within one wave, a power of two)
+    int R = kPcgThreads / 64;
+    if ((n + R - 1) / R > wg_cap && pcg_lds_bytes(n, 2 * R, items(2 * R)) <= (size_t)kPcgMaxLds) R *= 2;
+    if ((n + R - 1) / R > 240 || pcg_lds_bytes(n, R, items(R)) > (size_t)kPcgMaxLds) return;
+    if (inverse_lds_bytes(sp.npad_tail) > (size_t)kPcgMaxLds) return;  // M's core rows in LDS
+    sp.pcg_nitem = items(R);
     sp.pcg = true;
     sp.pcg_R = R;
     sp.pcg_nwg = (n + R - 1) / R;
-    sp.pcg_ldx = (int)align_up((size_t)n, kCholTile);
+    sp.pcg_ldx = (int)align_up((size_t)n, 16);
+    sp.pcg_ldt = (int)align_up((size_t)n, 4);
     sp.pcg_nv = pcg_nv(n);
     // the matrix-vector product's lists: per pose its diagonal block, then its pair blocks
     sp.apt.assign((size_t)npose + 1, 0);
@@ -1449,6 +1469,8 @@ int enqueue_inverse(const m3s_gn_args& a, Ctx& c) {
     v.Hd = sp.dptr<double>(sp.o_dense);
     v.Linv = sp.dptr<double>(sp.o_linv);
     v.X = sp.dptr<double>(sp.o_pcgx);
+    v.Xt = sp.dptr<float>(sp.o_pcgxt);
+    v.ldt = sp.pcg_ldt;
     v.flags = c.at<int>(c.L.flags);
     // M3S_PCG_SIDE (default 1): on the side stream, beside the next iteration's accumulate (it
     // reads the factor and the flags, writes X only; the next PCG launch waits for it); 0: on
@@ -1464,7 +1486,32 @@ int enqueue_inverse(const m3s_gn_args& a, Ctx& c) {
     if (rc) return rc;
     M3S_HIP_CHECK(hipEventRecord(e1, c.st));
     M3S_HIP_CHECK(hipStreamWaitEvent(ss, e1, 0));
+    // M3S_PCG_DEBUG=1: the refresh's duration on the side stream (timing events; serialises)
+    static const bool dbg = env_int("M3S_PCG_DEBUG", 0) != 0;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    static long long* ibuf = nullptr;
+    if (dbg && !ibuf && hipMalloc(&ibuf, sizeof(long long) * 8) != hipSuccess) ibuf = nullptr;
+    v.dbg = dbg ? ibuf : nullptr;
+    if (dbg) {
+        if (ibuf) M3S_HIP_CHECK(hipMemsetAsync(ibuf, 0, sizeof(long long) * 8, ss));
+        M3S_HIP_CHECK(hipEventCreate(&t0));
+        M3S_HIP_CHECK(hipEventCreate(&t1));
+        M3S_HIP_CHECK(hipEventRecord(t0, ss));
+    }
     M3S_HIP_CHECK(launch_sp_inverse(ss, v));
+    if (dbg) {
+        M3S_HIP_CHECK(hipEventRecord(t1, ss));
+        M3S_HIP_CHECK(hipEventSynchronize(t1));
+        float ms = 0.f;
+        M3S_HIP_CHECK(hipEventElapsedTime(&ms, t0, t1));
+        long long h[8] = {0};
+        if (ibuf) M3S_HIP_CHECK(hipMemcpy(h, ibuf, sizeof(h), hipMemcpyDeviceToHost));
+        fprintf(stderr, "pcg inverse (M refresh): %.1f us, %d workgroups; wg0: init %.1f fwd rounds %.1f core %.1f back rounds %.1f f32 copy %.1f us\n",
+                ms * 1e3, (v.n + 15) / 16, (h[1] - h[0]) * 0.01, (h[2] - h[1]) * 0.01, (h[3] - h[2]) * 0.01,
+                (h[4] - h[3]) * 0.01, (h[5] - h[4]) * 0.01);
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+    }
     M3S_HIP_CHECK(hipEventRecord(e2, ss));
     c.inv_pending = true;
     c.inv_done = e2;
@@ -1478,17 +1525,16 @@ int enqueue_pcg(const m3s_gn_args& a, Ctx& c) {
     g.A = g.b + sp.bpad;
     g.adj_ptr = sp.iptr(sp.i_apt);
     g.adj = reinterpret_cast<const int2*>(sp.iptr(sp.i_adj));
-    g.npose = (int)(a.N - 1);
-    g.nadj = (int)(sp.adj.size() / 2);
-    g.napt4 = pcg_napt4(g.npose);
-    g.X = sp.dptr<double>(sp.o_pcgx);
-    g.ldx = sp.pcg_ldx;
+    g.nitem = sp.pcg_nitem;
+    g.R4 = pcg_r4(sp.pcg_R);
+    g.Xt = sp.dptr<float>(sp.o_pcgxt);
+    g.ldt = sp.pcg_ldt;
     g.n = 7 * (int)(a.N - 1);
     g.nv = sp.pcg_nv;
     g.R = sp.pcg_R;
     g.nwg = sp.pcg_nwg;
     g.gran = reinterpret_cast<unsigned long long*>(sp.dbuf + sp.o_gran);
-    // tags: unique within the call (the granules are zeroed per call), kmax + 1 exchanges a launch
+    // tags: unique within the call (the granules are zeroed per call), 2 kmax + 1 exchanges a launch
     static const int kmax = std::max(1, std::min(200, env_int("M3S_PCG_KMAX", 30)));
     static const double tol = [] {
         const char* e = getenv("M3S_PCG_TOL");
@@ -1496,7 +1542,7 @@ int enqueue_pcg(const m3s_gn_args& a, Ctx& c) {
     }();
     g.kmax = kmax;
     g.tol2 = tol * tol;
-    g.tag0 = 1u + (unsigned)c.pcg_launches * (unsigned)(kmax + 2);
+    g.tag0 = 1u + (unsigned)c.pcg_launches * (unsigned)(2 * kmax + 2);
     c.pcg_launches++;
     const char* ft = getenv("M3S_TEST_FORCE_TIMEOUT");
     g.spin_limit = (ft && atoi(ft) != 0) ? 0 : (1 << 22);
@@ -1506,7 +1552,29 @@ int enqueue_pcg(const m3s_gn_args& a, Ctx& c) {
     g.delta_thresh = a.delta_thresh;
     g.contract = a.contract;
     g.flags = c.at<int>(c.L.flags);
+    // M3S_PCG_DEBUG=1: workgroup 0's phase clocks, printed after the launch (the wait serialises
+    // the call: diagnostics only)
+    static const bool dbg = env_int("M3S_PCG_DEBUG", 0) != 0;
+    static long long* dbuf = nullptr;
+    if (dbg && !dbuf && hipMalloc(&dbuf, sizeof(long long) * kPcgDbgSlots) != hipSuccess) dbuf = nullptr;
+    if (dbg && dbuf) M3S_HIP_CHECK(hipMemsetAsync(dbuf, 0, sizeof(long long) * kPcgDbgSlots, c.st));
+    g.dbg = dbg ? dbuf : nullptr;
     M3S_HIP_CHECK(launch_pcg(c.st, g));
+    if (g.dbg) {
+        long long h[kPcgDbgSlots];
+        M3S_HIP_CHECK(hipMemcpyAsync(h, dbuf, sizeof(h), hipMemcpyDeviceToHost, c.st));
+        M3S_HIP_CHECK(hipStreamSynchronize(c.st));
+        // s_memrealtime: 100 MHz
+        fprintf(stderr, "pcg[%d] R %d nwg %d: stage %.2f us, z0 %.2f us;", c.pcg_launches - 1, g.R, g.nwg,
+                (h[1] - h[0]) * 0.01, (h[2] - h[1]) * 0.01);
+        long long prev = h[2];
+        for (int st = 1; 3 * st + 2 < kPcgDbgSlots && h[3 * st + 2] != 0; st++) {
+            fprintf(stderr, " [Ap %.2f pq %.2f z %.2f]", (h[3 * st] - prev) * 0.01, (h[3 * st + 1] - h[3 * st]) * 0.01,
+                    (h[3 * st + 2] - h[3 * st + 1]) * 0.01);
+            prev = h[3 * st + 2];
+        }
+        fprintf(stderr, "\n");
+    }
     return M3S_OK;
 }
 

@@ -204,19 +204,24 @@ struct InvArgs {
     int n, ldx, nrounds, ntail, npad;
     const int *rounds, *nodes, *fptr, *fronts, *inl, *rc4, *tail;
     const double *Lstore, *W, *Hd, *Linv;
-    double* X;
+    double* X;       // [n][ldx] f64 work (the columns as they are solved)
+    float* Xt;       // [n][ldt] f32: M row-major (= its columns: M is symmetric), what the PCG reads
+    int ldt;         // n rounded up to 4
     const int* flags;
+    long long* dbg;  // M3S_PCG_DEBUG: workgroup 0's phase clocks (6), else null
 };
+size_t inverse_lds_bytes(int npad);  // (the core's rows of 16 columns live in LDS: npad <= ~900)
 hipError_t launch_sp_inverse(hipStream_t st, const InvArgs& a);
-constexpr int kPcgMaxN = 2048;               // unknowns the PCG takes (8 vector entries per thread)
+constexpr int kPcgThreads = 768;             // threads of a PCG workgroup
+constexpr int kPcgMaxN = 2304;               // unknowns the PCG takes (3 vector entries per thread)
 constexpr int kPcgMaxLds = 160 * 1024 - 1024;  // dynamic LDS of one PCG workgroup
 struct PcgArgs {
     const double *b, *A;           // the block-format system (gn_assemble_kernel)
     const int* adj_ptr;            // per pose: its blocks (the diagonal first) ...
-    const int2* adj;               // ... as (block, other pose); both staged in LDS
-    int npose, nadj, napt4;        // poses, list entries, adj_ptr's LDS ints (pcg_napt4)
-    const double* X;               // M = X (sp_inverse_kernel), row-major, ld ldx
-    int64_t ldx;
+    const int2* adj;               // ... as (block, other pose)
+    int nitem, R4;                 // max (row, block) items of a workgroup's rows (LDS), pcg_r4(R)
+    const float* Xt;               // M (sp_inverse_kernel's f32 copy), row-major, ld ldt
+    int ldt;
     int n, nv, R, nwg;             // unknowns, vector stride (pcg_nv), rows of M per workgroup, workgroups
     unsigned long long* gran;      // 2 x nv x 16 B: the z exchange's data-tagged granules (zeroed per call)
     unsigned tag0;                 // this launch's first tag (unique within the call)
@@ -228,10 +233,12 @@ struct PcgArgs {
     float delta_thresh;
     int contract;
     int* flags;
+    long long* dbg;                // M3S_PCG_DEBUG: phase clocks of workgroup 0 (kPcgDbgSlots), else null
 };
+constexpr int kPcgDbgSlots = 128;
 int pcg_nv(int n);
-int pcg_napt4(int npose);
-size_t pcg_lds_bytes(int n, int R, int nadj);
+int pcg_r4(int R);
+size_t pcg_lds_bytes(int n, int R, int nitem);
 hipError_t launch_pcg(hipStream_t st, const PcgArgs& a);
 // Fused single-workgroup solve (gn_solve.hip)
 constexpr int kSolveThreads = 256;

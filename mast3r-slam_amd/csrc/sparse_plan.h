@@ -31,8 +31,8 @@ struct SparsePlan {
     // PCG iterations (gn_pcg.hip; set by the driver): M's rows per workgroup, workgroups, X's
     // leading dimension, the vector stride; device: X (n x ldx f64) and the exchange granules
     bool pcg = false;
-    int pcg_R = 0, pcg_nwg = 0, pcg_ldx = 0, pcg_nv = 0;
-    size_t o_pcgx = 0, o_gran = 0;
+    int pcg_R = 0, pcg_nwg = 0, pcg_ldx = 0, pcg_ldt = 0, pcg_nv = 0, pcg_nitem = 0;
+    size_t o_pcgx = 0, o_pcgxt = 0, o_gran = 0;
     int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
     std::vector<SpRound> rounds;
     std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;

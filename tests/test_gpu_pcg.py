@@ -31,6 +31,7 @@ def _graph(cfg, H, W, seed=None):
 
 
 def _run(backend, monkeypatch, g, mode, iters, **env):
+    env.setdefault("M3S_GN_PCG", 2)  # (the default enables it on cores of >= 8 tile columns only)
     for k, v in env.items():
         monkeypatch.setenv(k, str(v))
     monkeypatch.setenv("M3S_GN_DEBUG_FLAGS", "2")
@@ -47,7 +48,7 @@ def _run(backend, monkeypatch, g, mode, iters, **env):
 def test_pcg_runs_and_matches_the_direct_solve(backend, monkeypatch, cfg, H, W):
     """Both bench topologies (cfg3: the hybrid plan; cfg4: the multi plan), 10 iterations: eight
     PCG solves, none falling back; poses within 1e-6 of the direct solve's (the CG stop is
-    sqrt(r'z / r0'z0) <= 1e-7) and bitwise reproducible."""
+    sqrt(r'z / r0'z0) <= 1e-6) and bitwise reproducible."""
     mode = synth.CONFIGS[cfg]["mode"]
     g = _graph(cfg, H, W)
     T_d, dx_d, st_d = _run(backend, monkeypatch, g, mode, 10, M3S_GN_PCG=0)
@@ -88,7 +89,7 @@ def test_pcg_fallback_is_bitwise_the_direct_solve(backend, monkeypatch):
 
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "T.npy")
-        env = dict(os.environ, M3S_PCG_KMAX="1", M3S_GN_DEBUG_FLAGS="2")
+        env = dict(os.environ, M3S_PCG_KMAX="1", M3S_GN_DEBUG_FLAGS="2", M3S_GN_PCG="2")
         r = subprocess.run([sys.executable, "-c", code, out], env=env, capture_output=True, text=True, timeout=240,
                            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         assert r.returncode == 0, r.stderr[-2000:]
@@ -99,11 +100,12 @@ def test_pcg_fallback_is_bitwise_the_direct_solve(backend, monkeypatch):
 
 @pytest.mark.parametrize("cfg,H,W", [("cfg3", 384, 512), ("cfg4", 384, 512)])
 def test_pcg_bench_graphs_full_size_within_1e5_of_oracle(backend, oracle, monkeypatch, cfg, H, W):
-    """The timed workloads at full 512x384 (10 iterations, PCG from iteration 2): within
-    north_star's 1e-5 of the CPU oracle."""
+    """The timed workloads at full 512x384 (10 iterations, PCG from iteration 2 -- by default on
+    cfg4, whose core has 14 tile columns; forced on cfg3's 4): within north_star's 1e-5 of the CPU
+    oracle."""
     mode = synth.CONFIGS[cfg]["mode"]
     g = _graph(cfg, H, W)
-    T_p, _, st = _run(backend, monkeypatch, g, mode, 10)
+    T_p, _, st = _run(backend, monkeypatch, g, mode, 10, M3S_GN_PCG=1 if cfg == "cfg4" else 2)
     assert st["pcg_runs"] == 8 and st["pcg_fallbacks"] == 0, st
     T_o, _, _ = _run_oracle(oracle, g, mode, 10)
     d = _rel(T_p, T_o)

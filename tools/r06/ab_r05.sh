@@ -13,3 +13,4 @@ run direct M3S_GN_PCG=0 timeout -k 10 200 python -u bench.py --no-cpu-baseline -
 run pcg timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-matching
 run r05b M3S_BACKEND_LIB=mast3r-slam_amd/lib_r05/libm3s_backend.so timeout -k 10 200 python -u bench_r05.py --no-cpu-baseline --no-matching
 timeout -k 10 400 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_gpu_pcg.py -s > gpurun_out/r06_e_pytest_pcg.log 2>&1; tail -12 gpurun_out/r06_e_pytest_pcg.log
+timeout -k 10 300 python -u tools/r06/pcg_debug.py > gpurun_out/r06_e_pcg_debug.log 2>&1; tail -20 gpurun_out/r06_e_pcg_debug.log
