@@ -336,16 +336,18 @@ def time_config(cfg, iters_arg, steps, warmup, world, rank, rehearse, dev, comm)
 
 
 def _solve_path(st, iters, solve_ms):
-    """How a call solved its iterations: the direct block-sparse factorisation (iterations 0-1,
-    and any fallback) and the lagged-factor PCG (gn_pcg.hip) from iteration 2 on; the solve phase
-    per iteration (events of the untimed phase step) before and from iteration 2."""
+    """How a call solved its iterations: the direct block-sparse factorisation (the first
+    iterations, M3S_PCG_FROM = 3 by default, and any fallback) and the lagged-factor PCG
+    (gn_pcg.hip) after them; the solve phase per iteration (events of the untimed phase step)
+    before and from the first PCG iteration."""
     runs = st["pcg_runs"]
-    head, tail = solve_ms[:2], solve_ms[2:iters]
+    k = iters - runs  # the first PCG iteration (PCG runs on every iteration from it on)
+    head, tail = solve_ms[:k], solve_ms[k:iters]
     return {"pcg_planned": st["pcg_planned"], "direct_iterations": iters - runs + st["pcg_fallbacks"],
             "pcg_iterations": runs - st["pcg_fallbacks"], "pcg_fallbacks": st["pcg_fallbacks"],
             "cg_steps_per_pcg_solve": (st["pcg_steps"] / runs) if runs else None,
-            "solve_ms_iterations_0_1": (sum(head) / len(head)) if head else None,
-            "solve_ms_iterations_2_on": (sum(tail) / len(tail)) if tail else None}
+            "solve_ms_before_pcg": (sum(head) / len(head)) if head else None,
+            "solve_ms_pcg_iterations": (sum(tail) / len(tail)) if tail else None}
 
 
 def launch_spread(ms):

@@ -688,6 +688,8 @@ bool hyb_core_fits(const SparsePlan& p) {
     return hyb_core_df() ? p.ntail <= kHybDfTailMax : p.fused_tail;
 }
 
+int pcg_lag();
+
 int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -707,9 +709,14 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     }
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
     if (sp.pcg) {
+        sp.snap_bytes = 0;
+        if (pcg_lag() >= 2) {
+            sp.snap_bytes = (sp.npad_tail > 0 ? sp.o_linv + chol_linv_bytes(sp.npad_tail) : sp.o_xd) - sp.o_L;
+            sp.o_snap = take(sp.snap_bytes);
+        }
         sp.o_pcgx = take(sizeof(double) * (size_t)npose * 7 * sp.pcg_ldx);
         sp.o_pcgxt = take(sizeof(float) * (size_t)npose * 7 * sp.pcg_ldt);
-        sp.o_gran = take(16 * 2 * (size_t)sp.pcg_nv);
+        sp.o_gran = take(16 * 4 * (size_t)sp.pcg_nv);
     }
     // the plan integers in one array (layout: SparsePlan), the rounds BEFORE tmap: a launch that
     // only back-substitutes stages [nodes fptr fronts tail rounds] and not the core map
@@ -737,7 +744,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         M3S_HIP_CHECK(hipMemsetAsync(chol_ready_ptr(sp.dptr<double>(sp.o_linv), sp.npad_tail), 0,
                                      chol_ready_bytes(sp.npad_tail), st));
     if (sp.pcg)  // the exchange's tags start below every launch's
-        M3S_HIP_CHECK(hipMemsetAsync(sp.dbuf + sp.o_gran, 0, 16 * 2 * (size_t)sp.pcg_nv, st));
+        M3S_HIP_CHECK(hipMemsetAsync(sp.dbuf + sp.o_gran, 0, 16 * 4 * (size_t)sp.pcg_nv, st));
     if (n > 0) {
         int* h = reinterpret_cast<int*>(stagings().out.get(sizeof(int) * n));
         M3S_REQUIRE(h != nullptr, "gauss_newton: pinned host allocation failed");
@@ -885,9 +892,32 @@ int prepare_iterations(const m3s_gn_args& a, Ctx& c);
 
 // early_pack: launch the packed stream (prepare_iterations) as soon as the edge lists are on
 // the device, before the host builds the accumulate schedule
+// The per-call solver buffers come from the device's default stream-ordered pool
+// (hipMallocAsync); its default release threshold (0) hands freed memory back to the driver at
+// every synchronisation -- and the call synchronises once on its edge lists -- so every call
+// mapped its buffers again (~10 MB with the PCG's M and factor copy).  M3S_POOL_KEEP_MB (default
+// 1024): keep that much cached in the pool.  Once per device; the pool is the HIP runtime's (not
+// torch's caching allocator).
+void keep_pool() {
+    static std::mutex mu;
+    static bool done[64] = {false};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done[dev]) return;
+    done[dev] = true;
+    const long mb = env_int("M3S_POOL_KEEP_MB", 1024);
+    if (mb <= 0) return;
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return;
+    uint64_t thr = (uint64_t)mb << 20;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+}
+
 int setup(const m3s_gn_args& a, Ctx& c, bool early_pack = false) {
     int rc = validate(a);
     if (rc) return rc;
+    keep_pool();
     c.st = (hipStream_t)a.stream;
     c.ws = (char*)a.ws;
     c.L = make_layout(a.mode, a.N, a.HW, a.E_total, a.E_local);
@@ -1195,7 +1225,9 @@ hipError_t launch_gn_solve_dbg(hipStream_t st, const SolveArgs& S) {
     return e;
 }
 
-int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
+// fallback: the direct solve enqueued behind a PCG launch (it runs only when the PCG did not
+// converge; otherwise each of its launches returns at once, ~4-5 us apiece)
+int enqueue_solve(const m3s_gn_args& a, Ctx& c, bool fallback = false) {
     const Layout& L = c.L;
     const int npose = (int)(a.N - 1);
     int* flags = c.at<int>(L.flags);
@@ -1292,7 +1324,11 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     // 0.43 ms cooperative groups -- in-kernel a round's chain is ~4 us, but coherent (MALL)
     // block traffic + write-through + the barrier cost as much as the ~5 us launch overhead saved
     static const int coop_mode = env_int("M3S_SOLVE_COOP", 0);
-    const bool coop = coop_mode != 0;
+    // M3S_PCG_FALLBACK_COOP (default 1): a PCG iteration's fallback runs its rounds (and the
+    // hybrid core's fill) as the one all-rounds launch -- slower when it runs, but a converged
+    // PCG skips one launch instead of one per round (cfg3: 5 round launches + the fill)
+    static const bool fb_coop = env_int("M3S_PCG_FALLBACK_COOP", 0) != 0;
+    const bool coop = coop_mode != 0 || (fallback && fb_coop);
     if (coop) {
         c.may_timeout = true;  // grid barriers
         SpCoopArgs ca{};
@@ -1327,10 +1363,11 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
     // the in-register core, <= 27 poses.  The planner read the switch (hyb_core_df) and sized the
     // core for it: the plan carries the choice.
     const bool core_df = sp.core_df;
-    if (sp.hybrid && core_df && !coop && sp.ntail > 0) {
+    if (sp.hybrid && core_df && sp.ntail > 0) {
         c.may_timeout = true;  // chol_df's bounded waits
-        M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
-                                          sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
+        if (!coop)  // (the all-rounds launch filled the core)
+            M3S_HIP_CHECK(launch_sp_tail_fill(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
+                                              sp.npad_tail, sp.dptr<double>(sp.o_dense), flags));
         M3S_HIP_CHECK(launch_dense_factor_solve(c.st, sp.npad_tail, sp.dptr<double>(sp.o_dense),
                                                 sp.dptr<double>(sp.o_linv), sp.dptr<double>(sp.o_xd), flags,
                                                 ++c.chol_epoch));
@@ -1377,15 +1414,25 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c) {
 }
 
 // ---- the lagged-factor PCG (gn_pcg.hip) ----
-// From iteration M3S_PCG_FROM (default 2) on, the step may be solved by CG
-// preconditioned with the inverse of iteration (M3S_PCG_FROM - 1)'s system, which that
+// From iteration M3S_PCG_FROM (default 3) on, the step may be solved by CG
+// preconditioned with the inverse of iteration (M3S_PCG_FROM - M3S_PCG_LAG)'s system, which that
 // iteration's direct factorisation provides (sp_inverse_kernel); the direct solve stays enqueued
 // behind every PCG launch as its fallback and returns at once when the PCG converged.  Plans whose
 // factor the inverse reads: elimination rounds by sp_round_kernel and a chol_df core (the hybrid
 // with M3S_HYB_CORE=1, the multi plan); not the single-workgroup solve, the reference-order mode,
 // the all-rounds launch or the dense solver.
 int pcg_from() {
-    static const int v = std::max(1, env_int("M3S_PCG_FROM", 2));
+    static const int v = std::max(1, env_int("M3S_PCG_FROM", 3));
+    return v;
+}
+// M3S_PCG_LAG (default 2): M is the inverse of iteration (M3S_PCG_FROM - lag)'s system.  With
+// lag 1 the inverse (~0.75 ms alone on cfg4, ~2.7 ms beside an accumulate that fills the chip:
+// rocprofv3 trace r06_l) runs over one accumulate and the first PCG waits ~0.7 ms for it; with
+// lag 2 it has an accumulate, a direct solve and another accumulate, and reads a copy of that
+// iteration's factor (the next direct solve overwrites the live one).  Refreshes after a PCG
+// that fell back use lag 1 (the next PCG waits for them).
+int pcg_lag() {
+    static const int v = std::max(1, std::min(pcg_from(), env_int("M3S_PCG_LAG", 2)));
     return v;
 }
 // M3S_GN_PCG: 0 off; 1 (default) when the direct solve's dense core has >= M3S_PCG_MIN_TILES (8)
@@ -1415,13 +1462,22 @@ void choose_pcg(const m3s_gn_args& a, const Ctx& c, const Plan& plan, int npose,
     const int maxdeg = npose > 0 ? *std::max_element(deg.begin(), deg.end()) : 1;
     auto items = [&](int R) { return 7 * maxdeg * (R / 7 + 2); };
     // (R = threads / 64 or threads / 32: a row's threads stay within one wave, a power of two)
-    int R = kPcgThreads / 64;
-    if ((n + R - 1) / R > wg_cap && pcg_lds_bytes(n, 2 * R, items(2 * R)) <= (size_t)kPcgMaxLds) R *= 2;
-    if ((n + R - 1) / R > 240 || pcg_lds_bytes(n, R, items(R)) > (size_t)kPcgMaxLds) return;
+    // M3S_PCG_ONEX (default 1): one exchange per CG step (B = M A's rows in LDS beside M's) where
+    // they fit (cfg3's 896 unknowns: yes; cfg4's 1792: no -- two exchanges per step)
+    auto pick = [&](bool ox) {
+        int R = kPcgThreads / 64;
+        auto fits = [&](int r) { return pcg_lds_bytes(n, r, items(r), ox) <= (size_t)kPcgMaxLds && (!ox || r <= kPcgMaxR); };
+        if ((n + R - 1) / R > wg_cap && fits(2 * R)) R *= 2;
+        return (n + R - 1) / R > 240 || !fits(R) ? 0 : R;
+    };
+    bool onex = env_int("M3S_PCG_ONEX", 0) != 0 && pick(true) > 0;
+    const int R = pick(onex);
+    if (R == 0) return;
     if (inverse_lds_bytes(sp.npad_tail) > (size_t)kPcgMaxLds) return;  // M's core rows in LDS
     sp.pcg_nitem = items(R);
     sp.pcg = true;
     sp.pcg_R = R;
+    sp.pcg_onex = onex;
     sp.pcg_nwg = (n + R - 1) / R;
     sp.pcg_ldx = (int)align_up((size_t)n, 16);
     sp.pcg_ldt = (int)align_up((size_t)n, 4);
@@ -1449,8 +1505,14 @@ void choose_pcg(const m3s_gn_args& a, const Ctx& c, const Plan& plan, int npose,
     }
 }
 
-int enqueue_inverse(const m3s_gn_args& a, Ctx& c) {
+// snapshot: read a copy of the factor taken now (sp.o_snap), not the live one
+int enqueue_inverse(const m3s_gn_args& a, Ctx& c, bool snapshot) {
     const SparsePlan& sp = c.sp;
+    const size_t shift = snapshot ? sp.o_snap - sp.o_L : 0;
+    if (snapshot) {
+        M3S_REQUIRE(sp.snap_bytes > 0, "PCG: no factor snapshot buffer");
+        M3S_HIP_CHECK(hipMemcpyAsync(sp.dbuf + sp.o_snap, sp.dbuf + sp.o_L, sp.snap_bytes, hipMemcpyDeviceToDevice, c.st));
+    }
     InvArgs v{};
     v.n = 7 * (int)(a.N - 1);
     v.ldx = sp.pcg_ldx;
@@ -1464,10 +1526,10 @@ int enqueue_inverse(const m3s_gn_args& a, Ctx& c) {
     v.inl = sp.iptr(sp.i_inl);
     v.rc4 = sp.iptr(sp.i_rc4);
     v.tail = sp.iptr(sp.i_tail);
-    v.Lstore = sp.dptr<double>(sp.o_L);
-    v.W = sp.dptr<double>(sp.o_W);
-    v.Hd = sp.dptr<double>(sp.o_dense);
-    v.Linv = sp.dptr<double>(sp.o_linv);
+    v.Lstore = sp.dptr<double>(sp.o_L + shift);
+    v.W = sp.dptr<double>(sp.o_W + shift);
+    v.Hd = sp.dptr<double>(sp.o_dense + shift);
+    v.Linv = sp.dptr<double>(sp.o_linv + shift);
     v.X = sp.dptr<double>(sp.o_pcgx);
     v.Xt = sp.dptr<float>(sp.o_pcgxt);
     v.ldt = sp.pcg_ldt;
@@ -1531,6 +1593,7 @@ int enqueue_pcg(const m3s_gn_args& a, Ctx& c) {
     g.ldt = sp.pcg_ldt;
     g.n = 7 * (int)(a.N - 1);
     g.nv = sp.pcg_nv;
+    g.onex = sp.pcg_onex ? 1 : 0;
     g.R = sp.pcg_R;
     g.nwg = sp.pcg_nwg;
     g.gran = reinterpret_cast<unsigned long long*>(sp.dbuf + sp.o_gran);
@@ -1754,17 +1817,17 @@ int run(const m3s_gn_args& a) {
             rc = enqueue_pcg(a, c);
             if (rc) return rc;
         }
-        rc = enqueue_solve(a, c);
+        rc = enqueue_solve(a, c, c.sp.pcg && itr >= pcg_from());
         if (rc) return rc;
         g_prof.mark(c.st);
         if (!c.sp.fused && !c.sp.hybrid)  // gn_solve retracts inside its launch
             M3S_HIP_CHECK(launch_retract(c.st, a.Twc, c.at<double>(L.x), a.dx, (int)a.N,
                                          a.delta_thresh, flags, a.contract));
-        // M for the next PCG iteration from this iteration's factor: the first direct solve
-        // before the PCG iterations, then after every PCG that fell back to the direct solve
+        // M from this iteration's factor: iteration M3S_PCG_FROM - M3S_PCG_LAG's (a copy of it
+        // when the lag is 2 or more), then after every PCG that fell back to the direct solve
         // (sp_inverse_kernel returns at once when this iteration's PCG converged: M stays)
-        if (c.sp.pcg && itr >= pcg_from() - 1 && itr + 1 < a.max_iter) {
-            rc = enqueue_inverse(a, c);
+        if (c.sp.pcg && (itr == pcg_from() - pcg_lag() || itr >= pcg_from()) && itr + 1 < a.max_iter) {
+            rc = enqueue_inverse(a, c, itr < pcg_from() - 1);
             if (rc) return rc;
         }
         g_prof.mark(c.st);

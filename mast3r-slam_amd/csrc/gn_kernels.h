@@ -223,7 +223,10 @@ struct PcgArgs {
     const float* Xt;               // M (sp_inverse_kernel's f32 copy), row-major, ld ldt
     int ldt;
     int n, nv, R, nwg;             // unknowns, vector stride (pcg_nv), rows of M per workgroup, workgroups
-    unsigned long long* gran;      // 2 x nv x 16 B: the z exchange's data-tagged granules (zeroed per call)
+    // onex: one exchange per CG step -- each workgroup also holds its rows of B = M A (f32, formed
+    // in the launch's staging) and publishes (A p, B p) together: z is updated as z - alpha B p
+    int onex;
+    unsigned long long* gran;      // 2 x 2 x nv x 16 B: the exchanges' data-tagged granules (zeroed per call)
     unsigned tag0;                 // this launch's first tag (unique within the call)
     double tol2;                   // converged when r'z <= tol2 * r0'z0
     int kmax, spin_limit;
@@ -236,9 +239,10 @@ struct PcgArgs {
     long long* dbg;                // M3S_PCG_DEBUG: phase clocks of workgroup 0 (kPcgDbgSlots), else null
 };
 constexpr int kPcgDbgSlots = 128;
+constexpr int kPcgMaxR = 24;  // rows per workgroup with onex (B's row sums in registers)
 int pcg_nv(int n);
 int pcg_r4(int R);
-size_t pcg_lds_bytes(int n, int R, int nitem);
+size_t pcg_lds_bytes(int n, int R, int nitem, bool onex);
 hipError_t launch_pcg(hipStream_t st, const PcgArgs& a);
 // Fused single-workgroup solve (gn_solve.hip)
 constexpr int kSolveThreads = 256;

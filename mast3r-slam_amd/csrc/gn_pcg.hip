@@ -356,6 +356,8 @@ __global__ __launch_bounds__(PTH) void pcg_kernel(PcgArgs a) {
     int* sib = sps + ni;                                   // [R + 1]: the rows' first item
     int* sabort = sib + a.R4;                              // this workgroup saw a gather give up
     float* Xs = reinterpret_cast<float*>(sabort + 4);      // [R][n]: this workgroup's rows of M
+    float* Bs = Xs + (size_t)R * n;                        // [R][n]: its rows of B = M A (onex)
+    const bool onex = a.onex != 0;
     if (tid == 0) *sabort = 0;
     // M3S_PCG_DEBUG (diagnostics): workgroup 0's wall clock at the phase ends, one slot per
     // phase (slot 0: entry, 1: staged, 2: z0 gathered, then per step 3s: q gathered, 3s+1: p'q,
@@ -399,42 +401,78 @@ __global__ __launch_bounds__(PTH) void pcg_kernel(PcgArgs a) {
         for (int u = 0; u < 4; u++)
             if (jj + u < n) Xs[i * n + jj + u] = vv[u];
     }
+    if (onex) {
+        // B = M A, this workgroup's rows: column c = 7 pj + d of B is sum over the blocks (pk, pj)
+        // of M's columns 7 pk .. 7 pk + 6 times the block's column d (the blocks are symmetric:
+        // Ji = -Jj makes every 7x7 block +-D with D symmetric, gn_refacc.hip header).  One thread
+        // per column, the R rows in registers, f64 sums rounded once to f32.
+        __syncthreads();  // (Xs staged)
+        for (int col = tid; col < n; col += PTH) {
+            const int pj = col / 7, d = col - 7 * pj;
+            double acc[kPcgMaxR];
+#pragma unroll
+            for (int i = 0; i < kPcgMaxR; i++) acc[i] = 0.0;
+            for (int it = a.adj_ptr[pj]; it < a.adj_ptr[pj + 1]; it++) {
+                const int2 bs = a.adj[it];
+                const double* Ab = a.A + (int64_t)bs.x * 49 + d;
+                double ac[7];
+#pragma unroll
+                for (int c = 0; c < 7; c++) ac[c] = Ab[7 * c];
+                const float* xk = Xs + 7 * bs.y;
+#pragma unroll
+                for (int i = 0; i < kPcgMaxR; i++)
+                    if (i < R) {
+#pragma unroll
+                        for (int c = 0; c < 7; c++) acc[i] = fma((double)xk[i * n + c], ac[c], acc[i]);
+                    }
+            }
+#pragma unroll
+            for (int i = 0; i < kPcgMaxR; i++)
+                if (i < R) Bs[i * n + col] = (float)acc[i];
+        }
+    }
     // full vectors in every workgroup (entry e in thread e % PTH); identical in all of them
-    double x[kNE], r[kNE], p[kNE], z[kNE], q[kNE];
+    double x[kNE], r[kNE], p[kNE], z[kNE], q[kNE], w[kNE];
 #pragma unroll
     for (int k = 0; k < kNE; k++) {
         const int e = tid + PTH * k;
         x[k] = 0.0;
         r[k] = e < n ? a.b[e] : 0.0;
-        p[k] = z[k] = q[k] = 0.0;
+        p[k] = z[k] = q[k] = w[k] = 0.0;
     }
     unsigned xchg = 0;  // exchanges so far (tag and buffer parity)
     // publish this workgroup's rows `val` (thread i < R holds row i), then gather every row into
     // out[] -- data-tagged granules, all of a thread's loads in flight together, double-buffered
     // by exchange parity (a workgroup reuses a buffer only after every other one published the
     // next exchange, i.e. finished reading this one)
-    auto exchange = [&](double val, double (&out)[kNE]) {
-        Gran* buf = reinterpret_cast<Gran*>(a.gran) + (int64_t)(xchg & 1) * a.nv;
+    auto exchange2 = [&](int nval, double val0, double val1, double (&out0)[kNE], double (&out1)[kNE]) {
+        Gran* buf = reinterpret_cast<Gran*>(a.gran) + (int64_t)(xchg & 1) * 2 * a.nv;
         const unsigned tag = a.tag0 + xchg;
         xchg++;
-        if (tid < R && row0 + tid < n) publish(buf + row0 + tid, tag, val);
+        if (tid < R && row0 + tid < n) {
+            publish(buf + row0 + tid, tag, val0);
+            if (nval > 1) publish(buf + a.nv + row0 + tid, tag, val1);
+        }
         bool ok = true;
-        unsigned need = 0;
+        unsigned need = 0;  // bit k: entry k of value 0; bit kNE + k: of value 1
 #pragma unroll
         for (int k = 0; k < kNE; k++)
-            if (tid + PTH * k < n) need |= 1u << k;
+            if (tid + PTH * k < n) need |= (nval > 1 ? 1u | 1u << kNE : 1u) << k;
         for (int spins = 0; need;) {
-            unsigned long long lo[kNE], hi[kNE];
+            unsigned long long lo[2 * kNE], hi[2 * kNE];
 #pragma unroll
-            for (int k = 0; k < kNE; k++)
+            for (int k = 0; k < 2 * kNE; k++)
                 if (need >> k & 1) {
-                    lo[k] = __hip_atomic_load(&buf[tid + PTH * k].lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    hi[k] = __hip_atomic_load(&buf[tid + PTH * k].hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const Gran* g = buf + (k >= kNE ? a.nv : 0) + tid + PTH * (k % kNE);
+                    lo[k] = __hip_atomic_load(&g->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    hi[k] = __hip_atomic_load(&g->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
 #pragma unroll
-            for (int k = 0; k < kNE; k++)
+            for (int k = 0; k < 2 * kNE; k++)
                 if ((need >> k & 1) && (unsigned)(lo[k] >> 32) == tag && (unsigned)(hi[k] >> 32) == tag) {
-                    out[k] = __hiloint2double((int)(unsigned)hi[k], (int)(unsigned)lo[k]);
+                    const double v = __hiloint2double((int)(unsigned)hi[k], (int)(unsigned)lo[k]);
+                    if (k < kNE) out0[k] = v;
+                    else out1[k - kNE] = v;
                     need &= ~(1u << k);
                 }
             if (!need) break;
@@ -453,6 +491,7 @@ __global__ __launch_bounds__(PTH) void pcg_kernel(PcgArgs a) {
         __syncthreads();
         return *sabort == 0;
     };
+    auto exchange = [&](double val, double (&out)[kNE]) { return exchange2(1, val, 0.0, out, out); };
     auto to_sv = [&](const double (&u)[kNE]) {
 #pragma unroll
         for (int k = 0; k < kNE; k++) {
@@ -476,7 +515,7 @@ __global__ __launch_bounds__(PTH) void pcg_kernel(PcgArgs a) {
         const double mine = tid < R ? sv[tid] : 0.0;
         return exchange(mine, z);
     };
-    auto apply_A = [&]() {  // -> q (p in sv)
+    auto apply_A = [&]() {  // -> q, and w = B p with onex (p in sv)
         to_sv(p);
         for (int it = tid; it < sib[R]; it += PTH) {
             const double* Ar = sA + 7 * it;
@@ -486,11 +525,21 @@ __global__ __launch_bounds__(PTH) void pcg_kernel(PcgArgs a) {
             for (int jj = 0; jj < 7; jj++) acc = fma(Ar[jj], ps[jj], acc);
             spart[it] = acc;
         }
+        double wrow = 0.0;
+        if (onex) {  // (the row sums of B p as apply_M's of M r)
+            const float* br = Bs + ri * n;
+            for (int jj = rs; jj < n; jj += tpr) wrow = fma((double)br[jj], sv[jj], wrow);
+            for (int o = tpr >> 1; o >= 1; o >>= 1) wrow += __shfl_xor(wrow, o);
+        }
         __syncthreads();
         double mine = 0.0;
         if (tid < R)
             for (int it = sib[tid]; it < sib[tid + 1]; it++) mine += spart[it];
-        return exchange(mine, q);
+        if (!onex) return exchange(mine, q);
+        if (rs == 0) sv[ri] = wrow;  // (p in sv was read before the barrier above)
+        __syncthreads();
+        const double wmine = tid < R ? sv[tid] : 0.0;
+        return exchange2(2, mine, wmine, q, w);
     };
     auto dot = [&](const double (&u)[kNE], const double (&v)[kNE]) {
         double s = 0.0;
@@ -526,8 +575,9 @@ __global__ __launch_bounds__(PTH) void pcg_kernel(PcgArgs a) {
         for (int k = 0; k < kNE; k++) {
             x[k] = fma(alpha, p[k], x[k]);
             r[k] = fma(-alpha, q[k], r[k]);
+            if (onex) z[k] = fma(-alpha, w[k], z[k]);  // z = M r = z - alpha M A p
         }
-        if (!apply_M()) {
+        if (!onex && !apply_M()) {
             good = false;
             break;
         }
@@ -601,13 +651,14 @@ __global__ __launch_bounds__(PTH) void pcg_kernel(PcgArgs a) {
 
 int pcg_nv(int n) { return n < 256 ? 256 : (n + 3) / 4 * 4; }  // (>= 256: the norm tree of the retraction)
 int pcg_r4(int R) { return (R + 1 + 3) / 4 * 4; }
-size_t pcg_lds_bytes(int n, int R, int nitem) {
+size_t pcg_lds_bytes(int n, int R, int nitem, bool onex) {
     return sizeof(double) * ((size_t)pcg_nv(n) + 16 + 8 * (size_t)nitem) + sizeof(int) * (2 * (size_t)nitem + pcg_r4(R) + 4) +
-           sizeof(float) * (size_t)R * n;
+           sizeof(float) * (size_t)R * n * (onex ? 2 : 1);
 }
 
 hipError_t launch_pcg(hipStream_t st, const PcgArgs& a) {
-    const size_t lds = pcg_lds_bytes(a.n, a.R, a.nitem);
+    const size_t lds = pcg_lds_bytes(a.n, a.R, a.nitem, a.onex != 0);
+    if (a.onex && a.R > kPcgMaxR) return hipErrorInvalidValue;
     static bool attr = false;  // (one function, one attribute: the maximum the kernel may ask for)
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)pcg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

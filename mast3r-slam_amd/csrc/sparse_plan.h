@@ -30,9 +30,12 @@ struct SparsePlan {
     bool core_df = true;      // hybrid: the core by chol_df (else in registers); the planner's choice
     // PCG iterations (gn_pcg.hip; set by the driver): M's rows per workgroup, workgroups, X's
     // leading dimension, the vector stride; device: X (n x ldx f64) and the exchange granules
-    bool pcg = false;
+    bool pcg = false, pcg_onex = false;
     int pcg_R = 0, pcg_nwg = 0, pcg_ldx = 0, pcg_ldt = 0, pcg_nv = 0, pcg_nitem = 0;
     size_t o_pcgx = 0, o_pcgxt = 0, o_gran = 0;
+    // the factor the first inverse reads, copied out of the live one (Lstore .. Linv) when M comes
+    // from an earlier iteration than the one before the first PCG (gn_driver.hip pcg_lag)
+    size_t o_snap = 0, snap_bytes = 0;
     int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
     std::vector<SpRound> rounds;
     std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
