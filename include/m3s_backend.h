@@ -125,9 +125,10 @@ int m3s_match_iterative_proj(const float* X11, const float* X21, const float* D1
  * flags at the end (one extra synchronisation); out4 = {early exit, pivot failure, packed stream,
  * ray-constrained calib accumulate (Xj read as its depth)} of the last such call. */
 void m3s_gn_debug_flags(int* out4);
-/* The same call's lagged-factor PCG: out4 = {PCG solves, their CG steps in all,
- * PCG solves that fell back to the direct factorisation, 1 if the call planned PCG iterations}. */
-void m3s_gn_pcg_stats(int* out4);
+/* The same call's lagged-factor PCG: out5 = {PCG solves, their CG steps in all,
+ * PCG solves that fell back to the direct factorisation, 1 if the call planned PCG iterations,
+ * the first PCG iteration (0 if none planned)}. */
+void m3s_gn_pcg_stats(int* out5);
 
 /* Deferred error report.  A GN call whose solver has bounded device-side waits (the dataflow
  * factorisation) exports its timeout flag without a host wait.  A call whose wait timed out

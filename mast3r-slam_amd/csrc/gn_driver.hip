@@ -80,7 +80,7 @@ std::vector<double> g_prof_solve_ms;   // the last phase session: each iteration
 }  // namespace
 
 int g_dbg_flags[4] = {0, 0, 0, 0};  // done, fail, packed, ray-constrained accumulate (last call)
-int g_dbg_pcg[4] = {0, 0, 0, 0};    // PCG solves, their CG steps, fallbacks, PCG planned (last call)
+int g_dbg_pcg[5] = {0, 0, 0, 0, 0};  // PCG solves, their CG steps, fallbacks, PCG planned, first PCG iteration (last call)
 
 void set_error(const char* fmt, ...) {
     char buf[1024];
@@ -688,8 +688,6 @@ bool hyb_core_fits(const SparsePlan& p) {
     return hyb_core_df() ? p.ntail <= kHybDfTailMax : p.fused_tail;
 }
 
-int pcg_lag();
-
 int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -710,7 +708,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
     if (sp.pcg) {
         sp.snap_bytes = 0;
-        if (pcg_lag() >= 2) {
+        if (sp.pcg_lag >= 2) {
             sp.snap_bytes = (sp.npad_tail > 0 ? sp.o_linv + chol_linv_bytes(sp.npad_tail) : sp.o_xd) - sp.o_L;
             sp.o_snap = take(sp.snap_bytes);
         }
@@ -1414,39 +1412,42 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c, bool fallback = false) {
 }
 
 // ---- the lagged-factor PCG (gn_pcg.hip) ----
-// From iteration M3S_PCG_FROM (default 3) on, the step may be solved by CG
-// preconditioned with the inverse of iteration (M3S_PCG_FROM - M3S_PCG_LAG)'s system, which that
-// iteration's direct factorisation provides (sp_inverse_kernel); the direct solve stays enqueued
-// behind every PCG launch as its fallback and returns at once when the PCG converged.  Plans whose
-// factor the inverse reads: elimination rounds by sp_round_kernel and a chol_df core (the hybrid
-// with M3S_HYB_CORE=1, the multi plan); not the single-workgroup solve, the reference-order mode,
-// the all-rounds launch or the dense solver.
-int pcg_from() {
-    static const int v = std::max(1, env_int("M3S_PCG_FROM", 3));
-    return v;
+// From iteration `from` on, the step may be solved by CG preconditioned with the inverse of
+// iteration (from - lag)'s system, which that iteration's direct factorisation provides
+// (sp_inverse_kernel); the direct solve stays enqueued behind every PCG launch as its fallback and
+// returns at once when the PCG converged.  Plans whose factor the inverse reads: elimination
+// rounds by sp_round_kernel and a chol_df core (the hybrid with M3S_HYB_CORE=1, the multi plan);
+// not the single-workgroup solve, the reference-order mode, the all-rounds launch or the dense
+// solver.
+//   from (M3S_PCG_FROM, default by the core's size): 3 when the direct solve's dense core has >= 8
+//     tile columns -- its factorisation chain (~14 us per column on one CU) is what the iteration
+//     waits for, and M = A_1^-1 takes 4 CG steps (cfg4: solve 0.27 -> 0.09 ms); 4 below that --
+//     the direct solve is short (cfg3, 4 columns: 0.116 ms) and the 8 direct launches behind a
+//     PCG (its fallback, ~4-5 us each even when they return at once) leave room only for M =
+//     A_2^-1's 4 steps (0.077 ms), not A_1^-1's 6 (0.094 ms: no net gain).
+//   lag (M3S_PCG_LAG, default 2): with lag 1 the inverse (~0.75 ms alone on cfg4, ~2.7 ms beside an
+//     accumulate that fills the chip: rocprofv3 trace r06_l) runs over one accumulate and the
+//     first PCG waits ~0.7 ms for it; with lag 2 it has an accumulate, a direct solve and
+//     another accumulate, and reads a copy of that iteration's factor (the next direct solve
+//     overwrites the live one).  Refreshes after a PCG that fell back use lag 1 (the next PCG
+//     waits for them).
+int pcg_from_for(int tiles) {
+    const int v = env_int("M3S_PCG_FROM", 0);
+    return v > 0 ? v : (tiles >= 8 ? 3 : 4);
 }
-// M3S_PCG_LAG (default 2): M is the inverse of iteration (M3S_PCG_FROM - lag)'s system.  With
-// lag 1 the inverse (~0.75 ms alone on cfg4, ~2.7 ms beside an accumulate that fills the chip:
-// rocprofv3 trace r06_l) runs over one accumulate and the first PCG waits ~0.7 ms for it; with
-// lag 2 it has an accumulate, a direct solve and another accumulate, and reads a copy of that
-// iteration's factor (the next direct solve overwrites the live one).  Refreshes after a PCG
-// that fell back use lag 1 (the next PCG waits for them).
-int pcg_lag() {
-    static const int v = std::max(1, std::min(pcg_from(), env_int("M3S_PCG_LAG", 2)));
-    return v;
-}
-// M3S_GN_PCG: 0 off; 1 (default) when the direct solve's dense core has >= M3S_PCG_MIN_TILES (8)
-// tile columns -- its factorisation chain (~14 us per column on one CU) is then what the
-// iteration waits for; with fewer, the chain is short and the direct launches behind the PCG
-// (its fallback: each costs ~5 us even when it returns at once, rocprofv3 trace) eat the gain
-// (cfg3: 4 tile columns) -- 2 always.
+int pcg_lag_for(int from) { return std::max(1, std::min(from, env_int("M3S_PCG_LAG", 2))); }
+// M3S_GN_PCG: 0 off; 1 (default) on every plan above whose core has >= M3S_PCG_MIN_TILES (1) tile
+// columns; 2 always.
 void choose_pcg(const m3s_gn_args& a, const Ctx& c, const Plan& plan, int npose, SparsePlan& sp) {
     sp.pcg = false;
     const int n = 7 * npose;
     const int mode = env_int("M3S_GN_PCG", 1);
-    const int min_tiles = env_int("M3S_PCG_MIN_TILES", 8);
-    if (mode == 0 || (mode == 1 && sp.npad_tail / kCholTile < min_tiles) || c.ref_order || !sp.enabled ||
-        sp.fused || (sp.hybrid && !sp.core_df) || env_int("M3S_SOLVE_COOP", 0) != 0 || a.max_iter <= pcg_from() ||
+    const int min_tiles = env_int("M3S_PCG_MIN_TILES", 1);
+    const int tiles = sp.npad_tail / kCholTile;
+    sp.pcg_from = pcg_from_for(tiles);
+    sp.pcg_lag = pcg_lag_for(sp.pcg_from);
+    if (mode == 0 || (mode == 1 && tiles < min_tiles) || c.ref_order || !sp.enabled || sp.fused ||
+        (sp.hybrid && !sp.core_df) || env_int("M3S_SOLVE_COOP", 0) != 0 || a.max_iter <= sp.pcg_from ||
         n > kPcgMaxN || n < 7)
         return;
     // rows of M per workgroup: 12 or 24, the smaller one giving <= M3S_PCG_WG
@@ -1809,7 +1810,8 @@ int run(const m3s_gn_args& a) {
         g_prof.mark(c.st);
         // the poses the call started from, so that a timed-out call can restore them (below)
         if (itr == 0) M3S_HIP_CHECK(launch_twc_save(c.st, a.Twc, c.at<float>(L.twc_save), (int)(8 * a.N)));
-        if (c.sp.pcg && itr >= pcg_from()) {  // the direct solve below is its fallback
+        const int from = c.sp.pcg_from, lag = c.sp.pcg_lag;
+        if (c.sp.pcg && itr >= from) {  // the direct solve below is its fallback
             if (c.inv_pending) {  // M's refresh (side stream) must be complete
                 M3S_HIP_CHECK(hipStreamWaitEvent(c.st, c.inv_done, 0));
                 c.inv_pending = false;
@@ -1817,7 +1819,7 @@ int run(const m3s_gn_args& a) {
             rc = enqueue_pcg(a, c);
             if (rc) return rc;
         }
-        rc = enqueue_solve(a, c, c.sp.pcg && itr >= pcg_from());
+        rc = enqueue_solve(a, c, c.sp.pcg && itr >= from);
         if (rc) return rc;
         g_prof.mark(c.st);
         if (!c.sp.fused && !c.sp.hybrid)  // gn_solve retracts inside its launch
@@ -1826,8 +1828,8 @@ int run(const m3s_gn_args& a) {
         // M from this iteration's factor: iteration M3S_PCG_FROM - M3S_PCG_LAG's (a copy of it
         // when the lag is 2 or more), then after every PCG that fell back to the direct solve
         // (sp_inverse_kernel returns at once when this iteration's PCG converged: M stays)
-        if (c.sp.pcg && (itr == pcg_from() - pcg_lag() || itr >= pcg_from()) && itr + 1 < a.max_iter) {
-            rc = enqueue_inverse(a, c, itr < pcg_from() - 1);
+        if (c.sp.pcg && (itr == from - lag || itr >= from) && itr + 1 < a.max_iter) {
+            rc = enqueue_inverse(a, c, itr < from - 1);
             if (rc) return rc;
         }
         g_prof.mark(c.st);
@@ -1888,6 +1890,7 @@ int run(const m3s_gn_args& a) {
         g_dbg_pcg[1] = hf[kFlagPcgSteps];
         g_dbg_pcg[2] = hf[kFlagPcgFall];
         g_dbg_pcg[3] = c.sp.pcg ? 1 : 0;
+        g_dbg_pcg[4] = c.sp.pcg ? c.sp.pcg_from : 0;
         if (dbg != 2)
             fprintf(stderr, "gn flags: done %d fail %d not_ray %d timeout %d packed %d pcg runs %d steps %d fallbacks %d\n",
                     hf[kFlagDone], hf[kFlagFail], hf[kFlagNotRay], hf[kFlagTimeout], (int)c.packed,
@@ -1916,8 +1919,8 @@ extern "C" void m3s_gn_debug_flags(int* out4) {
     for (int k = 0; k < 4; k++) out4[k] = m3s::g_dbg_flags[k];
 }
 
-extern "C" void m3s_gn_pcg_stats(int* out4) {
-    for (int k = 0; k < 4; k++) out4[k] = m3s::g_dbg_pcg[k];
+extern "C" void m3s_gn_pcg_stats(int* out5) {
+    for (int k = 0; k < 5; k++) out5[k] = m3s::g_dbg_pcg[k];
 }
 
 extern "C" const char* m3s_version(void) { return "m3s 0.1.0 gfx950"; }

@@ -31,6 +31,7 @@ struct SparsePlan {
     // PCG iterations (gn_pcg.hip; set by the driver): M's rows per workgroup, workgroups, X's
     // leading dimension, the vector stride; device: X (n x ldx f64) and the exchange granules
     bool pcg = false, pcg_onex = false;
+    int pcg_from = 0, pcg_lag = 0;  // first PCG iteration; M from iteration pcg_from - pcg_lag
     int pcg_R = 0, pcg_nwg = 0, pcg_ldx = 0, pcg_ldt = 0, pcg_nv = 0, pcg_nitem = 0;
     size_t o_pcgx = 0, o_pcgxt = 0, o_gran = 0;
     // the factor the first inverse reads, copied out of the live one (Lstore .. Linv) when M comes

@@ -681,10 +681,11 @@ def gn_debug_flags() -> dict:
     (include/m3s_backend.h m3s_gn_debug_flags / m3s_gn_pcg_stats)."""
     f = (ctypes.c_int * 4)()
     lib.m3s_gn_debug_flags(f)
-    q = (ctypes.c_int * 4)()
+    q = (ctypes.c_int * 5)()
     lib.m3s_gn_pcg_stats(q)
     return {"done": f[0], "fail": f[1], "packed": bool(f[2]), "ray_constrained": bool(f[3]),
-            "pcg_planned": bool(q[3]), "pcg_runs": q[0], "pcg_steps": q[1], "pcg_fallbacks": q[2]}
+            "pcg_planned": bool(q[3]), "pcg_runs": q[0], "pcg_steps": q[1], "pcg_fallbacks": q[2],
+            "pcg_from": q[4]}
 
 
 def version() -> str:

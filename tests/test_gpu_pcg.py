@@ -20,7 +20,9 @@ from tests.test_gpu_gn import _rel, _run_gpu, _run_oracle
 
 pytestmark = pytest.mark.gpu
 
-PCG_FROM = 3  # gn_driver.hip pcg_from(): iterations 0-2 direct, M from iteration 1's factor
+# gn_driver.hip pcg_from_for: the first PCG iteration -- 3 on cores of >= 8 tile columns (cfg4's
+# multi plan, 14), 4 below (cfg3's hybrid core, 4); M from two iterations earlier
+PCG_FROM = {"cfg3": 4, "cfg4": 3}
 
 
 def _graph(cfg, H, W, seed=None):
@@ -48,8 +50,8 @@ def _run(backend, monkeypatch, g, mode, iters, **env):
 
 @pytest.mark.parametrize("cfg,H,W", [("cfg3", 96, 128), ("cfg4", 48, 64)])
 def test_pcg_runs_and_matches_the_direct_solve(backend, monkeypatch, cfg, H, W):
-    """Both bench topologies (cfg3: the hybrid plan; cfg4: the multi plan), 10 iterations: seven
-    PCG solves, none falling back; poses within 1e-6 of the direct solve's (the CG stop is
+    """Both bench topologies (cfg3: the hybrid plan; cfg4: the multi plan), 10 iterations: six /
+    seven PCG solves, none falling back; poses within 1e-6 of the direct solve's (the CG stop is
     sqrt(r'z / r0'z0) <= 1e-6) and bitwise reproducible."""
     mode = synth.CONFIGS[cfg]["mode"]
     g = _graph(cfg, H, W)
@@ -57,8 +59,9 @@ def test_pcg_runs_and_matches_the_direct_solve(backend, monkeypatch, cfg, H, W):
     assert not st_d["pcg_planned"] and st_d["pcg_runs"] == 0
     T_p, dx_p, st = _run(backend, monkeypatch, g, mode, 10)
     print(cfg, st)
-    assert st["pcg_planned"] and st["pcg_runs"] == 10 - PCG_FROM and st["pcg_fallbacks"] == 0, st
-    assert 10 - PCG_FROM <= st["pcg_steps"] <= (10 - PCG_FROM) * 30, st
+    k = PCG_FROM[cfg]
+    assert st["pcg_planned"] and st["pcg_from"] == k and st["pcg_runs"] == 10 - k and st["pcg_fallbacks"] == 0, st
+    assert 10 - k <= st["pcg_steps"] <= (10 - k) * 30, st
     assert np.isfinite(T_p).all()
     assert _rel(T_p, T_d) < 1e-6, _rel(T_p, T_d)
     T_p2, dx_p2, _ = _run(backend, monkeypatch, g, mode, 10)
@@ -95,7 +98,7 @@ def test_pcg_fallback_is_bitwise_the_direct_solve(backend, monkeypatch):
         r = subprocess.run([sys.executable, "-c", code, out], env=env, capture_output=True, text=True, timeout=240,
                            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         assert r.returncode == 0, r.stderr[-2000:]
-        n = 6 - PCG_FROM
+        n = 6 - PCG_FROM["cfg3"]
         assert f"'pcg_runs': {n}" in r.stdout and f"'pcg_fallbacks': {n}" in r.stdout, r.stdout
         T_f = np.load(out)
     assert np.array_equal(T_f, T_d)
@@ -103,13 +106,13 @@ def test_pcg_fallback_is_bitwise_the_direct_solve(backend, monkeypatch):
 
 @pytest.mark.parametrize("cfg,H,W", [("cfg3", 384, 512), ("cfg4", 384, 512)])
 def test_pcg_bench_graphs_full_size_within_1e5_of_oracle(backend, oracle, monkeypatch, cfg, H, W):
-    """The timed workloads at full 512x384 (10 iterations, PCG from iteration 3 -- by default on
-    cfg4, whose core has 14 tile columns; forced on cfg3's 4): within north_star's 1e-5 of the CPU
-    oracle."""
+    """The timed workloads at full 512x384 (10 iterations, the default policy: PCG from iteration
+    3 on cfg4, whose core has 14 tile columns, from 4 on cfg3's 4): within north_star's 1e-5 of
+    the CPU oracle."""
     mode = synth.CONFIGS[cfg]["mode"]
     g = _graph(cfg, H, W)
-    T_p, _, st = _run(backend, monkeypatch, g, mode, 10, M3S_GN_PCG=1 if cfg == "cfg4" else 2)
-    assert st["pcg_runs"] == 10 - PCG_FROM and st["pcg_fallbacks"] == 0, st
+    T_p, _, st = _run(backend, monkeypatch, g, mode, 10, M3S_GN_PCG=1)
+    assert st["pcg_runs"] == 10 - PCG_FROM[cfg] and st["pcg_fallbacks"] == 0, st
     T_o, _, _ = _run_oracle(oracle, g, mode, 10)
     d = _rel(T_p, T_o)
     print(cfg, "pcg vs oracle", d, st)
