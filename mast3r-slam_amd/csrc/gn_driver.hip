@@ -706,6 +706,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
         sp.o_linv = take(chol_linv_bytes(sp.npad_tail));
     }
     sp.o_Lg = take(sp.fused_tail ? sizeof(double) * 49 * (size_t)sp.ntail * sp.ntail : 0);
+    sp.o_dfcnt = take(sizeof(int) * (size_t)sp_rounds_df_words((int)sp.rounds.size()));
     if (sp.pcg) {
         sp.snap_bytes = 0;
         if (sp.pcg_lag >= 2) {
@@ -738,6 +739,7 @@ int upload_sparse_plan(SparsePlan& sp, int npose, hipStream_t st) {
     }
     sp.o_int = take(sizeof(int) * std::max<size_t>(n, 1));
     M3S_HIP_CHECK(hipMallocAsync((void**)&sp.dbuf, off, st));
+    M3S_HIP_CHECK(hipMemsetAsync(sp.dbuf + sp.o_dfcnt, 0, sizeof(int) * (size_t)sp_rounds_df_words((int)sp.rounds.size()), st));
     if (sp.npad_tail > 0)  // the dataflow factor's ready words start below every epoch
         M3S_HIP_CHECK(hipMemsetAsync(chol_ready_ptr(sp.dptr<double>(sp.o_linv), sp.npad_tail), 0,
                                      chol_ready_bytes(sp.npad_tail), st));
@@ -1326,7 +1328,12 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c, bool fallback = false) {
     // hybrid core's fill) as the one all-rounds launch -- slower when it runs, but a converged
     // PCG skips one launch instead of one per round (cfg3: 5 round launches + the fill)
     static const bool fb_coop = env_int("M3S_PCG_FALLBACK_COOP", 0) != 0;
-    const bool coop = coop_mode != 0 || (fallback && fb_coop);
+    // M3S_SOLVE_DF: 1 (default) = a PCG iteration's fallback runs its rounds (and the hybrid core's
+    // fill) as ONE plain launch of ticketed targets (sp_rounds_df_kernel: no co-residency); 2 =
+    // every direct solve does; 0 = one launch per round everywhere
+    static const int df_mode = env_int("M3S_SOLVE_DF", 1);
+    const bool df = coop_mode == 0 && !(fallback && fb_coop) && (df_mode == 2 || (df_mode == 1 && fallback));
+    const bool coop = coop_mode != 0 || (fallback && fb_coop) || df;
     if (coop) {
         c.may_timeout = true;  // grid barriers
         SpCoopArgs ca{};
@@ -1347,7 +1354,10 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c, bool fallback = false) {
         ca.ntail = sp.hybrid ? sp.ntail : 0;
         ca.npad = sp.npad_tail;
         ca.coop = coop_mode == 2;
-        M3S_HIP_CHECK(launch_sp_rounds_coop(c.st, ca));
+        if (df)
+            M3S_HIP_CHECK(launch_sp_rounds_df(c.st, ca, sp.dptr<int>(sp.o_dfcnt)));
+        else
+            M3S_HIP_CHECK(launch_sp_rounds_coop(c.st, ca));
     } else {
         for (const SpRound& R : sp.rounds)
             M3S_HIP_CHECK(launch_sp_round(c.st, sp.iptr(sp.i_inl), R.tbeg + R.rbeg, R.nbt, R.nrt,

@@ -185,6 +185,13 @@ struct SpCoopArgs {
     int coop;  // 1: cooperative-groups grid sync; 0: own barrier (both as a cooperative launch)
 };
 hipError_t launch_sp_rounds_coop(hipStream_t st, const SpCoopArgs& args);
+// The same rounds (and the hybrid core's fill) in one PLAIN launch without co-residency: the
+// workgroups claim (round, target) tickets in order from a counter and a target waits for the
+// previous round's completion count -- only ever on tickets running workgroups already hold.
+// cnt: 4 + nrounds ints zeroed once (ticket, exits, spare, spare, per-round done counts); the last
+// workgroup out re-zeroes them.  (gn_sparse.hip sp_rounds_df_kernel)
+hipError_t launch_sp_rounds_df(hipStream_t st, const SpCoopArgs& args, int* cnt);
+inline int sp_rounds_df_words(int nrounds) { return (4 + nrounds + 31) / 32 * 32; }
 hipError_t launch_sp_round(hipStream_t st, const int* inl, int ibeg, int nbt, int nrt, const int* tc3,
                            const int* rc4, double* A, double* b, double* Lstore, double* W, double* y,
                            int* flags);

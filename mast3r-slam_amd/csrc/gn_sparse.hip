@@ -24,7 +24,9 @@
 #include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "block7.h"
 #include "gn_kernels.h"
@@ -212,14 +214,20 @@ __global__ __launch_bounds__(64) void sp_back_kernel(
 
 // Dense core: Hd [npad + 64, npad] from the blocks of the ntail remaining poses (tmap:
 // ntail x ntail -> 2*block + transposed, or -1), RHS border row from b.
+// (entries first, first + step, ... below end; end < 0: the whole matrix)
 template <bool COH>
 __device__ __forceinline__ void sp_tail_fill(const double* __restrict__ A, const double* __restrict__ b,
                                              const int* __restrict__ tmap, const int* __restrict__ tail,
-                                             int ntail, int npad, double* __restrict__ Hd) {
+                                             int ntail, int npad, double* __restrict__ Hd,
+                                             int64_t first = -1, int64_t step = 0, int64_t end = -1) {
     const int n = ntail * 7;
-    const int64_t total = (int64_t)(npad + kCholTile) * npad;
-    for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
-         id += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t whole = (int64_t)(npad + kCholTile) * npad;
+    const int64_t total = end < 0 ? whole : (end < whole ? end : whole);
+    if (first < 0) {
+        first = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        step = (int64_t)gridDim.x * blockDim.x;
+    }
+    for (int64_t id = first; id < total; id += step) {
         const int r = (int)(id / npad), c = (int)(id % npad);
         double val;
         if (r > npad) {
@@ -317,6 +325,88 @@ __global__ __launch_bounds__(64) void sp_rounds_coop_kernel(SpCoopArgs a) {
     if (a.ntail > 0 && a.Hd) sp_tail_fill<true>(a.A, a.b, a.tmap, a.tail, a.ntail, a.npad, a.Hd);
 }
 
+// The rounds without a grid barrier or co-residency (launch_sp_rounds_df, gn_kernels.h): the
+// (round, target) pairs are tickets in round order, then the core fill in chunks of kDfFill
+// entries; a workgroup claims the next ticket, waits (one lane, bounded) for the previous round's
+// done count (the fill: the last round's), runs it with the coherent block accesses of the
+// all-rounds launch and bumps its round's count after its stores landed.  Every wait is on tickets
+// that running workgroups hold, so any resident subset progresses; a workgroup's target does not
+// change the arithmetic (bitwise the per-round launches).
+constexpr int kDfFill = 4096;
+__global__ __launch_bounds__(64) void sp_rounds_df_kernel(SpCoopArgs a, int* __restrict__ cnt) {
+    __shared__ double sR[kGroups][7 * kLd];
+    __shared__ double sS[kGroups][7 * kLd];
+    __shared__ int s_tk;
+    __shared__ int s_bad;
+    if (solve_skipped(a.flags)) return;  // (read once: written by earlier launches; all leave or none)
+    const int tid = threadIdx.x;
+    int total = 0;
+    for (int rd = 0; rd < a.nrounds; rd++) total += a.rounds[8 * rd + 3] + a.rounds[8 * rd + 5];
+    const int nround_tk = total;
+    const bool fill = a.ntail > 0 && a.Hd;
+    const int64_t fill_n = fill ? (int64_t)(a.npad + kCholTile) * a.npad : 0;
+    total += (int)((fill_n + kDfFill - 1) / kDfFill);
+    int* done = cnt + 4;
+    if (tid == 0) s_bad = 0;
+    for (;;) {
+        __syncthreads();  // (s_tk's previous readers)
+        if (tid == 0) s_tk = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int tk = s_tk;
+        if (tk >= total) break;
+        // the ticket's round (rounds are few: a scan)
+        int rd = 0, base = 0, need_rd = -1, need = 0;
+        if (tk < nround_tk) {
+            while (tk >= base + a.rounds[8 * rd + 3] + a.rounds[8 * rd + 5]) {
+                base += a.rounds[8 * rd + 3] + a.rounds[8 * rd + 5];
+                rd++;
+            }
+            if (rd > 0) {
+                need_rd = rd - 1;
+                need = a.rounds[8 * need_rd + 3] + a.rounds[8 * need_rd + 5];
+            }
+        } else if (a.nrounds > 0) {
+            need_rd = a.nrounds - 1;
+            need = a.rounds[8 * need_rd + 3] + a.rounds[8 * need_rd + 5];
+        }
+        if (need_rd >= 0 && tid == 0) {
+            int spins = 0;
+            while (__hip_atomic_load(done + need_rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1 << 22)) {
+                    __hip_atomic_store(a.flags + kFlagTimeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(a.flags + kFlagFail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_bad = 1;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_bad) continue;  // (a timed-out wait: drain the remaining tickets without work)
+        if (tk < nround_tk) {
+            const int* R = a.rounds + 8 * rd;  // node_begin, nnodes, tbeg, nbt, rbeg, nrt, wbeg, wcount
+            const int t = tk - base;
+            sp_round_target<true>(a.inl + (int64_t)(R[2] + R[4] + t) * kSpRec, t < R[3], a.tc3, a.rc4, nullptr,
+                                  a.A, a.b, a.Lstore, a.W, a.y, a.flags, sR, sS);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this target's write-through stores landed
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add(done + rd, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const int64_t f0 = (int64_t)(tk - nround_tk) * kDfFill;
+            sp_tail_fill<true>(a.A, a.b, a.tmap, a.tail, a.ntail, a.npad, a.Hd, f0 + tid, 64, f0 + kDfFill);
+        }
+    }
+    // the last workgroup out re-zeroes the counters for the next launch
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == (int)gridDim.x - 1) {
+            for (int k = 0; k < a.nrounds; k++) __hip_atomic_store(done + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void sp_tail_scatter_kernel(const double* __restrict__ xd,
                                                               const int* __restrict__ tail,
                                                               int ntail, double* __restrict__ x,
@@ -354,6 +444,22 @@ hipError_t launch_sp_rounds_coop(hipStream_t st, const SpCoopArgs& args) {
     SpCoopArgs a = args;
     void* kargs[] = {&a};
     return hipLaunchCooperativeKernel((const void*)sp_rounds_coop_kernel, dim3(grid), dim3(64), kargs, 0, st);
+}
+
+hipError_t launch_sp_rounds_df(hipStream_t st, const SpCoopArgs& args, int* cnt) {
+    if (args.nrounds <= 0 && (args.ntail <= 0 || !args.Hd)) return hipSuccess;
+    // one 64-thread workgroup per CU at most (M3S_SOLVE_DF_WG): the widest round has ~500 targets
+    static int grid = 0;
+    if (grid == 0) {
+        int dev = 0, ncu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        const char* s = getenv("M3S_SOLVE_DF_WG");
+        grid = std::max(1, s ? atoi(s) : ncu);
+    }
+    hipLaunchKernelGGL(sp_rounds_df_kernel, dim3(grid), dim3(64), 0, st, args, cnt);
+    return hipGetLastError();
 }
 
 hipError_t launch_sp_back(hipStream_t st, int nnodes, const int* nodes, const int* fptr,

@@ -37,6 +37,7 @@ struct SparsePlan {
     // the factor the first inverse reads, copied out of the live one (Lstore .. Linv) when M comes
     // from an earlier iteration than the one before the first PCG (gn_driver.hip pcg_lag)
     size_t o_snap = 0, snap_bytes = 0;
+    size_t o_dfcnt = 0;  // the ticketed all-rounds launch's counters (sp_rounds_df_words ints)
     int nblocks = 0, nW = 0, ntail = 0, npad_tail = 0, zero_blk = 0;
     std::vector<SpRound> rounds;
     std::vector<int> nodes, fptr, fronts, tg, tc, rtg, rc, tail, tmap;
