@@ -1348,10 +1348,11 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c, bool fallback = false) {
         ca.Lstore = Ls;
         ca.W = W;
         ca.y = y;
-        ca.Hd = sp.hybrid && sp.ntail > 0 ? sp.dptr<double>(sp.o_dense) : nullptr;
+        // (the ticketed launch fills the multi plan's core too: one launch less behind a PCG)
+        ca.Hd = (sp.hybrid || df) && sp.ntail > 0 ? sp.dptr<double>(sp.o_dense) : nullptr;
         ca.flags = flags;
         ca.nrounds = (int)sp.rounds.size();
-        ca.ntail = sp.hybrid ? sp.ntail : 0;
+        ca.ntail = (sp.hybrid || df) ? sp.ntail : 0;
         ca.npad = sp.npad_tail;
         ca.coop = coop_mode == 2;
         if (df)
@@ -1414,7 +1415,7 @@ int enqueue_solve(const m3s_gn_args& a, Ctx& c, bool fallback = false) {
     if (sp.ntail > 0) c.may_timeout = true;  // the core's dataflow factorisation (chol_df)
     M3S_HIP_CHECK(launch_sp_tail(c.st, A, b, sp.iptr(sp.i_tmap), sp.iptr(sp.i_tail), sp.ntail,
                                  sp.npad_tail, sp.dptr<double>(sp.o_dense), sp.dptr<double>(sp.o_linv),
-                                 sp.dptr<double>(sp.o_xd), x, flags, ++c.chol_epoch));
+                                 sp.dptr<double>(sp.o_xd), x, flags, ++c.chol_epoch, !df));
     for (auto it = sp.rounds.rbegin(); it != sp.rounds.rend(); ++it)
         M3S_HIP_CHECK(launch_sp_back(c.st, it->nnodes, sp.iptr(sp.i_nodes), sp.iptr(sp.i_fptr),
                                      sp.iptr(sp.i_fronts), it->node_begin, Ls, W, y, x, flags));

@@ -202,7 +202,7 @@ hipError_t launch_sp_tail_fill(hipStream_t st, const double* A, const double* b,
                                const int* tail, int ntail, int npad, double* Hd, const int* flags);
 hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, const int* tmap,
                           const int* tail, int ntail, int npad, double* Hd, double* Linv,
-                          double* xd, double* x, int* flags, int epoch);
+                          double* xd, double* x, int* flags, int epoch, bool fill = true);
 hipError_t launch_fill_only(hipStream_t st, const double* compact, const int* slotmap, int nblk,
                             int npose, int n, int npad, double* Hd, const int* flags);
 // The lagged-factor PCG (gn_pcg.hip).  X = A^-1 from the last direct solve's factor (the

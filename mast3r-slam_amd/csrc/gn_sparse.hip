@@ -495,9 +495,9 @@ hipError_t launch_sp_tail_scatter(hipStream_t st, const double* xd, const int* t
 // measured slower: 0.177 vs 0.156 ms per cfg3 solve, r04_u.)
 hipError_t launch_sp_tail(hipStream_t st, const double* A, const double* b, const int* tmap,
                           const int* tail, int ntail, int npad, double* Hd, double* Linv,
-                          double* xd, double* x, int* flags, int epoch) {
+                          double* xd, double* x, int* flags, int epoch, bool fill) {
     if (ntail <= 0) return hipSuccess;
-    hipError_t e = launch_sp_tail_fill(st, A, b, tmap, tail, ntail, npad, Hd, flags);
+    hipError_t e = fill ? launch_sp_tail_fill(st, A, b, tmap, tail, ntail, npad, Hd, flags) : hipSuccess;
     if (e != hipSuccess) return e;
     const DfScatter g{tail, ntail, x};
     return launch_dense_factor_solve(st, npad, Hd, Linv, xd, flags, epoch, &g);
