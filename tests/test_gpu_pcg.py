@@ -129,3 +129,22 @@ def test_pcg_singular_system_keeps_dx_zero(backend, monkeypatch):
     assert np.array_equal(T, g.Twc.numpy())
     assert dx is None or not np.any(dx)
     assert st["pcg_runs"] == st["pcg_fallbacks"], st
+
+
+@pytest.mark.parametrize("nblocks", [128, 256])
+def test_pcg_with_cus_held_by_another_stream(backend, monkeypatch, nblocks):
+    """another stream's workgroups hold 64 KiB of LDS on about half / all of the
+    CUs for 30 ms while a PCG iteration runs (cfg4 topology, PCG from iteration 3): the PCG's
+    130-KiB workgroups start late, the resident ones wait in their first exchange (its bound is
+    seconds, not the 30 ms) -- the call ends with bitwise the unhindered poses, no fallback."""
+    from mast3r_slam_backends import variants
+
+    g = _graph("cfg4", 48, 64)
+    T_ref, dx_ref, st_ref = _run(backend, monkeypatch, g, "rays", 6, M3S_GN_PCG=1)
+    assert st_ref["pcg_runs"] == 6 - PCG_FROM["cfg4"] and st_ref["pcg_fallbacks"] == 0, st_ref
+    side = torch.cuda.Stream()
+    variants.hold_cus(nblocks, 64 * 1024, 30000, side)
+    T_h, dx_h, st = _run(backend, monkeypatch, g, "rays", 6, M3S_GN_PCG=1)
+    torch.cuda.synchronize()
+    assert st["pcg_fallbacks"] == 0, st
+    assert np.array_equal(T_h, T_ref) and np.array_equal(dx_h, dx_ref)
